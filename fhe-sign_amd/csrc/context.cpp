@@ -1,0 +1,402 @@
+// context.cpp -- device context, server-key upload, LUT registry and the PBS driver.
+#include "context.h"
+
+#include <cmath>
+#include <cstring>
+
+#include "kernels.h"
+
+namespace fhe {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+const char* last_error() { return g_err.c_str(); }
+
+void fft_tables(std::vector<double2>* W, std::vector<double2>* psi) {
+    // Same expressions, same evaluation order as oracle/tfhe_oracle.c:fho_tables_init.
+    const double pi = 3.14159265358979323846264338327950288;
+    W->resize(512);
+    psi->resize(1024);
+    for (int k = 0; k < 512; ++k) {
+        double a = 2.0 * pi * (double)k / 1024.0;
+        (*W)[k] = make_double2(std::cos(a), std::sin(a));
+    }
+    (*W)[0] = make_double2(1.0, 0.0);
+    (*W)[256] = make_double2(0.0, 1.0);
+    for (int j = 0; j < 1024; ++j) {
+        double a = pi * (double)j / 2048.0;
+        (*psi)[j] = make_double2(std::cos(a), std::sin(a));
+    }
+    (*psi)[0] = make_double2(1.0, 0.0);
+}
+
+void make_lut_poly(const Params& p, const uint32_t* f, std::vector<uint64_t>* lut) {
+    const uint32_t mods = p.msg_carry();
+    const uint32_t box = kPolySize / mods, half = box / 2;
+    const uint64_t delta = p.delta();
+    std::vector<uint64_t> tmp(kPolySize);
+    for (uint32_t i = 0; i < mods; ++i)
+        for (uint32_t t = 0; t < box; ++t) tmp[i * box + t] = (uint64_t)(f[i] % mods) * delta;
+    for (uint32_t t = 0; t < half; ++t) tmp[t] = 0ull - tmp[t];
+    lut->resize(kPolySize);
+    for (uint32_t j = 0; j < kPolySize; ++j) (*lut)[j] = tmp[(j + half) % kPolySize];
+}
+
+}  // namespace fhe
+
+using namespace fhe;
+
+int fhe_ctx::ensure_ms(size_t count) {
+    if (count <= ms_cap) return FHE_OK;
+    if (d_ms) FHE_HIP_CHECK(hipFree(d_ms));
+    size_t cap = count < 256 ? 256 : count;
+    ms_stride = (int)((p.n + 1 + 7) / 8 * 8);
+    FHE_HIP_CHECK(hipMalloc(&d_ms, cap * ms_stride * sizeof(uint16_t)));
+    ms_cap = cap;
+    return FHE_OK;
+}
+
+int fhe_ctx::ensure_stage(size_t count) {
+    if (count <= stage_cap) return FHE_OK;
+    if (d_stage_in) FHE_HIP_CHECK(hipFree(d_stage_in));
+    if (d_stage_out) FHE_HIP_CHECK(hipFree(d_stage_out));
+    if (d_stage_lut) FHE_HIP_CHECK(hipFree(d_stage_lut));
+    size_t cap = count < 256 ? 256 : count;
+    FHE_HIP_CHECK(hipMalloc(&d_stage_in, cap * kBigCt * 8));
+    FHE_HIP_CHECK(hipMalloc(&d_stage_out, cap * kBigCt * 8));
+    FHE_HIP_CHECK(hipMalloc(&d_stage_lut, cap * 4));
+    stage_cap = cap;
+    return FHE_OK;
+}
+
+int fhe_ctx::register_lut(const uint32_t* table, uint32_t* id) {
+    const uint32_t mods = p.msg_carry();
+    std::vector<uint32_t> key(table, table + mods);
+    for (auto& v : key) v %= mods;
+    auto it = lut_ids.find(key);
+    if (it != lut_ids.end()) {
+        *id = it->second;
+        return FHE_OK;
+    }
+    std::vector<uint64_t> poly;
+    make_lut_poly(p, key.data(), &poly);
+    const uint32_t nid = (uint32_t)lut_ids.size();
+    h_luts.insert(h_luts.end(), poly.begin(), poly.end());
+    lut_ids.emplace(std::move(key), nid);
+    luts_dirty = true;
+    *id = nid;
+    return FHE_OK;
+}
+
+int fhe_ctx::sync_luts() {
+    if (!luts_dirty) return FHE_OK;
+    const size_t nl = h_luts.size() / kPolySize;
+    if (nl > d_luts_cap) {
+        // the stream may still read the old table: order the free behind it
+        if (d_luts) {
+            FHE_HIP_CHECK(hipStreamSynchronize(stream));
+            FHE_HIP_CHECK(hipFree(d_luts));
+        }
+        size_t cap = nl < 64 ? 64 : nl * 2;
+        FHE_HIP_CHECK(hipMalloc(&d_luts, cap * kPolySize * 8));
+        d_luts_cap = cap;
+    }
+    FHE_HIP_CHECK(hipMemcpyAsync(d_luts, h_luts.data(), h_luts.size() * 8, hipMemcpyHostToDevice, stream));
+    luts_dirty = false;
+    return FHE_OK;
+}
+
+int fhe_ctx::pbs_device(const uint64_t* d_in, size_t count, const uint32_t* d_lut, uint64_t* d_out) {
+    if (!has_key) {
+        set_error("no server key installed (fhe_set_server_key)");
+        return FHE_ERR_NO_KEY;
+    }
+    if (count == 0) return FHE_OK;
+    if (count > (size_t)0x7fffffff) {
+        set_error("batch too large");
+        return FHE_ERR_INVALID;
+    }
+    int rc = ensure_ms(count);
+    if (rc) return rc;
+    rc = sync_luts();
+    if (rc) return rc;
+    if (!d_luts) {
+        set_error("no lookup table registered");
+        return FHE_ERR_INVALID;
+    }
+    if (timing) FHE_HIP_CHECK(hipEventRecord(ev[0], stream));
+    FHE_HIP_CHECK(launch_keyswitch(d_in, (int)count, d_ksk, d_ms, ms_stride, (int)p.n, stream));
+    if (timing) FHE_HIP_CHECK(hipEventRecord(ev[1], stream));
+    FHE_HIP_CHECK(launch_blind_rotate(d_ms, ms_stride, d_lut, d_luts, d_bsk, d_W, d_psi, d_out, (int)count,
+                                      (int)p.n, stream));
+    if (timing) {
+        FHE_HIP_CHECK(hipEventRecord(ev[2], stream));
+        FHE_HIP_CHECK(hipEventSynchronize(ev[2]));
+        FHE_HIP_CHECK(hipEventElapsedTime(&last_ks_ms, ev[0], ev[1]));
+        FHE_HIP_CHECK(hipEventElapsedTime(&last_br_ms, ev[1], ev[2]));
+    }
+    return FHE_OK;
+}
+
+// =========================================================================== C ABI (core)
+extern "C" {
+
+const char* fhe_last_error(void) { return fhe::last_error(); }
+
+int fhe_params_default(fhe_params* out) {
+    if (!out) return FHE_ERR_INVALID;
+    *out = Params().to_c();
+    return FHE_OK;
+}
+
+int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** ck, fhe_server_key** sk) {
+    if (!params || !ck || !sk) {
+        set_error("null argument");
+        return FHE_ERR_INVALID;
+    }
+    Params p;
+    const char* why = nullptr;
+    if (!Params::from_c(*params, &p, &why)) {
+        set_error(why);
+        return FHE_ERR_UNSUPPORTED;
+    }
+    try {
+        auto* c = new fhe_client_key();
+        auto* s = new fhe_server_key();
+        generate_keys(p, seed, c, s);
+        *ck = c;
+        *sk = s;
+    } catch (const std::exception& e) {
+        set_error(std::string("keygen failed: ") + e.what());
+        return FHE_ERR_ALLOC;
+    }
+    return FHE_OK;
+}
+
+void fhe_client_key_destroy(fhe_client_key* ck) { delete ck; }
+void fhe_server_key_destroy(fhe_server_key* sk) { delete sk; }
+
+int fhe_client_key_export(const fhe_client_key* ck, uint64_t* lwe_sk, size_t lwe_len, uint64_t* glwe_sk,
+                          size_t glwe_len) {
+    if (!ck || lwe_len < ck->lwe_sk.size() || glwe_len < ck->glwe_sk.size()) {
+        set_error("client key export: buffer too small");
+        return FHE_ERR_INVALID;
+    }
+    std::memcpy(lwe_sk, ck->lwe_sk.data(), ck->lwe_sk.size() * 8);
+    std::memcpy(glwe_sk, ck->glwe_sk.data(), ck->glwe_sk.size() * 8);
+    return FHE_OK;
+}
+
+int fhe_server_key_export(const fhe_server_key* sk, uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len) {
+    if (!sk || ksk_len < sk->ksk.size() || bsk_len < sk->bsk.size()) {
+        set_error("server key export: buffer too small");
+        return FHE_ERR_INVALID;
+    }
+    std::memcpy(ksk, sk->ksk.data(), sk->ksk.size() * 8);
+    std::memcpy(bsk, sk->bsk.data(), sk->bsk.size() * 8);
+    return FHE_OK;
+}
+
+int fhe_client_key_seed_encryption(fhe_client_key* ck, uint64_t seed, uint32_t stream) {
+    if (!ck) return FHE_ERR_INVALID;
+    ck->enc_rng.reset(seed, stream);
+    return FHE_OK;
+}
+
+int fhe_encrypt_block(fhe_client_key* ck, uint64_t value, uint64_t* ct) {
+    if (!ck || !ct) return FHE_ERR_INVALID;
+    if (value >= ck->params.msg_carry()) {
+        set_error("block value out of range");
+        return FHE_ERR_INVALID;
+    }
+    encrypt_big(ck, value * ck->params.delta(), ct);
+    return FHE_OK;
+}
+
+int fhe_decrypt_block(const fhe_client_key* ck, const uint64_t* ct, uint64_t* value) {
+    if (!ck || !ct || !value) return FHE_ERR_INVALID;
+    *value = decode_block(ck->params, decrypt_phase_big(ck, ct));
+    return FHE_OK;
+}
+
+int fhe_ctx_create(int device, fhe_ctx** out) {
+    if (!out) return FHE_ERR_INVALID;
+    int ndev = 0;
+    FHE_HIP_CHECK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) {
+        set_error("no such GPU device (the HIP path has no CPU fallback)");
+        return FHE_ERR_INVALID;
+    }
+    FHE_HIP_CHECK(hipSetDevice(device));
+    auto* c = new fhe_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        set_error(std::string("hipStreamCreate: ") + hipGetErrorString(e));
+        return FHE_ERR_HIP;
+    }
+    for (auto& ev : c->ev) FHE_HIP_CHECK(hipEventCreate(&ev));
+    std::vector<double2> W, psi;
+    fft_tables(&W, &psi);
+    FHE_HIP_CHECK(hipMalloc(&c->d_W, W.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMalloc(&c->d_psi, psi.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMemcpy(c->d_W, W.data(), W.size() * sizeof(double2), hipMemcpyHostToDevice));
+    FHE_HIP_CHECK(hipMemcpy(c->d_psi, psi.data(), psi.size() * sizeof(double2), hipMemcpyHostToDevice));
+    *out = c;
+    return FHE_OK;
+}
+
+void fhe_ctx_destroy(fhe_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void* ptrs[] = {c->d_ksk, c->d_bsk, c->d_W, c->d_psi, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out,
+                    c->d_stage_lut};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
+    if (!c || !sk) return FHE_ERR_INVALID;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    const Params& p = sk->params;
+    if (c->has_key) {
+        FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+        FHE_HIP_CHECK(hipFree(c->d_ksk));
+        FHE_HIP_CHECK(hipFree(c->d_bsk));
+        c->d_ksk = nullptr;
+        c->d_bsk = nullptr;
+        c->has_key = false;
+    }
+    FHE_HIP_CHECK(hipMalloc(&c->d_ksk, sk->ksk.size() * 8));
+    FHE_HIP_CHECK(hipMemcpyAsync(c->d_ksk, sk->ksk.data(), sk->ksk.size() * 8, hipMemcpyHostToDevice, c->stream));
+    const int npoly = (int)(p.n * 4);
+    uint64_t* d_std = nullptr;
+    FHE_HIP_CHECK(hipMalloc(&d_std, sk->bsk.size() * 8));
+    FHE_HIP_CHECK(hipMalloc(&c->d_bsk, (size_t)npoly * 1024 * sizeof(double2)));
+    FHE_HIP_CHECK(hipMemcpyAsync(d_std, sk->bsk.data(), sk->bsk.size() * 8, hipMemcpyHostToDevice, c->stream));
+    FHE_HIP_CHECK(launch_bsk_to_fourier(d_std, npoly, c->d_W, c->d_psi, c->d_bsk, c->stream));
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    FHE_HIP_CHECK(hipFree(d_std));
+    if (!c->has_key || !(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
+        c->lut_ids.clear();
+        c->h_luts.clear();
+        c->luts_dirty = true;
+    }
+    c->p = p;
+    c->has_key = true;
+    return FHE_OK;
+}
+
+int fhe_ctx_export_fourier_bsk(fhe_ctx* c, double* out, size_t len) {
+    if (!c || !c->has_key) return FHE_ERR_NO_KEY;
+    const size_t need = (size_t)c->p.n * 4 * 1024 * 2;
+    if (len < need) {
+        set_error("buffer too small");
+        return FHE_ERR_INVALID;
+    }
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    FHE_HIP_CHECK(hipMemcpy(out, c->d_bsk, need * 8, hipMemcpyDeviceToHost));
+    return FHE_OK;
+}
+
+int fhe_ctx_sync(fhe_ctx* c) {
+    if (!c) return FHE_ERR_INVALID;
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return FHE_OK;
+}
+
+int fhe_lut_register(fhe_ctx* c, const uint32_t* table, uint32_t table_len, uint32_t* id) {
+    if (!c || !table || !id) return FHE_ERR_INVALID;
+    if (!c->has_key) {
+        set_error("install a server key before registering LUTs");
+        return FHE_ERR_NO_KEY;
+    }
+    if (table_len != c->p.msg_carry()) {
+        set_error("LUT table length must equal message_modulus*carry_modulus");
+        return FHE_ERR_INVALID;
+    }
+    return c->register_lut(table, id);
+}
+
+int fhe_pbs_batch(fhe_ctx* c, const uint64_t* in, size_t count, const uint32_t* lut_ids, uint64_t* out) {
+    if (!c || (count && (!in || !lut_ids || !out))) return FHE_ERR_INVALID;
+    if (count == 0) return FHE_OK;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    for (size_t i = 0; i < count; ++i)
+        if (lut_ids[i] >= c->lut_ids.size()) {
+            set_error("unknown LUT id");
+            return FHE_ERR_INVALID;
+        }
+    int rc = c->ensure_stage(count);
+    if (rc) return rc;
+    FHE_HIP_CHECK(hipMemcpyAsync(c->d_stage_in, in, count * kBigCt * 8, hipMemcpyHostToDevice, c->stream));
+    FHE_HIP_CHECK(hipMemcpyAsync(c->d_stage_lut, lut_ids, count * 4, hipMemcpyHostToDevice, c->stream));
+    rc = c->pbs_device(c->d_stage_in, count, c->d_stage_lut, c->d_stage_out);
+    if (rc) return rc;
+    FHE_HIP_CHECK(hipMemcpyAsync(out, c->d_stage_out, count * kBigCt * 8, hipMemcpyDeviceToHost, c->stream));
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return FHE_OK;
+}
+
+int fhe_pbs_batch_device(fhe_ctx* c, const uint64_t* d_in, size_t count, const uint32_t* d_lut, uint64_t* d_out) {
+    if (!c) return FHE_ERR_INVALID;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    return c->pbs_device(d_in, count, d_lut, d_out);
+}
+
+void* fhe_device_alloc(fhe_ctx* c, size_t bytes) {
+    if (!c) return nullptr;
+    if (hipSetDevice(c->device) != hipSuccess) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+        set_error("hipMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+int fhe_device_free(fhe_ctx* c, void* p) {
+    if (!c) return FHE_ERR_INVALID;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    FHE_HIP_CHECK(hipFree(p));
+    return FHE_OK;
+}
+
+int fhe_memcpy_h2d(fhe_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c) return FHE_ERR_INVALID;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    FHE_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return FHE_OK;
+}
+
+int fhe_memcpy_d2h(fhe_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c) return FHE_ERR_INVALID;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    FHE_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return FHE_OK;
+}
+
+int fhe_ctx_enable_timing(fhe_ctx* c, int enable) {
+    if (!c) return FHE_ERR_INVALID;
+    c->timing = enable != 0;
+    return FHE_OK;
+}
+
+int fhe_ctx_last_pbs_timing(fhe_ctx* c, float* ks_ms, float* br_ms) {
+    if (!c) return FHE_ERR_INVALID;
+    if (ks_ms) *ks_ms = c->last_ks_ms;
+    if (br_ms) *br_ms = c->last_br_ms;
+    return FHE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// context.h -- per-thread device context: GPU stream, installed server key, LUT registry,
+// PBS workspace.  The analogue of tfhe-rs's thread-local server key (src/schnorr.rs:443).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "keys.h"
+
+namespace fhe {
+
+void set_error(const std::string& msg);
+#define FHE_HIP_CHECK(expr)                                                                   \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) {                                                               \
+            ::fhe::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));              \
+            return FHE_ERR_HIP;                                                               \
+        }                                                                                     \
+    } while (0)
+
+// Host-side FFT tables (bit-identical to oracle/tfhe_oracle.c:fho_tables_init).
+void fft_tables(std::vector<double2>* W, std::vector<double2>* psi);
+// Accumulator polynomial of a univariate LUT (tfhe shortint box encoding, padding bit).
+void make_lut_poly(const Params& p, const uint32_t* f, std::vector<uint64_t>* lut);
+
+}  // namespace fhe
+
+struct fhe_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool has_key = false;
+    fhe::Params p;
+    uint64_t* d_ksk = nullptr;
+    double2* d_bsk = nullptr;  // Fourier BSK, blind-rotate layout
+    double2* d_W = nullptr;
+    double2* d_psi = nullptr;
+    // LUT registry: table contents -> id, device array of accumulator polynomials
+    std::map<std::vector<uint32_t>, uint32_t> lut_ids;
+    std::vector<uint64_t> h_luts;
+    uint64_t* d_luts = nullptr;
+    size_t d_luts_cap = 0;  // in LUTs
+    bool luts_dirty = false;
+    // PBS workspace
+    uint16_t* d_ms = nullptr;
+    size_t ms_cap = 0;  // ciphertexts
+    int ms_stride = 0;
+    uint64_t* d_stage_in = nullptr;
+    uint64_t* d_stage_out = nullptr;
+    uint32_t* d_stage_lut = nullptr;
+    size_t stage_cap = 0;
+    // timing
+    bool timing = false;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    float last_ks_ms = 0.f, last_br_ms = 0.f;
+
+    int ensure_ms(size_t count);
+    int ensure_stage(size_t count);
+    int sync_luts();
+    int register_lut(const uint32_t* table, uint32_t* id);
+    // KS + BR(+SE) over device arrays, async on `stream`
+    int pbs_device(const uint64_t* d_in, size_t count, const uint32_t* d_lut, uint64_t* d_out);
+};

@@ -1,0 +1,226 @@
+// device_math.h -- CDNA4 (gfx950) device primitives for the PBS pipeline.
+//
+// Arithmetic contract (identical, operation for operation, to oracle/tfhe_oracle.c so that GPU
+// outputs are bit-exact against the CPU restatement):
+//   * complex multiply  y = x*w : y.re = fma(x.re, w.re, -(x.im*w.im)); y.im = fma(x.re, w.im, x.im*w.re)
+//   * forward FFT: radix-2 DIF, natural -> bit-reversed; inverse: radix-2 DIT with conj twiddles
+//   * multiplications by exactly 1 / +-i are done as moves (identical results up to the sign of
+//     zero, which cannot change any nonzero value and converts to torus 0 either way)
+//   * f64 -> torus: rint (v_rndne_f64), then exact mantissa/exponent reconstruction mod 2^64
+// The whole translation unit is compiled with -ffp-contract=off.
+//
+// FFT register layout (one wave64 owns one 1024-point complex FFT, 16 points per lane):
+//   phase A : lane L, reg t (0..15)          holds index L + 64 t          (DIF stages 0-3)
+//   phase B : lane (b = L&15, r = L>>4), u   holds index 64 b + r + 4 u    (DIF stages 4-7)
+//   phase C : lane L, reg R = 4 v + q        holds index 4 (L + 64 v) + q  (DIF stages 8-9)
+// Exchanges A<->B and B<->C go through a per-wave 16 KiB LDS region with XOR swizzles chosen so
+// the ds_read_b128 / ds_write_b128 lane groups hit distinct 16-byte bank slots.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef double2 cplx;
+
+#define FHE_DEV __device__ __forceinline__
+
+FHE_DEV cplx cmul(cplx x, cplx w) {
+    cplx y;
+    y.x = __fma_rn(x.x, w.x, -(x.y * w.y));
+    y.y = __fma_rn(x.x, w.y, x.y * w.x);
+    return y;
+}
+FHE_DEV cplx cadd(cplx a, cplx b) { return make_double2(a.x + b.x, a.y + b.y); }
+FHE_DEV cplx csub(cplx a, cplx b) { return make_double2(a.x - b.x, a.y - b.y); }
+FHE_DEV cplx conj_(cplx a) { return make_double2(a.x, -a.y); }
+// x * i  and  x * (-i), exact
+FHE_DEV cplx mul_i(cplx x) { return make_double2(-x.y, x.x); }
+FHE_DEV cplx mul_negi(cplx x) { return make_double2(x.y, -x.x); }
+
+FHE_DEV uint64_t f64_to_torus(double x) {
+    double r = __builtin_rint(x);
+    uint64_t b = (uint64_t)__double_as_longlong(r);
+    int e = (int)((b >> 52) & 0x7ff) - 1075;
+    uint64_t m = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
+    uint64_t v = (e >= 0) ? ((e < 64) ? (m << e) : 0ull) : ((e > -53) ? (m >> (-e)) : 0ull);
+    return (b >> 63) ? (0ull - v) : v;
+}
+
+// gadget decomposition, one level, base 2^BL, balanced digit in [-2^(BL-1), 2^(BL-1))
+template <int BL>
+FHE_DEV int32_t decomp1(uint64_t x) {
+    uint64_t v = (((x >> (63 - BL)) + 1) >> 1) & ((1ull << BL) - 1);
+    int32_t d = (int32_t)v;
+    return d >= (1 << (BL - 1)) ? d - (1 << BL) : d;
+}
+
+FHE_DEV uint32_t modswitch_2n(uint64_t x) {  // 2^64 -> 2N = 4096
+    return (uint32_t)((((x >> 51) + 1) >> 1) & 4095u);
+}
+
+// wave-level LDS ordering (rocPRIM wave_barrier idiom)
+FHE_DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------- swizzled LDS addressing
+FHE_DEV int swz_ab(int idx) { return idx ^ ((idx >> 6) & 15); }
+FHE_DEV int swz_bc(int idx) { return idx ^ ((idx >> 4) & 15); }
+
+// ---------------------------------------------------------------- forward FFT (DIF)
+FHE_DEV void dif_phase_a(cplx (&x)[16], int L, const cplx* __restrict__ W) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int hd = 8 >> s;
+#pragma unroll
+        for (int g = 0; g < hd; ++g) {  // distinct twiddles of this stage
+            const cplx w = W[(L + 64 * g) << s];
+#pragma unroll
+            for (int t = g; t < 16; t += 2 * hd) {
+                cplx a = x[t], c = x[t + hd];
+                x[t] = cadd(a, c);
+                x[t + hd] = cmul(csub(a, c), w);
+            }
+        }
+    }
+}
+
+FHE_DEV void dif_phase_b(cplx (&x)[16], int r, const cplx* __restrict__ W) {
+#pragma unroll
+    for (int s = 4; s < 8; ++s) {
+        const int hd = 8 >> (s - 4);
+#pragma unroll
+        for (int g = 0; g < hd; ++g) {
+            const cplx w = W[(r + 4 * g) << s];
+#pragma unroll
+            for (int u = g; u < 16; u += 2 * hd) {
+                cplx a = x[u], c = x[u + hd];
+                x[u] = cadd(a, c);
+                x[u + hd] = cmul(csub(a, c), w);
+            }
+        }
+    }
+}
+
+FHE_DEV void dif_phase_c(cplx (&x)[16]) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        cplx* y = x + 4 * v;
+        // stage 8 (h = 2): q=0 twiddle 1, q=1 twiddle W[256] = i
+        cplx a0 = y[0], c0 = y[2], a1 = y[1], c1 = y[3];
+        y[0] = cadd(a0, c0); y[2] = csub(a0, c0);
+        y[1] = cadd(a1, c1); y[3] = mul_i(csub(a1, c1));
+        // stage 9 (h = 1): twiddle 1
+        a0 = y[0]; c0 = y[1]; y[0] = cadd(a0, c0); y[1] = csub(a0, c0);
+        a1 = y[2]; c1 = y[3]; y[2] = cadd(a1, c1); y[3] = csub(a1, c1);
+    }
+}
+
+// ---------------------------------------------------------------- inverse FFT (DIT, conj)
+FHE_DEV void dit_phase_c(cplx (&x)[16]) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        cplx* y = x + 4 * v;
+        // stage 9 (h = 1)
+        cplx a0 = y[0], c0 = y[1], a1 = y[2], c1 = y[3];
+        y[0] = cadd(a0, c0); y[1] = csub(a0, c0);
+        y[2] = cadd(a1, c1); y[3] = csub(a1, c1);
+        // stage 8 (h = 2): q=1 twiddle conj(i) = -i
+        a0 = y[0]; c0 = y[2]; y[0] = cadd(a0, c0); y[2] = csub(a0, c0);
+        a1 = y[1]; c1 = mul_negi(y[3]); y[1] = cadd(a1, c1); y[3] = csub(a1, c1);
+    }
+}
+
+FHE_DEV void dit_phase_b(cplx (&x)[16], int r, const cplx* __restrict__ W) {
+#pragma unroll
+    for (int s = 7; s >= 4; --s) {
+        const int hd = 8 >> (s - 4);
+#pragma unroll
+        for (int g = 0; g < hd; ++g) {
+            const cplx w = conj_(W[(r + 4 * g) << s]);
+#pragma unroll
+            for (int u = g; u < 16; u += 2 * hd) {
+                cplx a = x[u], c = cmul(x[u + hd], w);
+                x[u] = cadd(a, c);
+                x[u + hd] = csub(a, c);
+            }
+        }
+    }
+}
+
+FHE_DEV void dit_phase_a(cplx (&x)[16], int L, const cplx* __restrict__ W) {
+#pragma unroll
+    for (int s = 3; s >= 0; --s) {
+        const int hd = 8 >> s;
+#pragma unroll
+        for (int g = 0; g < hd; ++g) {
+            const cplx w = conj_(W[(L + 64 * g) << s]);
+#pragma unroll
+            for (int t = g; t < 16; t += 2 * hd) {
+                cplx a = x[t], c = cmul(x[t + hd], w);
+                x[t] = cadd(a, c);
+                x[t + hd] = csub(a, c);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- exchanges (per-wave LDS)
+FHE_DEV void xchg_a_to_b(cplx (&x)[16], cplx* sc, int L) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) sc[swz_ab(L + 64 * t)] = x[t];
+    wave_sync();
+    const int b = L & 15, r = L >> 4;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) x[u] = sc[swz_ab(64 * b + r + 4 * u)];
+    wave_sync();
+}
+FHE_DEV void xchg_b_to_a(cplx (&x)[16], cplx* sc, int L) {
+    const int b = L & 15, r = L >> 4;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sc[swz_ab(64 * b + r + 4 * u)] = x[u];
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) x[t] = sc[swz_ab(L + 64 * t)];
+    wave_sync();
+}
+FHE_DEV void xchg_b_to_c(cplx (&x)[16], cplx* sc, int L) {
+    const int b = L & 15, r = L >> 4;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sc[swz_bc(64 * b + r + 4 * u)] = x[u];
+    wave_sync();
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[4 * v + q] = sc[swz_bc(4 * (L + 64 * v) + q)];
+    wave_sync();
+}
+FHE_DEV void xchg_c_to_b(cplx (&x)[16], cplx* sc, int L) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sc[swz_bc(4 * (L + 64 * v) + q)] = x[4 * v + q];
+    wave_sync();
+    const int b = L & 15, r = L >> 4;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) x[u] = sc[swz_bc(64 * b + r + 4 * u)];
+    wave_sync();
+}
+
+// natural-order (phase A) input -> bit-reversed output held in phase C layout
+FHE_DEV void fft_forward(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ W) {
+    dif_phase_a(x, L, W);
+    xchg_a_to_b(x, sc, L);
+    dif_phase_b(x, L >> 4, W);
+    xchg_b_to_c(x, sc, L);
+    dif_phase_c(x);
+}
+// phase C layout (bit-reversed) -> natural order in phase A layout, unscaled
+FHE_DEV void fft_inverse(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ W) {
+    dit_phase_c(x);
+    xchg_c_to_b(x, sc, L);
+    dit_phase_b(x, L >> 4, W);
+    xchg_b_to_a(x, sc, L);
+    dit_phase_a(x, L, W);
+}

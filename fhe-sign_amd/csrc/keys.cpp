@@ -1,0 +1,221 @@
+// keys.cpp -- client-side key generation, encryption and decryption (host).
+//
+// Reference call sites replaced: tfhe::generate_keys (src/schnorr.rs:442),
+// FheUint32::try_encrypt (src/biguint.rs:26,207), FheDecrypt::decrypt (src/biguint.rs:70).
+// The scheme is the published TFHE construction in tfhe-rs's default KS->PBS shape; the GPU
+// consumes the server key produced here.
+#include "keys.h"
+
+#include <cstring>
+#include <thread>
+
+namespace fhe {
+
+bool Params::from_c(const fhe_params& c, Params* out, const char** why) {
+    if (c.polynomial_size != kPolySize || c.glwe_dimension != 1 || c.pbs_level != 1) {
+        *why = "kernels support polynomial_size 2048, glwe_dimension 1, pbs_level 1 only";
+        return false;
+    }
+    if (c.ks_base_log != 3 || c.ks_level != 5) {
+        *why = "kernels support ks_base_log 3, ks_level 5 only";
+        return false;
+    }
+    if (c.lwe_dimension == 0 || c.lwe_dimension > 2048 || c.pbs_base_log == 0 || c.pbs_base_log > 30) {
+        *why = "lwe_dimension / pbs_base_log out of range";
+        return false;
+    }
+    if (c.pbs_base_log != 23) {
+        *why = "blind-rotate kernel is compiled for pbs_base_log 23";
+        return false;
+    }
+    uint32_t mc = c.message_modulus * c.carry_modulus;
+    if (c.message_modulus < 2 || mc > 64 || (mc & (mc - 1)) || (kPolySize % mc)) {
+        *why = "message*carry modulus must be a power of two <= 64";
+        return false;
+    }
+    if (c.lwe_noise_log2 > 62 || c.glwe_noise_log2 > 62) {
+        *why = "noise bound too large";
+        return false;
+    }
+    out->n = c.lwe_dimension;
+    out->pbs_base_log = c.pbs_base_log;
+    out->ks_base_log = c.ks_base_log;
+    out->ks_level = c.ks_level;
+    out->lwe_noise_log2 = c.lwe_noise_log2;
+    out->glwe_noise_log2 = c.glwe_noise_log2;
+    out->message_modulus = c.message_modulus;
+    out->carry_modulus = c.carry_modulus;
+    return true;
+}
+
+fhe_params Params::to_c() const {
+    fhe_params c;
+    c.lwe_dimension = n;
+    c.glwe_dimension = 1;
+    c.polynomial_size = kPolySize;
+    c.pbs_base_log = pbs_base_log;
+    c.pbs_level = 1;
+    c.ks_base_log = ks_base_log;
+    c.ks_level = ks_level;
+    c.lwe_noise_log2 = lwe_noise_log2;
+    c.glwe_noise_log2 = glwe_noise_log2;
+    c.message_modulus = message_modulus;
+    c.carry_modulus = carry_modulus;
+    return c;
+}
+
+// ------------------------------------------------------------------------------ ChaCha20
+static inline uint32_t rotl(uint32_t v, int c) { return (v << c) | (v >> (32 - c)); }
+static inline void qround(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+    a += b; d ^= a; d = rotl(d, 16);
+    c += d; b ^= c; b = rotl(b, 12);
+    a += b; d ^= a; d = rotl(d, 8);
+    c += d; b ^= c; b = rotl(b, 7);
+}
+
+void ChaChaStream::reset(uint64_t seed, uint32_t stream) {
+    key_.fill(0);
+    key_[0] = (uint32_t)seed;
+    key_[1] = (uint32_t)(seed >> 32);
+    key_[2] = 0x46484553u;  // "FHES"
+    nonce_ = {stream, 0x524f434du /* "ROCM" */, 0};
+    counter_ = 0;
+    pos_ = 16;
+}
+
+void ChaChaStream::refill() {
+    uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    for (int i = 0; i < 8; ++i) s[4 + i] = key_[i];
+    s[12] = counter_;
+    s[13] = nonce_[0];
+    s[14] = nonce_[1];
+    s[15] = nonce_[2];
+    uint32_t x[16];
+    std::memcpy(x, s, sizeof s);
+    for (int r = 0; r < 10; ++r) {
+        qround(x[0], x[4], x[8], x[12]);
+        qround(x[1], x[5], x[9], x[13]);
+        qround(x[2], x[6], x[10], x[14]);
+        qround(x[3], x[7], x[11], x[15]);
+        qround(x[0], x[5], x[10], x[15]);
+        qround(x[1], x[6], x[11], x[12]);
+        qround(x[2], x[7], x[8], x[13]);
+        qround(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; ++i) buf_[i] = x[i] + s[i];
+    if (++counter_ == 0) ++nonce_[2];
+    pos_ = 0;
+}
+
+uint64_t ChaChaStream::next_u64() {
+    if (pos_ >= 16) refill();
+    uint64_t lo = buf_[pos_++];
+    if (pos_ >= 16) refill();
+    uint64_t hi = buf_[pos_++];
+    return lo | (hi << 32);
+}
+
+int64_t ChaChaStream::tuniform(uint32_t b) {
+    const uint64_t x = next_u64();
+    const uint64_t u = x & ((1ull << (b + 1)) - 1);
+    const uint64_t c = (x >> (b + 1)) & 1ull;
+    return (int64_t)(u + c) - (int64_t)(1ull << b);
+}
+
+// ------------------------------------------------------------------------------ keygen
+// r += S * a mod (X^N + 1), S binary, exact in Z/2^64
+static void negacyclic_binary_mac(uint64_t* r, const uint64_t* a, const uint64_t* s) {
+    const int N = (int)kPolySize;
+    for (int j = 0; j < N; ++j) {
+        if (!s[j]) continue;
+        const uint64_t* src = a;
+        for (int m = j; m < N; ++m) r[m] += src[m - j];
+        for (int m = 0; m < j; ++m) r[m] -= src[m - j + N];
+    }
+}
+
+void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_server_key* sk) {
+    const uint32_t n = p.n, N = kPolySize, L = p.ks_level;
+    ck->params = p;
+    sk->params = p;
+    ck->lwe_sk.assign(n, 0);
+    ck->glwe_sk.assign(N, 0);
+    {
+        ChaChaStream r(seed, kStreamSecret);
+        for (auto& v : ck->lwe_sk) v = r.next_u64() & 1ull;
+        for (auto& v : ck->glwe_sk) v = r.next_u64() & 1ull;
+    }
+    ck->enc_rng.reset(seed, kStreamEncrypt);
+
+    // KSK[j][l] = LWE_{lwe_sk}( S_j * 2^(64 - base_log*(l+1)) )
+    sk->ksk.assign((size_t)N * L * (n + 1), 0);
+    {
+        ChaChaStream r(seed, kStreamKsk);
+        for (uint32_t j = 0; j < N; ++j)
+            for (uint32_t l = 0; l < L; ++l) {
+                uint64_t* row = sk->ksk.data() + ((size_t)j * L + l) * (n + 1);
+                uint64_t dot = 0;
+                for (uint32_t t = 0; t < n; ++t) {
+                    row[t] = r.next_u64();
+                    dot += row[t] * ck->lwe_sk[t];
+                }
+                const int64_t e = r.tuniform(p.lwe_noise_log2);
+                row[n] = dot + (ck->glwe_sk[j] << (64 - p.ks_base_log * (l + 1))) + (uint64_t)e;
+            }
+    }
+
+    // BSK[i] = GGSW_{S}(s_i): rows r = 0 (mask gadget), 1 (body gadget), one level.
+    // Masks and noises are drawn sequentially (deterministic stream), the exact A*S products are
+    // then computed in parallel on the host.
+    sk->bsk.assign((size_t)n * 4 * N, 0);
+    {
+        ChaChaStream r(seed, kStreamBsk);
+        for (uint32_t i = 0; i < n; ++i)
+            for (int row = 0; row < 2; ++row) {
+                uint64_t* A = sk->bsk.data() + (((size_t)i * 2 + row) * 2 + 0) * N;
+                uint64_t* B = sk->bsk.data() + (((size_t)i * 2 + row) * 2 + 1) * N;
+                for (uint32_t j = 0; j < N; ++j) A[j] = r.next_u64();
+                for (uint32_t j = 0; j < N; ++j) B[j] = (uint64_t)r.tuniform(p.glwe_noise_log2);
+            }
+    }
+    const uint32_t rows = n * 2;
+    unsigned nth = std::thread::hardware_concurrency();
+    if (nth == 0) nth = 4;
+    if (nth > 16) nth = 16;
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nth; ++t)
+        pool.emplace_back([&, t] {
+            for (uint32_t q = t; q < rows; q += nth) {
+                uint64_t* A = sk->bsk.data() + ((size_t)q * 2 + 0) * N;
+                uint64_t* B = sk->bsk.data() + ((size_t)q * 2 + 1) * N;
+                negacyclic_binary_mac(B, A, ck->glwe_sk.data());
+                const uint32_t i = q / 2, row = q % 2;
+                const uint64_t g = ck->lwe_sk[i] << (64 - p.pbs_base_log);
+                if (row == 0) A[0] += g; else B[0] += g;
+            }
+        });
+    for (auto& th : pool) th.join();
+}
+
+void encrypt_big(fhe_client_key* ck, uint64_t pt, uint64_t* ct) {
+    uint64_t dot = 0;
+    for (uint32_t j = 0; j < kBigDim; ++j) {
+        ct[j] = ck->enc_rng.next_u64();
+        dot += ct[j] * ck->glwe_sk[j];
+    }
+    const int64_t e = ck->enc_rng.tuniform(ck->params.glwe_noise_log2);
+    ct[kBigDim] = dot + pt + (uint64_t)e;
+}
+
+uint64_t decrypt_phase_big(const fhe_client_key* ck, const uint64_t* ct) {
+    uint64_t dot = 0;
+    for (uint32_t j = 0; j < kBigDim; ++j) dot += ct[j] * ck->glwe_sk[j];
+    return ct[kBigDim] - dot;
+}
+
+uint64_t decode_block(const Params& p, uint64_t phase) {
+    const uint64_t delta = p.delta();
+    return ((phase + delta / 2) / delta) % p.msg_carry();
+}
+
+}  // namespace fhe

@@ -1,0 +1,77 @@
+// keys.h -- client/server key material (host side) and the seeded CSPRNG.
+//
+// Replaces tfhe::generate_keys / ClientKey / ServerKey (src/schnorr.rs:441-443).  Client-side
+// operations (keygen, encrypt, decrypt) run on the host exactly as tfhe-rs runs them on the
+// client; the server key is uploaded to the GPU by fhe::Context::set_server_key.
+#pragma once
+#include <array>
+#include <cstdint>
+#include <vector>
+
+#include "fhe_rocm.h"
+
+namespace fhe {
+
+// Fixed shape of the device kernels.
+constexpr uint32_t kPolySize = 2048;
+constexpr uint32_t kBigDim = 2048;      // k * N
+constexpr uint32_t kBigCt = kBigDim + 1;
+
+struct Params {
+    uint32_t n = 834;
+    uint32_t pbs_base_log = 23;
+    uint32_t ks_base_log = 3;
+    uint32_t ks_level = 5;
+    uint32_t lwe_noise_log2 = 44;
+    uint32_t glwe_noise_log2 = 17;
+    uint32_t message_modulus = 4;
+    uint32_t carry_modulus = 4;
+
+    static bool from_c(const fhe_params& c, Params* out, const char** why);
+    fhe_params to_c() const;
+    uint64_t delta() const { return (1ull << 63) / ((uint64_t)message_modulus * carry_modulus); }
+    uint32_t msg_carry() const { return message_modulus * carry_modulus; }
+};
+
+// ChaCha20 block function (RFC 8439) as a deterministic stream of 64-bit words.
+class ChaChaStream {
+public:
+    ChaChaStream() = default;
+    ChaChaStream(uint64_t seed, uint32_t stream) { reset(seed, stream); }
+    void reset(uint64_t seed, uint32_t stream);
+    uint64_t next_u64();
+    int64_t tuniform(uint32_t log2_bound);
+
+private:
+    void refill();
+    std::array<uint32_t, 8> key_{};
+    std::array<uint32_t, 3> nonce_{};
+    uint32_t counter_ = 0;
+    std::array<uint32_t, 16> buf_{};
+    uint32_t pos_ = 16;
+};
+
+// Stream ids (shared convention with the oracle so key bytes can be compared).
+enum : uint32_t { kStreamSecret = 1, kStreamKsk = 2, kStreamBsk = 3, kStreamEncrypt = 100 };
+
+}  // namespace fhe
+
+struct fhe_client_key {
+    fhe::Params params;
+    std::vector<uint64_t> lwe_sk;   // n binary
+    std::vector<uint64_t> glwe_sk;  // N binary (= big LWE key)
+    fhe::ChaChaStream enc_rng;
+};
+
+struct fhe_server_key {
+    fhe::Params params;
+    std::vector<uint64_t> ksk;  // [N][ks_level][n+1]
+    std::vector<uint64_t> bsk;  // [n][row][poly][N] standard domain
+};
+
+namespace fhe {
+void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_server_key* sk);
+void encrypt_big(fhe_client_key* ck, uint64_t plaintext, uint64_t* ct);
+uint64_t decrypt_phase_big(const fhe_client_key* ck, const uint64_t* ct);
+uint64_t decode_block(const Params& p, uint64_t phase);  // value incl. carry, mod msg*carry
+}  // namespace fhe

@@ -1,0 +1,250 @@
+// pbs_kernels.hip -- programmable bootstrap (KS -> MS -> BR -> SE) for gfx950.
+//
+// Replaces the shortint/core_crypto PBS that tfhe 0.10.0 runs on the CPU under every radix op
+// the reference issues (src/biguint.rs:138,223,236,243,248; src/perf_test.rs:28-54).  The
+// algorithm restated by oracle/tfhe_oracle.c:fho_keyswitch / fho_blind_rotate /
+// fho_sample_extract; outputs are bit-exact against it.
+//
+// Kernels
+//   k_keyswitch      big LWE (2048+1) -> small LWE (n+1), fused modulus switch -> u16 [0, 2N)
+//   k_blind_rotate   n CMUX external products, f64 negacyclic FFT in registers+LDS,
+//                    fused sample extract -> big LWE
+//   k_bsk_to_fourier standard-domain BSK -> Fourier BSK in the blind-rotate lane layout
+#include "device_math.h"
+#include "kernels.h"
+
+namespace fhe {
+
+// ============================================================================ keyswitch
+// One workgroup = KS_C ciphertexts x 256 output coefficients.  Each KSK element is read once per
+// workgroup and applied to KS_C ciphertexts; digits are computed cooperatively into LDS (they
+// are uniform across the workgroup's lanes, so every digit read is an LDS broadcast).
+constexpr int KS_C = 16;   // ciphertexts per workgroup
+constexpr int KS_J = 16;   // input coefficients per LDS chunk
+constexpr int KS_LVL = 5;  // gadget levels (base 2^3)
+constexpr int KS_BL = 3;
+
+__global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ in, int count,
+                                                  const uint64_t* __restrict__ ksk,
+                                                  uint16_t* __restrict__ ms, int ms_stride,
+                                                  int n) {
+    __shared__ int8_t dig[KS_J][KS_LVL][KS_C];
+    const int c0 = blockIdx.x * KS_C;
+    const int k = blockIdx.y * 256 + threadIdx.x;
+    const bool active = k <= n;
+    uint64_t acc[KS_C];
+#pragma unroll
+    for (int c = 0; c < KS_C; ++c) acc[c] = 0;
+
+    const int tid = threadIdx.x;
+    const int dc = tid & (KS_C - 1), dj = tid >> 4;  // digit-producer mapping
+    const size_t row_stride = (size_t)(n + 1);
+    for (int j0 = 0; j0 < 2048; j0 += KS_J) {
+        {
+            const int ct = c0 + dc;
+            uint64_t a = (ct < count) ? in[(size_t)ct * 2049 + j0 + dj] : 0ull;
+            uint64_t v = (((a >> (63 - KS_BL * KS_LVL)) + 1) >> 1) & ((1ull << (KS_BL * KS_LVL)) - 1);
+#pragma unroll
+            for (int l = KS_LVL - 1; l >= 0; --l) {
+                int d = (int)(v & 7ull);
+                v >>= KS_BL;
+                if (d >= 4) { d -= 8; v += 1; }
+                dig[dj][l][dc] = (int8_t)d;
+            }
+        }
+        __syncthreads();
+        if (active) {
+#pragma unroll 2
+            for (int jj = 0; jj < KS_J; ++jj) {
+#pragma unroll
+                for (int l = 0; l < KS_LVL; ++l) {
+                    const uint64_t K = ksk[((size_t)(j0 + jj) * KS_LVL + l) * row_stride + k];
+#pragma unroll
+                    for (int c = 0; c < KS_C; ++c) {
+                        const int64_t d = dig[jj][l][c];
+                        acc[c] -= K * (uint64_t)d;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!active) return;
+#pragma unroll
+    for (int c = 0; c < KS_C; ++c) {
+        const int ct = c0 + c;
+        if (ct >= count) break;
+        uint64_t v = acc[c];
+        if (k == n) v += in[(size_t)ct * 2049 + 2048];
+        ms[(size_t)ct * ms_stride + k] = (uint16_t)modswitch_2n(v);
+    }
+}
+
+// ============================================================================ blind rotate
+// One workgroup (2 waves) per ciphertext.  Wave w owns GLWE polynomial w (0 = mask, 1 = body):
+// its accumulator lives in registers (lane L holds coefficients L + 64 t, t < 32), its FFT runs
+// in registers with two swizzled LDS exchanges, and the two waves swap their Fourier-domain
+// digit polynomials through LDS once per CMUX.
+constexpr int BR_PBS_BL = 23;
+
+__global__ __launch_bounds__(128) void k_blind_rotate(const uint16_t* __restrict__ ms, int ms_stride,
+                                                     const uint32_t* __restrict__ lut_idx,
+                                                     const uint64_t* __restrict__ luts,
+                                                     const cplx* __restrict__ bsk,
+                                                     const cplx* __restrict__ W,
+                                                     const cplx* __restrict__ psi,
+                                                     uint64_t* __restrict__ out, int n) {
+    __shared__ __attribute__((aligned(16))) cplx lds[2][1024];
+    const int ct = blockIdx.x;
+    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+    cplx* sc = lds[w];
+    cplx* sc_other = lds[w ^ 1];
+    uint64_t* scu = reinterpret_cast<uint64_t*>(sc);
+    const uint16_t* a_ct = ms + (size_t)ct * ms_stride;
+
+    uint64_t acc[32];
+    {
+        const uint32_t bt = a_ct[n];
+        const int rot = (int)((4096u - bt) & 4095u);  // X^{-b}
+        const uint64_t* lut = luts + (size_t)lut_idx[ct] * 2048;
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            uint64_t v = 0;
+            if (w == 1) {
+                int jj = L + 64 * t - rot;
+                if (jj >= 0) v = lut[jj];
+                else if (jj >= -2048) v = 0ull - lut[jj + 2048];
+                else v = lut[jj + 4096];
+            }
+            acc[t] = v;
+        }
+    }
+
+    uint32_t a_next = a_ct[0];
+    for (int i = 0; i < n; ++i) {
+        const uint32_t a = a_next;
+        a_next = a_ct[i + 1];
+        if (a == 0) continue;  // X^0 - 1 = 0: the external product is exactly zero
+
+        // ---- rotate, subtract, decompose, twist
+#pragma unroll
+        for (int t = 0; t < 32; ++t) scu[L + 64 * t] = acc[t];
+        wave_sync();
+        cplx x[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            int32_t d2[2];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int tt = t + 16 * hh;
+                int jj = L + 64 * tt - (int)a;
+                uint64_t v;
+                if (jj >= 0) v = scu[jj];
+                else if (jj >= -2048) v = 0ull - scu[jj + 2048];
+                else v = scu[jj + 4096];
+                d2[hh] = decomp1<BR_PBS_BL>(v - acc[tt]);
+            }
+            x[t] = cmul(make_double2((double)d2[0], (double)d2[1]), psi[L + 64 * t]);
+        }
+        wave_sync();
+
+        // ---- forward FFT of this wave's digit polynomial
+        fft_forward(x, sc, L, W);
+
+        // ---- swap Fourier digits with the partner wave, pointwise MAC with the BSK
+#pragma unroll
+        for (int R = 0; R < 16; ++R) sc[R * 64 + L] = x[R];
+        __syncthreads();
+        {
+            const cplx* b0 = bsk + ((size_t)((i * 2 + 0) * 2 + w) * 16) * 64 + L;  // row 0 (mask digit)
+            const cplx* b1 = bsk + ((size_t)((i * 2 + 1) * 2 + w) * 16) * 64 + L;  // row 1 (body digit)
+#pragma unroll
+            for (int R = 0; R < 16; ++R) {
+                const cplx mine = x[R];
+                const cplx other = sc_other[R * 64 + L];
+                const cplx d0 = (w == 0) ? mine : other;
+                const cplx d1 = (w == 0) ? other : mine;
+                const cplx B0 = b0[R * 64], B1 = b1[R * 64];
+                cplx o;
+                o.x = __fma_rn(d0.x, B0.x, __fma_rn(-d0.y, B0.y, __fma_rn(d1.x, B1.x, -(d1.y * B1.y))));
+                o.y = __fma_rn(d0.x, B0.y, __fma_rn(d0.y, B0.x, __fma_rn(d1.x, B1.y, d1.y * B1.x)));
+                x[R] = o;
+            }
+        }
+        __syncthreads();
+
+        // ---- inverse FFT, untwist, round, accumulate
+        fft_inverse(x, sc, L, W);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const cplx p = psi[L + 64 * t];
+            const cplx u = make_double2(p.x * 0.0009765625, -p.y * 0.0009765625);
+            const cplx y = cmul(x[t], u);
+            acc[t] += f64_to_torus(y.x);
+            acc[t + 16] += f64_to_torus(y.y);
+        }
+    }
+
+    // ---- sample extract (coefficient 0)
+    uint64_t* o = out + (size_t)ct * 2049;
+    if (w == 0) {
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const int j = L + 64 * t;
+            if (j == 0) o[0] = acc[t];
+            else o[2048 - j] = 0ull - acc[t];
+        }
+    } else if (L == 0) {
+        o[2048] = acc[0];
+    }
+}
+
+// ============================================================================ BSK -> Fourier
+// One wave per polynomial: [n][row][poly][2048] u64 -> [n][row][poly][R][L] complex (phase C).
+__global__ __launch_bounds__(64) void k_bsk_to_fourier(const uint64_t* __restrict__ bsk, int npoly,
+                                                       const cplx* __restrict__ W,
+                                                       const cplx* __restrict__ psi,
+                                                       cplx* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) cplx sc[1024];
+    const int q = blockIdx.x;
+    if (q >= npoly) return;
+    const int L = threadIdx.x;
+    const uint64_t* p = bsk + (size_t)q * 2048;
+    cplx x[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const double re = (double)(int64_t)p[L + 64 * t];
+        const double im = (double)(int64_t)p[L + 64 * t + 1024];
+        x[t] = cmul(make_double2(re, im), psi[L + 64 * t]);
+    }
+    fft_forward(x, sc, L, W);
+    cplx* o = out + (size_t)q * 1024 + L;
+#pragma unroll
+    for (int R = 0; R < 16; ++R) o[R * 64] = x[R];
+}
+
+// ============================================================================ launchers
+hipError_t launch_keyswitch(const uint64_t* in, int count, const uint64_t* ksk, uint16_t* ms,
+                            int ms_stride, int n, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    dim3 grid((count + KS_C - 1) / KS_C, (n + 1 + 255) / 256);
+    hipLaunchKernelGGL(k_keyswitch, grid, dim3(256), 0, s, in, count, ksk, ms, ms_stride, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate(const uint16_t* ms, int ms_stride, const uint32_t* lut_idx,
+                               const uint64_t* luts, const cplx* bsk, const cplx* W,
+                               const cplx* psi, uint64_t* out, int count, int n, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_blind_rotate, dim3(count), dim3(128), 0, s, ms, ms_stride, lut_idx, luts, bsk,
+                       W, psi, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_bsk_to_fourier(const uint64_t* bsk, int npoly, const cplx* W, const cplx* psi,
+                                 cplx* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_bsk_to_fourier, dim3(npoly), dim3(64), 0, s, bsk, npoly, W, psi, out);
+    return hipGetLastError();
+}
+
+}  // namespace fhe

@@ -1,0 +1,11 @@
+"""fhe_sign -- Python host binding of the MI355X-native TFHE radix engine (fhe-sign_amd).
+
+Mirrors the reference crate's surface (coset-io/fhe-sign):
+  generate_keys / set_server_key      tfhe HL API as used at src/schnorr.rs:441-443
+  FheUint{8,32,64}                    tfhe FheUint ops used by src/biguint.rs and src/perf_test.rs
+  BigUintFHE (+, *)                   src/biguint.rs:8-265
+  Schnorr.sign_fhe_with_k0 / sign_fhe src/schnorr.rs:154-290
+All ciphertext arithmetic runs on the GPU through lib/libfhe_rocm.so; this package only marshals.
+"""
+from ._lib import FheError, FheParams, load  # noqa: F401
+from .core import ClientKey, Context, ServerKey, default_params, generate_keys  # noqa: F401

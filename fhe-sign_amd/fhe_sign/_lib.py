@@ -1,0 +1,90 @@
+"""ctypes binding of include/fhe_rocm.h (the engine's C ABI).
+
+This is the same binding a maintainer would write for the reference's FFI;
+the tests and bench drive the engine exclusively through it.  The shared library must be the
+in-tree build (fhe-sign_amd/lib/libfhe_rocm.so); there is no fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libfhe_rocm.so")
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+dblp = C.POINTER(C.c_double)
+
+
+class FheParams(C.Structure):
+    _fields_ = [(name, C.c_uint32) for name in (
+        "lwe_dimension", "glwe_dimension", "polynomial_size", "pbs_base_log", "pbs_level",
+        "ks_base_log", "ks_level", "lwe_noise_log2", "glwe_noise_log2", "message_modulus",
+        "carry_modulus")]
+
+
+# (name, restype, argtypes) -- every symbol include/fhe_rocm.h declares
+_SIGNATURES = [
+    ("fhe_last_error", C.c_char_p, []),
+    ("fhe_params_default", C.c_int, [C.POINTER(FheParams)]),
+    ("fhe_generate_keys", C.c_int, [C.POINTER(FheParams), C.c_uint64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    ("fhe_client_key_destroy", None, [C.c_void_p]),
+    ("fhe_server_key_destroy", None, [C.c_void_p]),
+    ("fhe_client_key_export", C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
+    ("fhe_server_key_export", C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
+    ("fhe_client_key_seed_encryption", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32]),
+    ("fhe_encrypt_block", C.c_int, [C.c_void_p, C.c_uint64, u64p]),
+    ("fhe_decrypt_block", C.c_int, [C.c_void_p, u64p, u64p]),
+    ("fhe_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("fhe_ctx_destroy", None, [C.c_void_p]),
+    ("fhe_set_server_key", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("fhe_ctx_export_fourier_bsk", C.c_int, [C.c_void_p, dblp, C.c_size_t]),
+    ("fhe_ctx_sync", C.c_int, [C.c_void_p]),
+    ("fhe_lut_register", C.c_int, [C.c_void_p, u32p, C.c_uint32, u32p]),
+    ("fhe_pbs_batch", C.c_int, [C.c_void_p, u64p, C.c_size_t, u32p, u64p]),
+    ("fhe_pbs_batch_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
+    ("fhe_device_alloc", C.c_void_p, [C.c_void_p, C.c_size_t]),
+    ("fhe_device_free", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("fhe_memcpy_h2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("fhe_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("fhe_ctx_last_pbs_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    ("fhe_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
+]
+
+_lib = None
+
+
+class FheError(RuntimeError):
+    pass
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FheError(f"native engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in _SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def declared_symbols() -> list[str]:
+    return [s[0] for s in _SIGNATURES]
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().fhe_last_error()
+        raise FheError(f"fhe error {rc}: {msg.decode() if msg else ''}")
+
+
+def ptr(arr, ctype=C.c_uint64):
+    """Pointer to a contiguous numpy array."""
+    return arr.ctypes.data_as(C.POINTER(ctype))

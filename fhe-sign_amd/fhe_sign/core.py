@@ -1,0 +1,158 @@
+"""Keys, device context and the raw PBS boundary (thin wrappers over the C ABI)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import FheParams, check, load, ptr
+
+BIG_CT = 2049  # big LWE ciphertext words
+
+
+def default_params() -> FheParams:
+    p = FheParams()
+    check(load().fhe_params_default(C.byref(p)))
+    return p
+
+
+class ClientKey:
+    def __init__(self, handle, params: FheParams):
+        self._h = handle
+        self.params = params
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            load().fhe_client_key_destroy(self._h)
+            self._h = None
+
+    def export(self):
+        n = self.params.lwe_dimension
+        lwe = np.zeros(n, np.uint64)
+        glwe = np.zeros(self.params.polynomial_size, np.uint64)
+        check(load().fhe_client_key_export(self._h, ptr(lwe), n, ptr(glwe), glwe.size))
+        return lwe, glwe
+
+    def seed_encryption(self, seed: int, stream: int = 100) -> None:
+        check(load().fhe_client_key_seed_encryption(self._h, seed, stream))
+
+    def encrypt_block(self, value: int) -> np.ndarray:
+        ct = np.zeros(BIG_CT, np.uint64)
+        check(load().fhe_encrypt_block(self._h, value, ptr(ct)))
+        return ct
+
+    def decrypt_block(self, ct: np.ndarray) -> int:
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        out = C.c_uint64(0)
+        check(load().fhe_decrypt_block(self._h, ptr(ct), C.byref(out)))
+        return int(out.value)
+
+
+class ServerKey:
+    def __init__(self, handle, params: FheParams):
+        self._h = handle
+        self.params = params
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            load().fhe_server_key_destroy(self._h)
+            self._h = None
+
+    def export(self):
+        p = self.params
+        n, N, L = p.lwe_dimension, p.polynomial_size, p.ks_level
+        ksk = np.zeros(N * L * (n + 1), np.uint64)
+        bsk = np.zeros(n * 4 * N, np.uint64)
+        check(load().fhe_server_key_export(self._h, ptr(ksk), ksk.size, ptr(bsk), bsk.size))
+        return ksk, bsk
+
+
+def generate_keys(params: FheParams | None = None, seed: int = 0):
+    """tfhe::generate_keys(ConfigBuilder::default().build()) -- src/schnorr.rs:441-442."""
+    p = params or default_params()
+    ck, sk = C.c_void_p(), C.c_void_p()
+    check(load().fhe_generate_keys(C.byref(p), seed, C.byref(ck), C.byref(sk)))
+    return ClientKey(ck, p), ServerKey(sk, p)
+
+
+class Context:
+    """One GPU + installed server key (tfhe::set_server_key, src/schnorr.rs:443)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(load().fhe_ctx_create(device, C.byref(h)))
+        self._h = h
+        self.params = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().fhe_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_server_key(self, sk: ServerKey) -> None:
+        check(load().fhe_set_server_key(self._h, sk.handle))
+        self.params = sk.params
+
+    def export_fourier_bsk(self) -> np.ndarray:
+        n = self.params.lwe_dimension
+        out = np.zeros(n * 4 * 1024 * 2, np.float64)
+        check(load().fhe_ctx_export_fourier_bsk(self._h, ptr(out, C.c_double), out.size))
+        return out
+
+    def lut(self, table) -> int:
+        t = np.ascontiguousarray(np.asarray(table, dtype=np.uint32))
+        out = C.c_uint32(0)
+        check(load().fhe_lut_register(self._h, ptr(t, C.c_uint32), t.size, C.byref(out)))
+        return int(out.value)
+
+    def pbs(self, cts: np.ndarray, lut_ids) -> np.ndarray:
+        cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, BIG_CT)
+        ids = np.ascontiguousarray(np.broadcast_to(np.asarray(lut_ids, np.uint32), (cts.shape[0],)))
+        out = np.zeros_like(cts)
+        check(load().fhe_pbs_batch(self._h, ptr(cts), cts.shape[0], ptr(ids, C.c_uint32), ptr(out)))
+        return out
+
+    # device-resident helpers (bench)
+    def alloc(self, nbytes: int) -> int:
+        p = load().fhe_device_alloc(self._h, nbytes)
+        if not p:
+            check(-4)
+        return p
+
+    def free(self, p: int) -> None:
+        check(load().fhe_device_free(self._h, C.c_void_p(p)))
+
+    def h2d(self, dst: int, arr: np.ndarray) -> None:
+        check(load().fhe_memcpy_h2d(self._h, C.c_void_p(dst), arr.ctypes.data_as(C.c_void_p), arr.nbytes))
+
+    def d2h(self, arr: np.ndarray, src: int) -> None:
+        check(load().fhe_memcpy_d2h(self._h, arr.ctypes.data_as(C.c_void_p), C.c_void_p(src), arr.nbytes))
+
+    def pbs_device(self, d_in: int, count: int, d_lut: int, d_out: int) -> None:
+        check(load().fhe_pbs_batch_device(self._h, C.c_void_p(d_in), count, C.c_void_p(d_lut), C.c_void_p(d_out)))
+
+    def sync(self) -> None:
+        check(load().fhe_ctx_sync(self._h))
+
+    def enable_timing(self, on: bool = True) -> None:
+        check(load().fhe_ctx_enable_timing(self._h, 1 if on else 0))
+
+    def last_pbs_timing(self):
+        ks, br = C.c_float(), C.c_float()
+        check(load().fhe_ctx_last_pbs_timing(self._h, C.byref(ks), C.byref(br)))
+        return float(ks.value), float(br.value)

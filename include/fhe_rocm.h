@@ -1,0 +1,113 @@
+/*
+ * fhe_rocm.h -- C ABI of the MI355X-native TFHE radix-integer engine.
+ *
+ * Drop-in boundary for the hot path of coset-io/fhe-sign: the tfhe-rs high-level API that
+ * BigUintFHE (src/biguint.rs) and Schnorr::sign_fhe_with_k0 (src/schnorr.rs:235-290) call.
+ * Every entry point cites the reference interface it replaces.  Plain pointers and sizes only;
+ * no torch or HIP types cross this boundary.  All functions return FHE_OK (0) or a negative
+ * status; fhe_last_error() gives the message (thread-local).  Nothing aborts across the ABI
+ * (the reference panics via unwrap at src/biguint.rs:207; here that is FHE_ERR_*).
+ *
+ * Threading: like tfhe-rs's thread-local `set_server_key` (src/schnorr.rs:443), a server key is
+ * installed per context and a context is used by one host thread at a time.
+ *
+ * Ciphertext layout (one radix block = one LWE ciphertext under the big key):
+ *   uint64_t[2049] = mask[2048] then body.  A radix integer of B bits has B/2 blocks, LSB first.
+ */
+#ifndef FHE_ROCM_H
+#define FHE_ROCM_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FHE_OK 0
+#define FHE_ERR_INVALID (-1)
+#define FHE_ERR_HIP (-2)
+#define FHE_ERR_NO_KEY (-3)
+#define FHE_ERR_ALLOC (-4)
+#define FHE_ERR_UNSUPPORTED (-5)
+
+#define FHE_LWE_BIG_SIZE 2049u /* big LWE ciphertext words (k*N + 1) */
+
+/* Parameter set.  Default = tfhe 0.10.0 ConfigBuilder::default() shape (2_2 radix blocks,
+ * KS->PBS, TUniform); replaces `ConfigBuilder::default().build()` (src/schnorr.rs:441,
+ * src/perf_test.rs:9).  polynomial_size 2048, glwe_dimension 1, pbs_level 1, ks_level 5,
+ * ks_base_log 3 are fixed by the kernels; the others may vary. */
+typedef struct fhe_params {
+    uint32_t lwe_dimension;   /* n (834) */
+    uint32_t glwe_dimension;  /* k (1) */
+    uint32_t polynomial_size; /* N (2048) */
+    uint32_t pbs_base_log;    /* 23 */
+    uint32_t pbs_level;       /* 1 */
+    uint32_t ks_base_log;     /* 3 */
+    uint32_t ks_level;        /* 5 */
+    uint32_t lwe_noise_log2;  /* TUniform bound, small key (44) */
+    uint32_t glwe_noise_log2; /* TUniform bound, big/GLWE key (17) */
+    uint32_t message_modulus; /* 4 */
+    uint32_t carry_modulus;   /* 4 */
+} fhe_params;
+
+typedef struct fhe_client_key fhe_client_key;
+typedef struct fhe_server_key fhe_server_key;
+typedef struct fhe_ctx fhe_ctx;
+
+const char* fhe_last_error(void);
+int fhe_params_default(fhe_params* out);
+
+/* ---------------------------------------------------------------------------------- keys */
+/* Replaces tfhe::generate_keys(config) (src/schnorr.rs:442, src/biguint.rs:277,
+ * src/perf_test.rs:12).  Deterministic in `seed` (ChaCha20 streams). */
+int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** client_key,
+                      fhe_server_key** server_key);
+void fhe_client_key_destroy(fhe_client_key* ck);
+void fhe_server_key_destroy(fhe_server_key* sk);
+/* Raw key material (tests / serialization): sizes in uint64 words. */
+int fhe_client_key_export(const fhe_client_key* ck, uint64_t* lwe_sk, size_t lwe_len,
+                          uint64_t* glwe_sk, size_t glwe_len);
+int fhe_server_key_export(const fhe_server_key* sk, uint64_t* ksk, size_t ksk_len, uint64_t* bsk,
+                          size_t bsk_len);
+/* Re-seed the client key's encryption stream (deterministic tests). */
+int fhe_client_key_seed_encryption(fhe_client_key* ck, uint64_t seed, uint32_t stream);
+
+/* Shortint block encrypt/decrypt (the per-block step under FheUint32::try_encrypt,
+ * src/biguint.rs:26, and FheDecrypt, src/biguint.rs:70).  value < message*carry modulus. */
+int fhe_encrypt_block(fhe_client_key* ck, uint64_t value, uint64_t* ct /*2049*/);
+int fhe_decrypt_block(const fhe_client_key* ck, const uint64_t* ct, uint64_t* value /*msg+carry*/);
+
+/* ------------------------------------------------------------------------------- context */
+int fhe_ctx_create(int device, fhe_ctx** ctx);
+void fhe_ctx_destroy(fhe_ctx* ctx);
+/* Replaces tfhe::set_server_key(server_key) (src/schnorr.rs:443): uploads KSK + BSK to this
+ * context's GPU and converts the BSK to the Fourier domain there. */
+int fhe_set_server_key(fhe_ctx* ctx, const fhe_server_key* sk);
+/* Fourier BSK as held on the device (tests: bit-exact check against the CPU restatement);
+ * layout [n][row][poly][16][64] complex f64. */
+int fhe_ctx_export_fourier_bsk(fhe_ctx* ctx, double* out, size_t len_doubles);
+int fhe_ctx_sync(fhe_ctx* ctx);
+
+/* ------------------------------------------------------------------- raw PBS boundary */
+/* Register a univariate lookup table f: [0, msg*carry) -> [0, msg*carry). */
+int fhe_lut_register(fhe_ctx* ctx, const uint32_t* table, uint32_t table_len, uint32_t* lut_id);
+/* Keyswitch + bootstrap `count` big-key LWE blocks, block i through LUT lut_ids[i].
+ * Host pointers; synchronous. */
+int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* in, size_t count, const uint32_t* lut_ids,
+                  uint64_t* out);
+/* Same on device pointers, enqueued on the context stream (asynchronous). */
+int fhe_pbs_batch_device(fhe_ctx* ctx, const uint64_t* d_in, size_t count,
+                         const uint32_t* d_lut_ids, uint64_t* d_out);
+/* Device memory helpers (so callers need no HIP types). */
+void* fhe_device_alloc(fhe_ctx* ctx, size_t bytes);
+int fhe_device_free(fhe_ctx* ctx, void* p);
+int fhe_memcpy_h2d(fhe_ctx* ctx, void* dst, const void* src, size_t bytes);
+int fhe_memcpy_d2h(fhe_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Profiling: time of the last fhe_pbs_batch_device split by stage (ms, HIP events). */
+int fhe_ctx_last_pbs_timing(fhe_ctx* ctx, float* ks_ms, float* br_ms);
+int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,436 @@
+/*
+ * tfhe_oracle.c -- CPU restatement of the TFHE pipeline under the reference's FheUint ops.
+ * TEST INFRASTRUCTURE ONLY (see tfhe_oracle.h).  Build: oracle/Makefile (-ffp-contract=off).
+ *
+ * Reference anchors (the algorithm lives in the absent crate tfhe 0.10.0, Cargo.lock:482-504;
+ * these are the reference call sites whose results this pipeline produces):
+ *   FheUint64 * FheUint64      src/biguint.rs:223      (radix mul -> many PBS)
+ *   FheUint64 + FheUint64      src/biguint.rs:138,236,243 (radix add -> carry PBS)
+ *   FheUint32::try_encrypt     src/biguint.rs:26,207   (fho_encrypt_big per block)
+ *   digit.decrypt              src/biguint.rs:70       (fho_decrypt_phase_big + fho_decode)
+ *   generate_keys(ConfigBuilder::default())  src/schnorr.rs:441-442 (fho_keygen)
+ * Published TFHE algorithm restated (Chillotti et al., "TFHE: Fast Fully Homomorphic Encryption
+ * over the Torus", J. Cryptology 2020; KS->PBS order of tfhe-rs shortint):
+ *   KS  (Alg. "key switching", gadget base 2^ks_base_log, ks_level levels, rounding decomposition)
+ *   MS  (modulus switch 2^64 -> 2N with rounding)
+ *   BR  (blind rotation: ACC = X^{-b} * LUT, then n CMUX = external products with GGSW(s_i))
+ *   SE  (sample extract coefficient 0)
+ */
+#include "tfhe_oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+void fho_default_params(fho_params* p) {
+    /* tfhe 0.10.0 default (believed PARAM_MESSAGE_2_CARRY_2_KS_PBS_TUNIFORM_2M64) [ext, unverified] */
+    p->n = 834;
+    p->ks_base_log = 3;
+    p->ks_level = 5;
+    p->pbs_base_log = 23;
+    p->lwe_noise_log2 = 44;
+    p->glwe_noise_log2 = 17;
+    p->message_modulus = 4;
+    p->carry_modulus = 4;
+}
+
+/* ------------------------------------------------------------------ ChaCha20 (RFC 8439) */
+#define ROTL32(v, c) (((v) << (c)) | ((v) >> (32 - (c))))
+#define QR(a, b, c, d)                                                                      \
+    a += b; d ^= a; d = ROTL32(d, 16); c += d; b ^= c; b = ROTL32(b, 12);                   \
+    a += b; d ^= a; d = ROTL32(d, 8);  c += d; b ^= c; b = ROTL32(b, 7);
+
+static void chacha_block(fho_rng* r) {
+    uint32_t s[16], x[16];
+    s[0] = 0x61707865u; s[1] = 0x3320646eu; s[2] = 0x79622d32u; s[3] = 0x6b206574u;
+    for (int i = 0; i < 8; ++i) s[4 + i] = r->key[i];
+    s[12] = r->counter;
+    s[13] = r->nonce[0]; s[14] = r->nonce[1]; s[15] = r->nonce[2];
+    memcpy(x, s, sizeof s);
+    for (int i = 0; i < 10; ++i) {
+        QR(x[0], x[4], x[8], x[12]); QR(x[1], x[5], x[9], x[13]);
+        QR(x[2], x[6], x[10], x[14]); QR(x[3], x[7], x[11], x[15]);
+        QR(x[0], x[5], x[10], x[15]); QR(x[1], x[6], x[11], x[12]);
+        QR(x[2], x[7], x[8], x[13]); QR(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; ++i) r->buf[i] = x[i] + s[i];
+    r->counter++;
+    if (r->counter == 0) r->nonce[2]++; /* extend the 32-bit block counter */
+    r->pos = 0;
+}
+
+void fho_rng_init(fho_rng* r, uint64_t seed, uint32_t stream) {
+    memset(r, 0, sizeof *r);
+    r->key[0] = (uint32_t)seed;
+    r->key[1] = (uint32_t)(seed >> 32);
+    r->key[2] = 0x46484553u; /* "FHES" domain tag */
+    r->nonce[0] = stream;
+    r->nonce[1] = 0x524f434du; /* "ROCM" */
+    r->pos = 16;
+}
+
+static uint32_t rng_u32(fho_rng* r) {
+    if (r->pos >= 16) chacha_block(r);
+    return r->buf[r->pos++];
+}
+
+uint64_t fho_rng_u64(fho_rng* r) {
+    uint64_t lo = rng_u32(r);
+    uint64_t hi = rng_u32(r);
+    return lo | (hi << 32);
+}
+
+/* TUniform(b): integer in [-2^b, 2^b], end points at half the probability of the others. */
+int64_t fho_rng_tuniform(fho_rng* r, uint32_t b) {
+    uint64_t x = fho_rng_u64(r);
+    uint64_t u = x & ((1ull << (b + 1)) - 1);
+    uint64_t c = (x >> (b + 1)) & 1ull;
+    return (int64_t)(u + c) - (int64_t)(1ull << b);
+}
+
+/* ------------------------------------------------------------------ FFT tables */
+static double g_tw[512 * 2];
+static double g_psi[1024 * 2];
+static int g_tables_ready = 0;
+
+void fho_tables_init(void) {
+    if (g_tables_ready) return;
+    const double pi = 3.14159265358979323846264338327950288;
+    for (int k = 0; k < 512; ++k) {
+        double a = 2.0 * pi * (double)k / 1024.0;
+        g_tw[2 * k] = cos(a);
+        g_tw[2 * k + 1] = sin(a);
+    }
+    /* exact values where the angle is a multiple of pi/2 */
+    g_tw[0] = 1.0; g_tw[1] = 0.0;
+    g_tw[2 * 256] = 0.0; g_tw[2 * 256 + 1] = 1.0;
+    for (int j = 0; j < 1024; ++j) {
+        double a = pi * (double)j / 2048.0;
+        g_psi[2 * j] = cos(a);
+        g_psi[2 * j + 1] = sin(a);
+    }
+    g_psi[0] = 1.0; g_psi[1] = 0.0;
+    g_tables_ready = 1;
+}
+
+const double* fho_twiddles(void) { fho_tables_init(); return g_tw; }
+const double* fho_twist(void) { fho_tables_init(); return g_psi; }
+
+/* (x) * (w): the single complex-multiply formula used everywhere (GPU identical) */
+static inline void cmul(double xr, double xi, double wr, double wi, double* yr, double* yi) {
+    *yr = fma(xr, wr, -(xi * wi));
+    *yi = fma(xr, wi, xi * wr);
+}
+
+/* Forward: radix-2 decimation in frequency, natural order in, bit-reversed order out. */
+void fho_fft_forward(double* x) {
+    fho_tables_init();
+    for (int s = 0; s < 10; ++s) {
+        int h = 512 >> s;
+        for (int b = 0; b < 1024; b += 2 * h) {
+            for (int j = 0; j < h; ++j) {
+                double* p = x + 2 * (b + j);
+                double* q = x + 2 * (b + j + h);
+                double ar = p[0], ai = p[1], cr = q[0], ci = q[1];
+                double sr = ar + cr, si = ai + ci;
+                double dr = ar - cr, di = ai - ci;
+                const double* w = g_tw + 2 * (j << s);
+                p[0] = sr; p[1] = si;
+                cmul(dr, di, w[0], w[1], &q[0], &q[1]);
+            }
+        }
+    }
+}
+
+/* Inverse: radix-2 decimation in time with conjugate twiddles, bit-reversed in, natural out,
+ * unscaled (x 1024). */
+void fho_fft_inverse(double* x) {
+    fho_tables_init();
+    for (int s = 9; s >= 0; --s) {
+        int h = 512 >> s;
+        for (int b = 0; b < 1024; b += 2 * h) {
+            for (int j = 0; j < h; ++j) {
+                double* p = x + 2 * (b + j);
+                double* q = x + 2 * (b + j + h);
+                const double* w = g_tw + 2 * (j << s);
+                double tr, ti;
+                cmul(q[0], q[1], w[0], -w[1], &tr, &ti);
+                double ar = p[0], ai = p[1];
+                p[0] = ar + tr; p[1] = ai + ti;
+                q[0] = ar - tr; q[1] = ai - ti;
+            }
+        }
+    }
+}
+
+void fho_poly_to_fourier(const uint64_t* poly, double* out) {
+    fho_tables_init();
+    for (int j = 0; j < 1024; ++j) {
+        double re = (double)(int64_t)poly[j];
+        double im = (double)(int64_t)poly[j + 1024];
+        cmul(re, im, g_psi[2 * j], g_psi[2 * j + 1], &out[2 * j], &out[2 * j + 1]);
+    }
+    fho_fft_forward(out);
+}
+
+void fho_ipoly_to_fourier(const int64_t* poly, double* out) {
+    fho_tables_init();
+    for (int j = 0; j < 1024; ++j) {
+        double re = (double)poly[j];
+        double im = (double)poly[j + 1024];
+        cmul(re, im, g_psi[2 * j], g_psi[2 * j + 1], &out[2 * j], &out[2 * j + 1]);
+    }
+    fho_fft_forward(out);
+}
+
+/* round(x) mod 2^64, x finite.  rint = IEEE round-half-even (GPU: v_rndne_f64). */
+uint64_t fho_f64_to_torus(double x) {
+    double r = rint(x);
+    uint64_t b;
+    memcpy(&b, &r, 8);
+    int e = (int)((b >> 52) & 0x7ff) - 1075;
+    uint64_t m = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
+    uint64_t v;
+    if (e >= 0)
+        v = (e < 64) ? (m << e) : 0;
+    else
+        v = (e > -53) ? (m >> (-e)) : 0;
+    return (b >> 63) ? (uint64_t)0 - v : v;
+}
+
+void fho_fourier_add_to_poly(double* f, uint64_t* acc) {
+    fho_tables_init();
+    fho_fft_inverse(f);
+    const double inv = 0.0009765625; /* 2^-10, exact */
+    for (int j = 0; j < 1024; ++j) {
+        double ur = g_psi[2 * j] * inv, ui = -g_psi[2 * j + 1] * inv; /* exact scalings */
+        double yr, yi;
+        cmul(f[2 * j], f[2 * j + 1], ur, ui, &yr, &yi);
+        acc[j] += fho_f64_to_torus(yr);
+        acc[j + 1024] += fho_f64_to_torus(yi);
+    }
+}
+
+/* ------------------------------------------------------------------ keygen */
+/* r += S * A  (negacyclic, S binary), exact mod 2^64 */
+static void poly_mul_binary_acc(uint64_t* r, const uint64_t* a, const uint64_t* s) {
+    for (int j = 0; j < FHO_N; ++j) {
+        if (!s[j]) continue;
+        for (int m = j; m < FHO_N; ++m) r[m] += a[m - j];
+        for (int m = 0; m < j; ++m) r[m] -= a[m - j + FHO_N];
+    }
+}
+
+int fho_keygen(fho_keys* k, const fho_params* p, uint64_t seed) {
+    memset(k, 0, sizeof *k);
+    k->p = *p;
+    const uint32_t n = p->n, L = p->ks_level;
+    k->lwe_sk = (uint64_t*)calloc(n, 8);
+    k->glwe_sk = (uint64_t*)calloc(FHO_N, 8);
+    k->ksk = (uint64_t*)calloc((size_t)FHO_N * L * (n + 1), 8);
+    k->bsk = (uint64_t*)calloc((size_t)n * 4 * FHO_N, 8);
+    k->bsk_f = (double*)calloc((size_t)n * 4 * FHO_HALF * 2, 8);
+    if (!k->lwe_sk || !k->glwe_sk || !k->ksk || !k->bsk || !k->bsk_f) return -1;
+
+    fho_rng r;
+    fho_rng_init(&r, seed, 1); /* secret keys */
+    for (uint32_t i = 0; i < n; ++i) k->lwe_sk[i] = fho_rng_u64(&r) & 1ull;
+    for (uint32_t j = 0; j < FHO_N; ++j) k->glwe_sk[j] = fho_rng_u64(&r) & 1ull;
+
+    fho_rng_init(&r, seed, 2); /* KSK: LWE_s(S_j * 2^(64 - b(l+1))) */
+    for (uint32_t j = 0; j < FHO_N; ++j) {
+        for (uint32_t l = 0; l < L; ++l) {
+            uint64_t* row = k->ksk + ((size_t)j * L + l) * (n + 1);
+            uint64_t dot = 0;
+            for (uint32_t t = 0; t < n; ++t) {
+                row[t] = fho_rng_u64(&r);
+                dot += row[t] * k->lwe_sk[t];
+            }
+            int64_t e = fho_rng_tuniform(&r, p->lwe_noise_log2);
+            uint64_t msg = k->glwe_sk[j] << (64 - p->ks_base_log * (l + 1));
+            row[n] = dot + msg + (uint64_t)e;
+        }
+    }
+
+    fho_rng_init(&r, seed, 3); /* BSK: GGSW_S(s_i), one level, base 2^pbs_base_log */
+    uint64_t* e = (uint64_t*)malloc(FHO_N * 8);
+    for (uint32_t i = 0; i < n; ++i) {
+        for (int row = 0; row < 2; ++row) {
+            uint64_t* A = k->bsk + (((size_t)i * 2 + row) * 2 + 0) * FHO_N;
+            uint64_t* B = k->bsk + (((size_t)i * 2 + row) * 2 + 1) * FHO_N;
+            for (int j = 0; j < FHO_N; ++j) A[j] = fho_rng_u64(&r);
+            for (int j = 0; j < FHO_N; ++j) e[j] = (uint64_t)fho_rng_tuniform(&r, p->glwe_noise_log2);
+            memcpy(B, e, FHO_N * 8);
+            poly_mul_binary_acc(B, A, k->glwe_sk);
+            uint64_t g = k->lwe_sk[i] << (64 - p->pbs_base_log);
+            if (row == 0) A[0] += g; else B[0] += g;
+        }
+    }
+    free(e);
+    for (size_t q = 0; q < (size_t)n * 4; ++q)
+        fho_poly_to_fourier(k->bsk + q * FHO_N, k->bsk_f + q * FHO_HALF * 2);
+    return 0;
+}
+
+void fho_keys_free(fho_keys* k) {
+    free(k->lwe_sk); free(k->glwe_sk); free(k->ksk); free(k->bsk); free(k->bsk_f);
+    memset(k, 0, sizeof *k);
+}
+
+/* ------------------------------------------------------------------ encrypt / decrypt */
+uint64_t fho_delta(const fho_params* p) {
+    return (1ull << 63) / ((uint64_t)p->message_modulus * p->carry_modulus);
+}
+
+void fho_encrypt_big(const fho_keys* k, fho_rng* r, uint64_t pt, uint64_t* ct) {
+    uint64_t dot = 0;
+    for (int j = 0; j < FHO_N; ++j) {
+        ct[j] = fho_rng_u64(r);
+        dot += ct[j] * k->glwe_sk[j];
+    }
+    int64_t e = fho_rng_tuniform(r, k->p.glwe_noise_log2);
+    ct[FHO_N] = dot + pt + (uint64_t)e;
+}
+
+uint64_t fho_decrypt_phase_big(const fho_keys* k, const uint64_t* ct) {
+    uint64_t dot = 0;
+    for (int j = 0; j < FHO_N; ++j) dot += ct[j] * k->glwe_sk[j];
+    return ct[FHO_N] - dot;
+}
+
+uint32_t fho_decode(const fho_params* p, uint64_t phase) {
+    uint64_t delta = fho_delta(p);
+    uint64_t mod = 2ull * p->message_modulus * p->carry_modulus; /* incl. padding bit */
+    return (uint32_t)(((phase + delta / 2) / delta) % mod);
+}
+
+/* ------------------------------------------------------------------ PBS pipeline */
+void fho_keyswitch(const fho_keys* k, const uint64_t* in, uint64_t* out) {
+    const uint32_t n = k->p.n, L = k->p.ks_level, bl = k->p.ks_base_log;
+    const uint32_t bits = bl * L;               /* 15 */
+    const uint64_t mask = (1ull << bits) - 1;
+    const int64_t base = 1ll << bl, halfb = base >> 1;
+    memset(out, 0, (n + 1) * 8);
+    out[n] = in[FHO_N];
+    int64_t d[16];
+    for (int j = 0; j < FHO_N; ++j) {
+        uint64_t v = (((in[j] >> (63 - bits)) + 1) >> 1) & mask; /* round to top `bits` bits */
+        for (int l = (int)L - 1; l >= 0; --l) {
+            int64_t dig = (int64_t)(v & (uint64_t)(base - 1));
+            v >>= bl;
+            if (dig >= halfb) { dig -= base; v += 1; }
+            d[l] = dig;
+        }
+        for (uint32_t l = 0; l < L; ++l) {
+            if (!d[l]) continue;
+            const uint64_t* row = k->ksk + ((size_t)j * L + l) * (n + 1);
+            uint64_t dd = (uint64_t)d[l];
+            for (uint32_t t = 0; t <= n; ++t) out[t] -= dd * row[t];
+        }
+    }
+}
+
+uint32_t fho_modswitch(uint64_t x) {
+    return (uint32_t)((((x >> 51) + 1) >> 1) & (2 * FHO_N - 1));
+}
+
+/* out = X^r * v (negacyclic), r in [0, 2N) */
+static void poly_rotate(const uint64_t* v, uint32_t r, uint64_t* out) {
+    for (int j = 0; j < FHO_N; ++j) {
+        int t = j - (int)r;
+        if (t >= 0) out[j] = v[t];
+        else if (t >= -FHO_N) out[j] = (uint64_t)0 - v[t + FHO_N];
+        else out[j] = v[t + 2 * FHO_N];
+    }
+}
+
+static inline int64_t decomp_pbs(uint64_t x, uint32_t base_log) {
+    const uint32_t sh = 64 - base_log;                 /* 41 */
+    uint64_t v = (((x >> (sh - 1)) + 1) >> 1) & ((1ull << base_log) - 1);
+    int64_t d = (int64_t)v;
+    if (d >= (1ll << (base_log - 1))) d -= (1ll << base_log);
+    return d;
+}
+
+void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_t* lut,
+                      uint64_t* glwe) {
+    const uint32_t n = k->p.n;
+    uint64_t* acc0 = glwe;            /* mask */
+    uint64_t* acc1 = glwe + FHO_N;    /* body */
+    uint64_t* rot = (uint64_t*)malloc(FHO_N * 8);
+    int64_t* dig = (int64_t*)malloc(FHO_N * 8);
+    double* D0 = (double*)malloc(FHO_HALF * 16);
+    double* D1 = (double*)malloc(FHO_HALF * 16);
+    double* O = (double*)malloc(FHO_HALF * 16);
+
+    uint32_t bt = fho_modswitch(ct_small[n]);
+    memset(acc0, 0, FHO_N * 8);
+    poly_rotate(lut, (2 * FHO_N - bt) & (2 * FHO_N - 1), acc1);
+
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t a = fho_modswitch(ct_small[i]);
+        if (a == 0) continue;
+        for (int m = 0; m < 2; ++m) {
+            uint64_t* acc = m ? acc1 : acc0;
+            poly_rotate(acc, a, rot);
+            for (int j = 0; j < FHO_N; ++j) dig[j] = decomp_pbs(rot[j] - acc[j], k->p.pbs_base_log);
+            fho_ipoly_to_fourier(dig, m ? D1 : D0);
+        }
+        const double* bi = k->bsk_f + (size_t)i * 4 * FHO_HALF * 2;
+        for (int w = 0; w < 2; ++w) {
+            const double* B0 = bi + (0 * 2 + w) * FHO_HALF * 2; /* row 0 (mask digit), poly w */
+            const double* B1 = bi + (1 * 2 + w) * FHO_HALF * 2; /* row 1 (body digit), poly w */
+            for (int q = 0; q < FHO_HALF; ++q) {
+                double d0r = D0[2 * q], d0i = D0[2 * q + 1], d1r = D1[2 * q], d1i = D1[2 * q + 1];
+                double b0r = B0[2 * q], b0i = B0[2 * q + 1], b1r = B1[2 * q], b1i = B1[2 * q + 1];
+                O[2 * q] = fma(d0r, b0r, fma(-d0i, b0i, fma(d1r, b1r, -(d1i * b1i))));
+                O[2 * q + 1] = fma(d0r, b0i, fma(d0i, b0r, fma(d1r, b1i, d1i * b1r)));
+            }
+            fho_fourier_add_to_poly(O, w ? acc1 : acc0);
+        }
+    }
+    free(rot); free(dig); free(D0); free(D1); free(O);
+}
+
+void fho_sample_extract(const uint64_t* glwe, uint64_t* ct) {
+    const uint64_t* A = glwe;
+    const uint64_t* B = glwe + FHO_N;
+    ct[0] = A[0];
+    for (int j = 1; j < FHO_N; ++j) ct[j] = (uint64_t)0 - A[FHO_N - j];
+    ct[FHO_N] = B[0];
+}
+
+void fho_pbs(const fho_keys* k, const uint64_t* in, const uint64_t* lut, uint64_t* out) {
+    uint64_t* small = (uint64_t*)malloc((k->p.n + 1) * 8);
+    uint64_t* glwe = (uint64_t*)malloc(2 * FHO_N * 8);
+    fho_keyswitch(k, in, small);
+    fho_blind_rotate(k, small, lut, glwe);
+    fho_sample_extract(glwe, out);
+    free(small); free(glwe);
+}
+
+void fho_pbs_batch(const fho_keys* k, const uint64_t* in, size_t count, const uint64_t* luts,
+                   const uint32_t* lut_index, uint64_t* out, int threads) {
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (long i = 0; i < (long)count; ++i)
+        fho_pbs(k, in + (size_t)i * (FHO_N + 1), luts + (size_t)(lut_index ? lut_index[i] : 0) * FHO_N,
+                out + (size_t)i * (FHO_N + 1));
+    (void)threads;
+}
+
+void fho_make_lut(const fho_params* p, const uint32_t* f, uint64_t* lut) {
+    const uint32_t mods = p->message_modulus * p->carry_modulus;
+    const uint32_t box = FHO_N / mods, half = box / 2;
+    const uint64_t delta = fho_delta(p);
+    uint64_t* tmp = (uint64_t*)malloc(FHO_N * 8);
+    for (uint32_t i = 0; i < mods; ++i)
+        for (uint32_t t = 0; t < box; ++t) tmp[i * box + t] = (uint64_t)(f[i] % mods) * delta;
+    for (uint32_t t = 0; t < half; ++t) tmp[t] = (uint64_t)0 - tmp[t];
+    for (int j = 0; j < FHO_N; ++j) lut[j] = tmp[(j + half) % FHO_N];
+    free(tmp);
+}

@@ -1,0 +1,60 @@
+"""Product keygen / encryption (fhe-sign_amd, C++) vs the oracle's restatement (C): byte-identical.
+
+Reference call sites: tfhe::generate_keys (src/schnorr.rs:441-442), FheUint32::try_encrypt
+(src/biguint.rs:26).  Key bytes against tfhe-rs itself: parity unpinned (no tfhe-rs fixture).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from fhe_sign import generate_keys
+
+SEED = 0x5EED_F11E
+
+
+@pytest.fixture(scope="module")
+def keys():
+    ck, sk = generate_keys(seed=SEED)
+    ok = oracle.OracleKeys(SEED)
+    return ck, sk, ok
+
+
+def test_secret_keys_identical(keys):
+    ck, _, ok = keys
+    lwe, glwe = ck.export()
+    assert np.array_equal(lwe, ok.lwe_sk)
+    assert np.array_equal(glwe, ok.glwe_sk)
+    assert set(np.unique(lwe)) <= {0, 1} and 300 < lwe.sum() < 534
+
+
+def test_server_keys_identical(keys):
+    _, sk, ok = keys
+    ksk, bsk = sk.export()
+    assert np.array_equal(ksk, ok.ksk)
+    assert np.array_equal(bsk, ok.bsk)
+
+
+def test_encryption_identical_and_decrypts(keys):
+    ck, _, ok = keys
+    ck.seed_encryption(77, 100)
+    r = ok.rng(77, 100)
+    for m in range(16):
+        a = ck.encrypt_block(m)
+        b = ok.encrypt(r, m)
+        assert np.array_equal(a, b)
+        assert ck.decrypt_block(a) == m
+        assert ok.decrypt(b) == m
+
+
+def test_ksk_rows_decrypt_to_gadget(keys):
+    """KSK[j][l] is an LWE encryption of S_j * 2^(64 - 3(l+1)) under the small key."""
+    _, _, ok = keys
+    n, L = ok.params.n, ok.params.ks_level
+    ksk = ok.ksk.reshape(2048, L, n + 1)
+    for j in (0, 1, 777, 2047):
+        for lv in range(L):
+            row = ksk[j, lv]
+            phase = (int(row[n]) - int(np.dot(row[:n].astype(object), ok.lwe_sk.astype(object)))) % 2**64
+            expect = (int(ok.glwe_sk[j]) << (64 - 3 * (lv + 1))) % 2**64
+            err = (phase - expect + 2**63) % 2**64 - 2**63
+            assert abs(err) <= 2**44

@@ -1,0 +1,85 @@
+"""The CPU oracle itself: FFT / negacyclic product / PBS correctness (test infrastructure).
+
+The oracle restates tfhe 0.10.0's PBS (published algorithm; crate absent).  Its
+known-answer checks are mathematical: the FFT must realise the exact negacyclic product up to
+rounding, and PBS(Enc(m), f) must decrypt to f(m) for every m.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+rng = np.random.default_rng(1234)
+
+
+def negacyclic(a, b):
+    n = len(a)
+    c = [0] * n
+    for i in range(n):
+        if a[i] == 0:
+            continue
+        for j in range(n):
+            k = i + j
+            if k < n:
+                c[k] += a[i] * b[j]
+            else:
+                c[k - n] -= a[i] * b[j]
+    return c
+
+
+def test_fft_roundtrip_exact_scaling():
+    x = rng.standard_normal(1024) + 1j * rng.standard_normal(1024)
+    y = oracle.fft_inverse(oracle.fft_forward(x)) / 1024
+    assert np.max(np.abs(y - x)) < 1e-12
+
+
+def test_fft_matches_numpy_dft():
+    x = rng.standard_normal(1024) + 1j * rng.standard_normal(1024)
+    f = oracle.fft_forward(x)
+    # DIF output is bit-reversed; twiddles are exp(+2 pi i k / 1024)
+    rev = np.array([int(format(i, "010b")[::-1], 2) for i in range(1024)])
+    ref = np.fft.ifft(x) * 1024
+    assert np.max(np.abs(f[rev] - ref)) < 1e-9
+
+
+def test_f64_to_torus():
+    assert oracle.f64_to_torus(0.0) == 0
+    assert oracle.f64_to_torus(-0.0) == 0
+    assert oracle.f64_to_torus(2.5) == 2          # half-even
+    assert oracle.f64_to_torus(3.5) == 4
+    assert oracle.f64_to_torus(-1.0) == 2**64 - 1
+    assert oracle.f64_to_torus(2.0**64) == 0
+    assert oracle.f64_to_torus(2.0**70 + 2.0**20) == 2**20
+    assert oracle.f64_to_torus(-(2.0**63)) == 2**63
+    assert oracle.f64_to_torus(1e30) == int(1e30) % 2**64
+
+
+@pytest.fixture(scope="module")
+def okeys():
+    return oracle.OracleKeys(99)
+
+
+def test_pbs_identity_and_square_all_messages(okeys):
+    r = okeys.rng(5)
+    f = [(m * m + 3) % 16 for m in range(16)]
+    lut = okeys.make_lut(f)
+    ident = okeys.make_lut(list(range(16)))
+    for m in range(16):
+        ct = okeys.encrypt(r, m)
+        assert okeys.decrypt(okeys.pbs(ct, lut)) == f[m]
+    for m in (0, 7, 15):
+        out = okeys.pbs(okeys.encrypt(r, m), ident)
+        assert okeys.decrypt(out) == m
+        noise = (okeys.phase(out) - m * okeys.delta() + 2**63) % 2**64 - 2**63
+        assert abs(noise) < 2**54  # fresh PBS noise far below delta/2 = 2^58
+
+
+def test_keyswitch_preserves_message(okeys):
+    r = okeys.rng(6)
+    n = okeys.params.n
+    for m in (0, 5, 11):
+        ct = okeys.encrypt(r, m)
+        small = okeys.keyswitch(ct)
+        phase = (int(small[n]) - int(np.dot(small[:n].astype(object), okeys.lwe_sk.astype(object)))) % 2**64
+        err = (phase - m * okeys.delta() + 2**63) % 2**64 - 2**63
+        assert abs(err) < 2**57
