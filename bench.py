@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X-native TFHE engine.
+
+Metric (BASELINE.json): "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds".
+A step = one batch of `--batch` programmable bootstraps (KS -> MS -> BR -> SE) over big-key LWE
+blocks already resident in HBM, i.e. one DAG level of the radix ops that BigUintFHE::mul issues
+(src/biguint.rs:223; the widest level of a 256-bit 8x8-limb mul is thousands of block PBS).
+`value` = PBS per second over all ranks.  Ranks are independent replicas of the batch
+(weak scaling; the path has no exchange step, so no data-path collective).
+
+Timed region: barrier + device sync, K steps, device sync + barrier; max over ranks.
+roofline: the dominant kernel (blind rotate) timed live with HIP events on the engine's stream;
+algorithmic f64 flops per PBS = n * 2^18, peak = FP64 vector rate.
+cpu_baseline: the C oracle (same algorithm, same parameters) on host cores, rank 0, N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds @1/2/4/8 GPU"
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector, spec (= FP32 vector rate / 2)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FLOPS_PER_CMUX = 4 * 51200 + 4 * 6144 + 32768   # 4 FFT-1024 (5 N log N), 4 twist/untwist, MAC
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=8192, help="PBS per step per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=0xF11E51)
+    return ap.parse_args()
+
+
+def dist_setup(n):
+    if n <= 1 and int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None, 0, 1, 0
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo")  # control plane only (barrier, max of times)
+    return dist, dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def allmax(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(seed, target_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    ok = oracle.OracleKeys(seed)
+    lut = ok.make_lut([(m + 1) % 16 for m in range(16)])[None, :]
+    r = ok.rng(3)
+    # calibrate with one PBS per thread, then size the sample to ~target_s
+    cts = np.stack([ok.encrypt(r, m % 16) for m in range(threads)])
+    t0 = time.perf_counter()
+    ok.pbs_batch(cts, lut, np.zeros(threads, np.uint32), threads)
+    per_round = time.perf_counter() - t0
+    rounds = max(1, int(target_s / max(per_round, 1e-3)))
+    count = threads * rounds
+    cts = np.concatenate([cts] * rounds)
+    t0 = time.perf_counter()
+    ok.pbs_batch(cts, lut, np.zeros(count, np.uint32), threads)
+    dt = time.perf_counter() - t0
+    return {"value": count / dt, "unit": "PBS/s", "cores": threads, "kind": "port",
+            "sample": f"{count} PBS (KS+BR+SE, same params/keys shape) with the C oracle, "
+                      f"OpenMP {threads} threads, {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    dist, rank, world, local = dist_setup(a.gpus)
+    from fhe_sign import Context, generate_keys
+
+    ck, sk = generate_keys(seed=a.seed)
+    ctx = Context(local)
+    ctx.set_server_key(sk)
+    n = sk.params.lwe_dimension
+    lid = ctx.lut([(m + 1) % 16 for m in range(16)])
+    B = a.batch
+    ck.seed_encryption(a.seed + rank, 100)
+    base = np.stack([ck.encrypt_block(m % 16) for m in range(256)])
+    reps = (B + 255) // 256
+    cts = np.ascontiguousarray(np.concatenate([base] * reps)[:B])
+    d_in = ctx.alloc(cts.nbytes)
+    d_out = ctx.alloc(cts.nbytes)
+    d_lut = ctx.alloc(B * 4)
+    ctx.h2d(d_in, cts)
+    ctx.h2d(d_lut, np.full(B, lid, np.uint32))
+
+    for _ in range(a.warmup):
+        ctx.pbs_device(d_in, B, d_lut, d_out)
+    ctx.sync()
+
+    # live per-kernel timing (HIP events on the engine stream) in separate untimed passes
+    ctx.enable_timing(True)
+    ks_t, br_t = [], []
+    for _ in range(max(2, min(a.steps, 5))):
+        ctx.pbs_device(d_in, B, d_lut, d_out)
+        ks, br = ctx.last_pbs_timing()
+        ks_t.append(ks)
+        br_t.append(br)
+    ctx.enable_timing(False)
+    ctx.sync()
+
+    barrier(dist)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctx.pbs_device(d_in, B, d_lut, d_out)
+    ctx.sync()
+    dt = time.perf_counter() - t0
+    barrier(dist)
+    dt = allmax(dist, dt)
+
+    # correctness spot check of the last step (decrypt a sample)
+    out = np.zeros_like(cts)
+    ctx.d2h(out, d_out)
+    ok = all(ck.decrypt_block(out[i]) == (i % 256 % 16 + 1) % 16 for i in range(0, B, max(1, B // 64)))
+    if not ok:
+        raise SystemExit("bench: decryption check failed")
+
+    total = world * B * a.steps
+    br_ms = float(np.mean(br_t))
+    ks_ms = float(np.mean(ks_t))
+    flops = B * n * FLOPS_PER_CMUX
+    achieved = flops / (br_ms * 1e-3) / 1e12
+    bsk_bytes = n * 4 * 1024 * 16
+    hbm_bytes = bsk_bytes + B * ((n + 1) * 2 + 2049 * 8 + 4)
+    res = {
+        "metric": METRIC,
+        "value": total / dt,
+        "unit": "PBS/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"batched programmable bootstrap (KS+MS+BR+SE) of {B} 2_2 radix blocks per GPU "
+                        "= one PBS level of BigUintFHE 256-bit mul (configs[1])",
+            "batch_pbs_per_gpu": B,
+            "params": f"n={n},N=2048,k=1,pbs=2^23x1,ks=2^3x5,msg=4,carry=4",
+            "parallelism": f"replicas x{world}",
+        },
+        "roofline": {
+            "bound": "valu_fp64",
+            "kernel": "k_blind_rotate",
+            "achieved": achieved,
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS,
+            "traffic": None,
+            "kernel_ms": br_ms,
+            "keyswitch_ms": ks_ms,
+            "hbm": {"bound": "hbm", "achieved": hbm_bytes / (br_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": hbm_bytes / (br_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    ctx.free(d_in)
+    ctx.free(d_out)
+    ctx.free(d_lut)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

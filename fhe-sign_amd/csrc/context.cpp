@@ -30,6 +30,22 @@ void fft_tables(std::vector<double2>* W, std::vector<double2>* psi) {
     (*psi)[0] = make_double2(1.0, 0.0);
 }
 
+void lane_twiddles(const std::vector<double2>& W, std::vector<double2>* Wl) {
+    // [slot][lane] copies of W entries, slot layout of device_math.h:tw_slot
+    Wl->assign(30 * 64, make_double2(0.0, 0.0));
+    for (int L = 0; L < 64; ++L) {
+        const int r = L >> 4;
+        for (int s = 0; s < 4; ++s) {
+            const int hd = 8 >> s;
+            for (int g = 0; g < hd; ++g) (*Wl)[(16 - 2 * hd + g) * 64 + L] = W[(L + 64 * g) << s];
+        }
+        for (int s = 4; s < 8; ++s) {
+            const int hd = 8 >> (s - 4);
+            for (int g = 0; g < hd; ++g) (*Wl)[(15 + 16 - 2 * hd + g) * 64 + L] = W[(r + 4 * g) << s];
+        }
+    }
+}
+
 void make_lut_poly(const Params& p, const uint32_t* f, std::vector<uint64_t>* lut) {
     const uint32_t mods = p.msg_carry();
     const uint32_t box = kPolySize / mods, half = box / 2;
@@ -237,8 +253,9 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
         return FHE_ERR_HIP;
     }
     for (auto& ev : c->ev) FHE_HIP_CHECK(hipEventCreate(&ev));
-    std::vector<double2> W, psi;
-    fft_tables(&W, &psi);
+    std::vector<double2> W0, W, psi;
+    fft_tables(&W0, &psi);
+    lane_twiddles(W0, &W);
     FHE_HIP_CHECK(hipMalloc(&c->d_W, W.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMalloc(&c->d_psi, psi.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_W, W.data(), W.size() * sizeof(double2), hipMemcpyHostToDevice));

@@ -23,6 +23,8 @@ void set_error(const std::string& msg);
 
 // Host-side FFT tables (bit-identical to oracle/tfhe_oracle.c:fho_tables_init).
 void fft_tables(std::vector<double2>* W, std::vector<double2>* psi);
+// Per-lane twiddle table [slot][lane] (device_math.h:tw_slot) built from W.
+void lane_twiddles(const std::vector<double2>& W, std::vector<double2>* Wl);
 // Accumulator polynomial of a univariate LUT (tfhe shortint box encoding, padding bit).
 void make_lut_poly(const Params& p, const uint32_t* f, std::vector<uint64_t>* lut);
 
@@ -35,7 +37,7 @@ struct fhe_ctx {
     fhe::Params p;
     uint64_t* d_ksk = nullptr;
     double2* d_bsk = nullptr;  // Fourier BSK, blind-rotate layout
-    double2* d_W = nullptr;
+    double2* d_W = nullptr;    // per-lane twiddle table [30][64]
     double2* d_psi = nullptr;
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;

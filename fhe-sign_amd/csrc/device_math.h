@@ -13,8 +13,9 @@
 //   phase A : lane L, reg t (0..15)          holds index L + 64 t          (DIF stages 0-3)
 //   phase B : lane (b = L&15, r = L>>4), u   holds index 64 b + r + 4 u    (DIF stages 4-7)
 //   phase C : lane L, reg R = 4 v + q        holds index 4 (L + 64 v) + q  (DIF stages 8-9)
-// Exchanges A<->B and B<->C go through a per-wave 16 KiB LDS region with XOR swizzles chosen so
-// the ds_read_b128 / ds_write_b128 lane groups hit distinct 16-byte bank slots.
+// Exchanges A<->B and B<->C go through a per-wave 17 KiB LDS region with padded layouts (one
+// 16-B pad per 64 resp. 16 entries) so that every per-lane address is lane_base + constant and
+// the ds_read_b128 16-lane groups hit (nearly) distinct 16-byte bank slots.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -64,18 +65,26 @@ FHE_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ---------------------------------------------------------------- swizzled LDS addressing
-FHE_DEV int swz_ab(int idx) { return idx ^ ((idx >> 6) & 15); }
-FHE_DEV int swz_bc(int idx) { return idx ^ ((idx >> 4) & 15); }
+// ---------------------------------------------------------------- padded LDS layouts
+// element idx of a 1024-point exchange lives at swz_ab(idx) (A<->B) or swz_bc(idx) (B<->C)
+constexpr int FFT_SCRATCH = 1024 + 64;  // complex entries per wave (17 KiB)
+FHE_DEV int swz_ab(int idx) { return idx + (idx >> 6); }
+FHE_DEV int swz_bc(int idx) { return idx + (idx >> 4); }
 
 // ---------------------------------------------------------------- forward FFT (DIF)
-FHE_DEV void dif_phase_a(cplx (&x)[16], int L, const cplx* __restrict__ W) {
+// Twiddles come from a per-lane table Wl[slot * 64] (Wl = table + lane), slot = tw_slot(s, g):
+// phase A (stages 0-3) slot(s, g) = 16 - 2 hd + g holds W[(L + 64 g) << s]; phase B (stages 4-7)
+// slot 15 + (16 - 2 hd + g) holds W[(r + 4 g) << s] (r = L >> 4).  Exact copies of W entries.
+constexpr int TW_SLOTS = 30;
+FHE_DEV int tw_slot(int hd, int g) { return 16 - 2 * hd + g; }
+
+FHE_DEV void dif_phase_a(cplx (&x)[16], const cplx* __restrict__ Wl) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int hd = 8 >> s;
 #pragma unroll
         for (int g = 0; g < hd; ++g) {  // distinct twiddles of this stage
-            const cplx w = W[(L + 64 * g) << s];
+            const cplx w = Wl[tw_slot(hd, g) * 64];
 #pragma unroll
             for (int t = g; t < 16; t += 2 * hd) {
                 cplx a = x[t], c = x[t + hd];
@@ -83,16 +92,17 @@ FHE_DEV void dif_phase_a(cplx (&x)[16], int L, const cplx* __restrict__ W) {
                 x[t + hd] = cmul(csub(a, c), w);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-FHE_DEV void dif_phase_b(cplx (&x)[16], int r, const cplx* __restrict__ W) {
+FHE_DEV void dif_phase_b(cplx (&x)[16], const cplx* __restrict__ Wl) {
 #pragma unroll
     for (int s = 4; s < 8; ++s) {
         const int hd = 8 >> (s - 4);
 #pragma unroll
         for (int g = 0; g < hd; ++g) {
-            const cplx w = W[(r + 4 * g) << s];
+            const cplx w = Wl[(15 + tw_slot(hd, g)) * 64];
 #pragma unroll
             for (int u = g; u < 16; u += 2 * hd) {
                 cplx a = x[u], c = x[u + hd];
@@ -100,6 +110,7 @@ FHE_DEV void dif_phase_b(cplx (&x)[16], int r, const cplx* __restrict__ W) {
                 x[u + hd] = cmul(csub(a, c), w);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -132,13 +143,13 @@ FHE_DEV void dit_phase_c(cplx (&x)[16]) {
     }
 }
 
-FHE_DEV void dit_phase_b(cplx (&x)[16], int r, const cplx* __restrict__ W) {
+FHE_DEV void dit_phase_b(cplx (&x)[16], const cplx* __restrict__ Wl) {
 #pragma unroll
     for (int s = 7; s >= 4; --s) {
         const int hd = 8 >> (s - 4);
 #pragma unroll
         for (int g = 0; g < hd; ++g) {
-            const cplx w = conj_(W[(r + 4 * g) << s]);
+            const cplx w = conj_(Wl[(15 + tw_slot(hd, g)) * 64]);
 #pragma unroll
             for (int u = g; u < 16; u += 2 * hd) {
                 cplx a = x[u], c = cmul(x[u + hd], w);
@@ -146,16 +157,17 @@ FHE_DEV void dit_phase_b(cplx (&x)[16], int r, const cplx* __restrict__ W) {
                 x[u + hd] = csub(a, c);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-FHE_DEV void dit_phase_a(cplx (&x)[16], int L, const cplx* __restrict__ W) {
+FHE_DEV void dit_phase_a(cplx (&x)[16], const cplx* __restrict__ Wl) {
 #pragma unroll
     for (int s = 3; s >= 0; --s) {
         const int hd = 8 >> s;
 #pragma unroll
         for (int g = 0; g < hd; ++g) {
-            const cplx w = conj_(W[(L + 64 * g) << s]);
+            const cplx w = conj_(Wl[tw_slot(hd, g) * 64]);
 #pragma unroll
             for (int t = g; t < 16; t += 2 * hd) {
                 cplx a = x[t], c = cmul(x[t + hd], w);
@@ -163,64 +175,74 @@ FHE_DEV void dit_phase_a(cplx (&x)[16], int L, const cplx* __restrict__ W) {
                 x[t + hd] = csub(a, c);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // ---------------------------------------------------------------- exchanges (per-wave LDS)
+// Padded addresses written out as lane_base + constant so the compiler emits one base VGPR and
+// ds_* immediate offsets:
+//   swz_ab(L + 64 t)          = L + 65 t
+//   swz_ab(64 b + r + 4 u)    = (65 b + r) + 4 u
+//   swz_bc(64 b + r + 4 u)    = (68 b + r) + 4 u + (u >> 2)
+//   swz_bc(4 (L + 64 v) + q)  = (4 L + (L >> 2)) + 272 v + q
 FHE_DEV void xchg_a_to_b(cplx (&x)[16], cplx* sc, int L) {
 #pragma unroll
-    for (int t = 0; t < 16; ++t) sc[swz_ab(L + 64 * t)] = x[t];
+    for (int t = 0; t < 16; ++t) sc[L + 65 * t] = x[t];
     wave_sync();
-    const int b = L & 15, r = L >> 4;
+    const cplx* rb = sc + 65 * (L & 15) + (L >> 4);
 #pragma unroll
-    for (int u = 0; u < 16; ++u) x[u] = sc[swz_ab(64 * b + r + 4 * u)];
+    for (int u = 0; u < 16; ++u) x[u] = rb[4 * u];
     wave_sync();
 }
 FHE_DEV void xchg_b_to_a(cplx (&x)[16], cplx* sc, int L) {
-    const int b = L & 15, r = L >> 4;
+    cplx* wb = sc + 65 * (L & 15) + (L >> 4);
 #pragma unroll
-    for (int u = 0; u < 16; ++u) sc[swz_ab(64 * b + r + 4 * u)] = x[u];
+    for (int u = 0; u < 16; ++u) wb[4 * u] = x[u];
     wave_sync();
 #pragma unroll
-    for (int t = 0; t < 16; ++t) x[t] = sc[swz_ab(L + 64 * t)];
+    for (int t = 0; t < 16; ++t) x[t] = sc[L + 65 * t];
     wave_sync();
 }
 FHE_DEV void xchg_b_to_c(cplx (&x)[16], cplx* sc, int L) {
-    const int b = L & 15, r = L >> 4;
+    cplx* wb = sc + 68 * (L & 15) + (L >> 4);
 #pragma unroll
-    for (int u = 0; u < 16; ++u) sc[swz_bc(64 * b + r + 4 * u)] = x[u];
+    for (int u = 0; u < 16; ++u) wb[4 * u + (u >> 2)] = x[u];
     wave_sync();
+    const cplx* rb = sc + 4 * L + (L >> 2);
 #pragma unroll
     for (int v = 0; v < 4; ++v)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x[4 * v + q] = sc[swz_bc(4 * (L + 64 * v) + q)];
+        for (int q = 0; q < 4; ++q) x[4 * v + q] = rb[272 * v + q];
     wave_sync();
 }
 FHE_DEV void xchg_c_to_b(cplx (&x)[16], cplx* sc, int L) {
+    cplx* wb = sc + 4 * L + (L >> 2);
 #pragma unroll
     for (int v = 0; v < 4; ++v)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sc[swz_bc(4 * (L + 64 * v) + q)] = x[4 * v + q];
+        for (int q = 0; q < 4; ++q) wb[272 * v + q] = x[4 * v + q];
     wave_sync();
-    const int b = L & 15, r = L >> 4;
+    const cplx* rb = sc + 68 * (L & 15) + (L >> 4);
 #pragma unroll
-    for (int u = 0; u < 16; ++u) x[u] = sc[swz_bc(64 * b + r + 4 * u)];
+    for (int u = 0; u < 16; ++u) x[u] = rb[4 * u + (u >> 2)];
     wave_sync();
 }
 
 // natural-order (phase A) input -> bit-reversed output held in phase C layout
-FHE_DEV void fft_forward(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ W) {
-    dif_phase_a(x, L, W);
+// Wl = per-lane twiddle table + L (see tw_slot)
+FHE_DEV void fft_forward(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ Wl) {
+    dif_phase_a(x, Wl);
     xchg_a_to_b(x, sc, L);
-    dif_phase_b(x, L >> 4, W);
+    dif_phase_b(x, Wl);
     xchg_b_to_c(x, sc, L);
     dif_phase_c(x);
 }
 // phase C layout (bit-reversed) -> natural order in phase A layout, unscaled
-FHE_DEV void fft_inverse(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ W) {
+FHE_DEV void fft_inverse(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ Wl) {
     dit_phase_c(x);
     xchg_c_to_b(x, sc, L);
-    dit_phase_b(x, L >> 4, W);
+    dit_phase_b(x, Wl);
     xchg_b_to_a(x, sc, L);
-    dit_phase_a(x, L, W);
+    dit_phase_a(x, Wl);
 }

@@ -87,14 +87,14 @@ __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ 
 // digit polynomials through LDS once per CMUX.
 constexpr int BR_PBS_BL = 23;
 
-__global__ __launch_bounds__(128) void k_blind_rotate(const uint16_t* __restrict__ ms, int ms_stride,
+__global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restrict__ ms, int ms_stride,
                                                      const uint32_t* __restrict__ lut_idx,
                                                      const uint64_t* __restrict__ luts,
                                                      const cplx* __restrict__ bsk,
                                                      const cplx* __restrict__ W,
                                                      const cplx* __restrict__ psi,
                                                      uint64_t* __restrict__ out, int n) {
-    __shared__ __attribute__((aligned(16))) cplx lds[2][1024];
+    __shared__ __attribute__((aligned(16))) cplx lds[2][FFT_SCRATCH];
     const int ct = blockIdx.x;
     const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
     cplx* sc = lds[w];
@@ -111,10 +111,9 @@ __global__ __launch_bounds__(128) void k_blind_rotate(const uint16_t* __restrict
         for (int t = 0; t < 32; ++t) {
             uint64_t v = 0;
             if (w == 1) {
-                int jj = L + 64 * t - rot;
-                if (jj >= 0) v = lut[jj];
-                else if (jj >= -2048) v = 0ull - lut[jj + 2048];
-                else v = lut[jj + 4096];
+                const uint32_t u = (uint32_t)(L + 64 * t - rot) & 4095u;
+                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
+                v = (lut[u & 2047u] ^ neg) - neg;
             }
             acc[t] = v;
         }
@@ -125,6 +124,11 @@ __global__ __launch_bounds__(128) void k_blind_rotate(const uint16_t* __restrict
         const uint32_t a = a_next;
         a_next = a_ct[i + 1];
         if (a == 0) continue;  // X^0 - 1 = 0: the external product is exactly zero
+        // Keep the twiddle / twist tables out of the register file: re-derive their base pointers
+        // every iteration so their (L1-resident) loads are not hoisted out of the loop.
+        const cplx* Wi = W;
+        const cplx* psii = psi;
+        asm volatile("" : "+s"(Wi), "+s"(psii));
 
         // ---- rotate, subtract, decompose, twist
 #pragma unroll
@@ -137,19 +141,19 @@ __global__ __launch_bounds__(128) void k_blind_rotate(const uint16_t* __restrict
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
                 const int tt = t + 16 * hh;
-                int jj = L + 64 * tt - (int)a;
-                uint64_t v;
-                if (jj >= 0) v = scu[jj];
-                else if (jj >= -2048) v = 0ull - scu[jj + 2048];
-                else v = scu[jj + 4096];
+                // (X^a acc)[j]: u = (j - a) mod 2N -> acc[u mod N], negated iff u >= N
+                const uint32_t u = (uint32_t)(L + 64 * tt - (int)a) & 4095u;
+                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
+                const uint64_t v = (scu[u & 2047u] ^ neg) - neg;
                 d2[hh] = decomp1<BR_PBS_BL>(v - acc[tt]);
             }
-            x[t] = cmul(make_double2((double)d2[0], (double)d2[1]), psi[L + 64 * t]);
+            x[t] = cmul(make_double2((double)d2[0], (double)d2[1]), psii[L + 64 * t]);
+            if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         wave_sync();
 
         // ---- forward FFT of this wave's digit polynomial
-        fft_forward(x, sc, L, W);
+        fft_forward(x, sc, L, Wi + L);
 
         // ---- swap Fourier digits with the partner wave, pointwise MAC with the BSK
 #pragma unroll
@@ -169,19 +173,21 @@ __global__ __launch_bounds__(128) void k_blind_rotate(const uint16_t* __restrict
                 o.x = __fma_rn(d0.x, B0.x, __fma_rn(-d0.y, B0.y, __fma_rn(d1.x, B1.x, -(d1.y * B1.y))));
                 o.y = __fma_rn(d0.x, B0.y, __fma_rn(d0.y, B0.x, __fma_rn(d1.x, B1.y, d1.y * B1.x)));
                 x[R] = o;
+                if ((R & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
         }
         __syncthreads();
 
         // ---- inverse FFT, untwist, round, accumulate
-        fft_inverse(x, sc, L, W);
+        fft_inverse(x, sc, L, Wi + L);
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-            const cplx p = psi[L + 64 * t];
+            const cplx p = psii[L + 64 * t];
             const cplx u = make_double2(p.x * 0.0009765625, -p.y * 0.0009765625);
             const cplx y = cmul(x[t], u);
             acc[t] += f64_to_torus(y.x);
             acc[t + 16] += f64_to_torus(y.y);
+            if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
     }
 
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(64) void k_bsk_to_fourier(const uint64_t* __restric
                                                        const cplx* __restrict__ W,
                                                        const cplx* __restrict__ psi,
                                                        cplx* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) cplx sc[1024];
+    __shared__ __attribute__((aligned(16))) cplx sc[FFT_SCRATCH];
     const int q = blockIdx.x;
     if (q >= npoly) return;
     const int L = threadIdx.x;
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(64) void k_bsk_to_fourier(const uint64_t* __restric
         const double im = (double)(int64_t)p[L + 64 * t + 1024];
         x[t] = cmul(make_double2(re, im), psi[L + 64 * t]);
     }
-    fft_forward(x, sc, L, W);
+    fft_forward(x, sc, L, W + L);
     cplx* o = out + (size_t)q * 1024 + L;
 #pragma unroll
     for (int R = 0; R < 16; ++R) o[R * 64] = x[R];
