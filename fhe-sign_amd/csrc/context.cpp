@@ -34,7 +34,7 @@ void lane_twiddles(const std::vector<double2>& W, std::vector<double2>* Wl) {
     // [slot][lane] copies of W entries, slot layout of device_math.h:tw_slot
     Wl->assign(30 * 64, make_double2(0.0, 0.0));
     for (int L = 0; L < 64; ++L) {
-        const int r = L >> 4;
+        const int r = L & 3;  // phase-B lane mapping b = L >> 2, r = L & 3
         for (int s = 0; s < 4; ++s) {
             const int hd = 8 >> s;
             for (int g = 0; g < hd; ++g) (*Wl)[(16 - 2 * hd + g) * 64 + L] = W[(L + 64 * g) << s];

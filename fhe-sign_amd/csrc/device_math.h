@@ -11,11 +11,14 @@
 //
 // FFT register layout (one wave64 owns one 1024-point complex FFT, 16 points per lane):
 //   phase A : lane L, reg t (0..15)          holds index L + 64 t          (DIF stages 0-3)
-//   phase B : lane (b = L&15, r = L>>4), u   holds index 64 b + r + 4 u    (DIF stages 4-7)
+//   phase B : lane (b = L>>2, r = L&3), u    holds index 64 b + r + 4 u    (DIF stages 4-7)
 //   phase C : lane L, reg R = 4 v + q        holds index 4 (L + 64 v) + q  (DIF stages 8-9)
-// Exchanges A<->B and B<->C go through a per-wave 17 KiB LDS region with padded layouts (one
-// 16-B pad per 64 resp. 16 entries) so that every per-lane address is lane_base + constant and
-// the ds_read_b128 16-lane groups hit (nearly) distinct 16-byte bank slots.
+// Exchanges A<->B and B<->C go through a per-wave 17 KiB LDS region with padded layouts
+// (A<->B: idx + 4 (idx >> 6); B<->C: idx + (idx >> 4)) so every per-lane address is
+// lane_base + constant and, under gfx950's lane-group banking (ds_read_b128: four 16-lane groups
+// over 16 slots; ds_write_b128: eight 8-lane groups over 8 slots), all accesses are conflict-free
+// except the C-side store of the inverse FFT (2-way; chosen by exhaustive search over paddings and
+// lane-bit permutations, tools/lds_layout_search.py).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -38,12 +41,18 @@ FHE_DEV cplx mul_i(cplx x) { return make_double2(-x.y, x.x); }
 FHE_DEV cplx mul_negi(cplx x) { return make_double2(x.y, -x.x); }
 
 FHE_DEV uint64_t f64_to_torus(double x) {
-    double r = __builtin_rint(x);
-    uint64_t b = (uint64_t)__double_as_longlong(r);
-    int e = (int)((b >> 52) & 0x7ff) - 1075;
-    uint64_t m = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
-    uint64_t v = (e >= 0) ? ((e < 64) ? (m << e) : 0ull) : ((e > -53) ? (m >> (-e)) : 0ull);
-    return (b >> 63) ? (0ull - v) : v;
+    // round to nearest (even), then the integer value mod 2^64 from mantissa/exponent; written
+    // with selects only (no divergent branches).  Identical function to the oracle's.
+    const double r = __builtin_rint(x);
+    const uint64_t b = (uint64_t)__double_as_longlong(r);
+    const int e = (int)((b >> 52) & 0x7ff) - 1075;
+    const uint64_t m = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
+    const uint64_t vl = m << (e & 63);
+    const uint64_t vr = m >> ((-e) & 63);
+    uint64_t v = (e >= 0) ? vl : vr;
+    v = ((unsigned)(e + 52) <= 115u) ? v : 0ull;  // keep e in [-52, 63]
+    const uint64_t neg = 0ull - (b >> 63);
+    return (v ^ neg) - neg;
 }
 
 // gadget decomposition, one level, base 2^BL, balanced digit in [-2^(BL-1), 2^(BL-1))
@@ -68,13 +77,13 @@ FHE_DEV void wave_sync() {
 // ---------------------------------------------------------------- padded LDS layouts
 // element idx of a 1024-point exchange lives at swz_ab(idx) (A<->B) or swz_bc(idx) (B<->C)
 constexpr int FFT_SCRATCH = 1024 + 64;  // complex entries per wave (17 KiB)
-FHE_DEV int swz_ab(int idx) { return idx + (idx >> 6); }
+FHE_DEV int swz_ab(int idx) { return idx + 4 * (idx >> 6); }
 FHE_DEV int swz_bc(int idx) { return idx + (idx >> 4); }
 
 // ---------------------------------------------------------------- forward FFT (DIF)
 // Twiddles come from a per-lane table Wl[slot * 64] (Wl = table + lane), slot = tw_slot(s, g):
 // phase A (stages 0-3) slot(s, g) = 16 - 2 hd + g holds W[(L + 64 g) << s]; phase B (stages 4-7)
-// slot 15 + (16 - 2 hd + g) holds W[(r + 4 g) << s] (r = L >> 4).  Exact copies of W entries.
+// slot 15 + (16 - 2 hd + g) holds W[(r + 4 g) << s] (r = L & 3).  Exact copies of W entries.
 constexpr int TW_SLOTS = 30;
 FHE_DEV int tw_slot(int hd, int g) { return 16 - 2 * hd + g; }
 
@@ -92,7 +101,6 @@ FHE_DEV void dif_phase_a(cplx (&x)[16], const cplx* __restrict__ Wl) {
                 x[t + hd] = cmul(csub(a, c), w);
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -110,7 +118,6 @@ FHE_DEV void dif_phase_b(cplx (&x)[16], const cplx* __restrict__ Wl) {
                 x[u + hd] = cmul(csub(a, c), w);
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -157,7 +164,6 @@ FHE_DEV void dit_phase_b(cplx (&x)[16], const cplx* __restrict__ Wl) {
                 x[u + hd] = csub(a, c);
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -175,37 +181,37 @@ FHE_DEV void dit_phase_a(cplx (&x)[16], const cplx* __restrict__ Wl) {
                 x[t + hd] = csub(a, c);
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // ---------------------------------------------------------------- exchanges (per-wave LDS)
-// Padded addresses written out as lane_base + constant so the compiler emits one base VGPR and
-// ds_* immediate offsets:
-//   swz_ab(L + 64 t)          = L + 65 t
-//   swz_ab(64 b + r + 4 u)    = (65 b + r) + 4 u
+// Padded addresses written out as lane_base + constant (one base VGPR, ds_* immediate offsets):
+//   swz_ab(L + 64 t)          = L + 68 t
+//   swz_ab(64 b + r + 4 u)    = (68 b + r) + 4 u
 //   swz_bc(64 b + r + 4 u)    = (68 b + r) + 4 u + (u >> 2)
 //   swz_bc(4 (L + 64 v) + q)  = (4 L + (L >> 2)) + 272 v + q
+FHE_DEV int lane_b_base(int L) { return 68 * (L >> 2) + (L & 3); }
+
 FHE_DEV void xchg_a_to_b(cplx (&x)[16], cplx* sc, int L) {
 #pragma unroll
-    for (int t = 0; t < 16; ++t) sc[L + 65 * t] = x[t];
+    for (int t = 0; t < 16; ++t) sc[L + 68 * t] = x[t];
     wave_sync();
-    const cplx* rb = sc + 65 * (L & 15) + (L >> 4);
+    const cplx* rb = sc + lane_b_base(L);
 #pragma unroll
     for (int u = 0; u < 16; ++u) x[u] = rb[4 * u];
     wave_sync();
 }
 FHE_DEV void xchg_b_to_a(cplx (&x)[16], cplx* sc, int L) {
-    cplx* wb = sc + 65 * (L & 15) + (L >> 4);
+    cplx* wb = sc + lane_b_base(L);
 #pragma unroll
     for (int u = 0; u < 16; ++u) wb[4 * u] = x[u];
     wave_sync();
 #pragma unroll
-    for (int t = 0; t < 16; ++t) x[t] = sc[L + 65 * t];
+    for (int t = 0; t < 16; ++t) x[t] = sc[L + 68 * t];
     wave_sync();
 }
 FHE_DEV void xchg_b_to_c(cplx (&x)[16], cplx* sc, int L) {
-    cplx* wb = sc + 68 * (L & 15) + (L >> 4);
+    cplx* wb = sc + lane_b_base(L);
 #pragma unroll
     for (int u = 0; u < 16; ++u) wb[4 * u + (u >> 2)] = x[u];
     wave_sync();
@@ -223,13 +229,12 @@ FHE_DEV void xchg_c_to_b(cplx (&x)[16], cplx* sc, int L) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) wb[272 * v + q] = x[4 * v + q];
     wave_sync();
-    const cplx* rb = sc + 68 * (L & 15) + (L >> 4);
+    const cplx* rb = sc + lane_b_base(L);
 #pragma unroll
     for (int u = 0; u < 16; ++u) x[u] = rb[4 * u + (u >> 2)];
     wave_sync();
 }
 
-// natural-order (phase A) input -> bit-reversed output held in phase C layout
 // Wl = per-lane twiddle table + L (see tw_slot)
 FHE_DEV void fft_forward(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ Wl) {
     dif_phase_a(x, Wl);

@@ -87,6 +87,24 @@ __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ 
 // digit polynomials through LDS once per CMUX.
 constexpr int BR_PBS_BL = 23;
 
+// out[R] = D0[R] * B0[R] + D1[R] * B1[R] (fused chain identical to the oracle), in place in x.
+template <bool OWN_IS_MASK>
+FHE_DEV void pointwise_mac(cplx (&x)[16], const cplx* __restrict__ other,
+                           const cplx* __restrict__ b0, const cplx* __restrict__ b1) {
+#pragma unroll
+    for (int R = 0; R < 16; ++R) {
+        const cplx mine = x[R];
+        const cplx oth = other[R * 64];
+        const cplx d0 = OWN_IS_MASK ? mine : oth;
+        const cplx d1 = OWN_IS_MASK ? oth : mine;
+        const cplx B0 = b0[R * 64], B1 = b1[R * 64];
+        cplx o;
+        o.x = __fma_rn(d0.x, B0.x, __fma_rn(-d0.y, B0.y, __fma_rn(d1.x, B1.x, -(d1.y * B1.y))));
+        o.y = __fma_rn(d0.x, B0.y, __fma_rn(d0.y, B0.x, __fma_rn(d1.x, B1.y, d1.y * B1.x)));
+        x[R] = o;
+    }
+}
+
 __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restrict__ ms, int ms_stride,
                                                      const uint32_t* __restrict__ lut_idx,
                                                      const uint64_t* __restrict__ luts,
@@ -160,21 +178,14 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restr
         for (int R = 0; R < 16; ++R) sc[R * 64 + L] = x[R];
         __syncthreads();
         {
-            const cplx* b0 = bsk + ((size_t)((i * 2 + 0) * 2 + w) * 16) * 64 + L;  // row 0 (mask digit)
-            const cplx* b1 = bsk + ((size_t)((i * 2 + 1) * 2 + w) * 16) * 64 + L;  // row 1 (body digit)
-#pragma unroll
-            for (int R = 0; R < 16; ++R) {
-                const cplx mine = x[R];
-                const cplx other = sc_other[R * 64 + L];
-                const cplx d0 = (w == 0) ? mine : other;
-                const cplx d1 = (w == 0) ? other : mine;
-                const cplx B0 = b0[R * 64], B1 = b1[R * 64];
-                cplx o;
-                o.x = __fma_rn(d0.x, B0.x, __fma_rn(-d0.y, B0.y, __fma_rn(d1.x, B1.x, -(d1.y * B1.y))));
-                o.y = __fma_rn(d0.x, B0.y, __fma_rn(d0.y, B0.x, __fma_rn(d1.x, B1.y, d1.y * B1.x)));
-                x[R] = o;
-                if ((R & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-            }
+            // row 0 multiplies the mask digits D0, row 1 the body digits D1 (oracle order); the
+            // branch is wave-uniform so both waves evaluate the identical expression tree.
+            const cplx* b0 = bsk + ((size_t)((i * 2 + 0) * 2 + w) * 16) * 64 + L;
+            const cplx* b1 = bsk + ((size_t)((i * 2 + 1) * 2 + w) * 16) * 64 + L;
+            if (__builtin_amdgcn_readfirstlane(w) == 0)
+                pointwise_mac<true>(x, sc_other + L, b0, b1);
+            else
+                pointwise_mac<false>(x, sc_other + L, b0, b1);
         }
         __syncthreads();
 
