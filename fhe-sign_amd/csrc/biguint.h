@@ -1,0 +1,28 @@
+// biguint.h -- BigUintFHE: encrypted unsigned big integer as LSB-first FheUint32 limbs
+// (reference: src/biguint.rs:8-13).  add/mul follow src/biguint.rs:120-265.
+#pragma once
+#include "radix.h"
+
+namespace fhe {
+
+constexpr uint32_t kLimbBlocks = 16;  // FheUint32 = 16 radix blocks
+
+struct BigUint {
+    std::vector<Radix> digits;  // each kLimbBlocks blocks
+};
+
+enum BigUintMode : int {
+    // Exact replay of the reference's limb loop, including the wrapping 32-bit add into
+    // result[idx+2] at src/biguint.rs:247-249 (a carry can be lost there).  Each reference
+    // step (i,j) is the window update R[idx..idx+3) += a_i*b_j mod 2^96 (mod 2^64 when
+    // idx+2 == len), which is the composition of the reference's FheUint64 adds and splits.
+    kCompat = 0,
+    // True product / sum with one wide carry propagation (differs from kCompat only on inputs
+    // where the reference loses a carry).
+    kFast = 1,
+};
+
+BigUint biguint_add(Engine& e, const BigUint& a, const BigUint& b, int mode);
+BigUint biguint_mul(Engine& e, const BigUint& a, const BigUint& b, int mode);
+
+}  // namespace fhe

@@ -1,0 +1,397 @@
+// capi_radix.cpp -- C ABI for radix integers (FheUint<N>) and BigUintFHE.
+#include <cstring>
+#include <stdexcept>
+
+#include "biguint.h"
+#include "fhe_rocm.h"
+
+struct fhe_radix {
+    fhe::Radix r;
+    uint32_t bits = 0;
+};
+
+struct fhe_biguint {
+    fhe::BigUint v;
+};
+
+using namespace fhe;
+
+namespace {
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return FHE_ERR_INVALID;
+    }
+}
+
+int need_engine(fhe_ctx* c) {
+    if (!c) {
+        set_error("null context");
+        return FHE_ERR_INVALID;
+    }
+    if (!c->has_key || !c->engine) {
+        set_error("no server key installed (fhe_set_server_key)");
+        return FHE_ERR_NO_KEY;
+    }
+    if (hipSetDevice(c->device) != hipSuccess) {
+        set_error("hipSetDevice failed");
+        return FHE_ERR_HIP;
+    }
+    return FHE_OK;
+}
+
+uint32_t word_bits(const uint64_t* w, uint32_t bit, uint32_t nbits_total) {
+    if (bit >= nbits_total) return 0;
+    return (uint32_t)(w[bit / 64] >> (bit % 64)) & 3u;
+}
+
+fhe_radix* wrap(Radix r, uint32_t bits) {
+    auto* x = new fhe_radix();
+    x->r = std::move(r);
+    x->bits = bits;
+    return x;
+}
+
+bool valid_bits(uint32_t bits) { return bits >= 2 && bits <= 128 && bits % 2 == 0; }
+
+// run a binary op on two radix of equal width
+template <class F>
+int binop(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out, F&& f) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !b || !out) return FHE_ERR_INVALID;
+    if (a->bits != b->bits) {
+        set_error("operands must have the same bit width");
+        return FHE_ERR_INVALID;
+    }
+    return guarded([&] {
+        *out = wrap(f(*c->engine, a->r, b->r), a->bits);
+        return FHE_OK;
+    });
+}
+
+template <class F>
+int unop(fhe_ctx* c, const fhe_radix* a, fhe_radix** out, F&& f) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !out) return FHE_ERR_INVALID;
+    return guarded([&] {
+        *out = wrap(f(*c->engine, a->r), a->bits);
+        return FHE_OK;
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int fhe_radix_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint64_t* words, uint32_t bits, fhe_radix** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!ck || !words || !out || !valid_bits(bits)) {
+        set_error("invalid arguments to fhe_radix_encrypt");
+        return FHE_ERR_INVALID;
+    }
+    return guarded([&] {
+        Radix r;
+        std::vector<uint64_t> ct(kBigCt);
+        for (uint32_t k = 0; k < bits / 2; ++k) {
+            const uint32_t m = word_bits(words, 2 * k, bits);
+            encrypt_big(ck, (uint64_t)m * ck->params.delta(), ct.data());
+            r.blocks.push_back(c->engine->upload(ct.data(), 3));
+        }
+        *out = wrap(std::move(r), bits);
+        return FHE_OK;
+    });
+}
+
+int fhe_radix_trivial(fhe_ctx* c, const uint64_t* words, uint32_t bits, fhe_radix** out) {
+    if (!c || !words || !out || !valid_bits(bits)) return FHE_ERR_INVALID;
+    Radix r;
+    for (uint32_t k = 0; k < bits / 2; ++k) r.blocks.push_back(Block::make_trivial(word_bits(words, 2 * k, bits)));
+    *out = wrap(std::move(r), bits);
+    return FHE_OK;
+}
+
+int fhe_radix_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_radix* x, uint64_t* words, size_t nwords) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!ck || !x || !words || nwords * 64 < x->bits) {
+        set_error("invalid arguments to fhe_radix_decrypt");
+        return FHE_ERR_INVALID;
+    }
+    return guarded([&] {
+        std::memset(words, 0, nwords * 8);
+        std::vector<uint64_t> ct(kBigCt);
+        // value = sum v_k 4^k mod 2^bits (v_k incl. carry bits)
+        unsigned __int128 lo = 0;  // bits < 128 handled by accumulating per block
+        std::vector<uint32_t> vals(x->r.nblocks());
+        for (uint32_t k = 0; k < x->r.nblocks(); ++k) {
+            const Block& b = x->r.blocks[k];
+            if (b.trivial())
+                vals[k] = b.value;
+            else {
+                c->engine->download(b, ct.data());
+                vals[k] = (uint32_t)decode_block(ck->params, decrypt_phase_big(ck, ct.data()));
+            }
+        }
+        // big-integer accumulate in 64-bit words
+        std::vector<uint64_t> acc((x->bits + 63) / 64 + 2, 0);
+        for (uint32_t k = 0; k < vals.size(); ++k) {
+            unsigned __int128 add = vals[k];
+            uint32_t bit = 2 * k;
+            size_t w = bit / 64;
+            add <<= (bit % 64);
+            while (add && w < acc.size()) {
+                unsigned __int128 s = (unsigned __int128)acc[w] + (uint64_t)add;
+                acc[w] = (uint64_t)s;
+                add = (add >> 64) + (s >> 64);
+                ++w;
+            }
+        }
+        (void)lo;
+        for (size_t w = 0; w < nwords && w < acc.size(); ++w) words[w] = acc[w];
+        // wrap mod 2^bits
+        const uint32_t top = x->bits;
+        for (size_t w = 0; w < nwords; ++w) {
+            const uint32_t lo_bit = (uint32_t)w * 64;
+            if (lo_bit >= top)
+                words[w] = 0;
+            else if (top - lo_bit < 64)
+                words[w] &= (1ull << (top - lo_bit)) - 1;
+        }
+        return FHE_OK;
+    });
+}
+
+int fhe_radix_num_bits(const fhe_radix* x, uint32_t* bits) {
+    if (!x || !bits) return FHE_ERR_INVALID;
+    *bits = x->bits;
+    return FHE_OK;
+}
+
+int fhe_radix_clone(const fhe_radix* x, fhe_radix** out) {
+    if (!x || !out) return FHE_ERR_INVALID;
+    *out = new fhe_radix(*x);
+    return FHE_OK;
+}
+
+void fhe_radix_destroy(fhe_radix* x) { delete x; }
+
+int fhe_radix_export(fhe_ctx* c, const fhe_radix* x, uint64_t* cts, size_t nwords) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!x || !cts || nwords < (size_t)x->r.nblocks() * kBigCt) return FHE_ERR_INVALID;
+    return guarded([&] {
+        for (uint32_t k = 0; k < x->r.nblocks(); ++k) {
+            uint64_t* ct = cts + (size_t)k * kBigCt;
+            const Block& b = x->r.blocks[k];
+            if (b.trivial()) {
+                std::memset(ct, 0, kBigCt * 8);
+                ct[kBigDim] = (uint64_t)b.value * c->p.delta();
+            } else {
+                c->engine->download(b, ct);
+            }
+        }
+        return FHE_OK;
+    });
+}
+
+int fhe_radix_add(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    return binop(c, a, b, out, [](Engine& e, const Radix& x, const Radix& y) { return radix_sum(e, {&x, &y}, x.nblocks()); });
+}
+int fhe_radix_sub(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    return binop(c, a, b, out, [](Engine& e, const Radix& x, const Radix& y) { return radix_sub(e, x, y); });
+}
+int fhe_radix_mul(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    return binop(c, a, b, out, [](Engine& e, const Radix& x, const Radix& y) { return radix_mul(e, x, y, x.nblocks()); });
+}
+int fhe_radix_min(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    return binop(c, a, b, out, [](Engine& e, const Radix& x, const Radix& y) { return radix_min(e, x, y); });
+}
+int fhe_radix_max(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    return binop(c, a, b, out, [](Engine& e, const Radix& x, const Radix& y) { return radix_max(e, x, y); });
+}
+int fhe_radix_bitand(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    return binop(c, a, b, out, [](Engine& e, const Radix& x, const Radix& y) { return radix_bitand(e, x, y); });
+}
+int fhe_radix_lt(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    int rc = binop(c, a, b, out, [](Engine& e, const Radix& x, const Radix& y) {
+        Radix r;
+        r.blocks = {radix_lt(e, x, y)};
+        return r;
+    });
+    if (rc == FHE_OK) (*out)->bits = 2;
+    return rc;
+}
+int fhe_radix_shr(fhe_ctx* c, const fhe_radix* a, const fhe_radix* amount, fhe_radix** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !amount || !out) return FHE_ERR_INVALID;
+    return guarded([&] {
+        *out = wrap(radix_shr(*c->engine, a->r, amount->r), a->bits);
+        return FHE_OK;
+    });
+}
+int fhe_radix_shl(fhe_ctx* c, const fhe_radix* a, const fhe_radix* amount, fhe_radix** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !amount || !out) return FHE_ERR_INVALID;
+    return guarded([&] {
+        *out = wrap(radix_shl(*c->engine, a->r, amount->r), a->bits);
+        return FHE_OK;
+    });
+}
+int fhe_radix_scalar_and(fhe_ctx* c, const fhe_radix* a, uint64_t mask, fhe_radix** out) {
+    return unop(c, a, out, [mask](Engine& e, const Radix& x) { return radix_scalar_and(e, x, mask, 0); });
+}
+int fhe_radix_scalar_shr(fhe_ctx* c, const fhe_radix* a, uint32_t shift, fhe_radix** out) {
+    if (!a) return FHE_ERR_INVALID;
+    const uint32_t s = shift % a->bits;  // tfhe: shift amount taken modulo the bit width
+    return unop(c, a, out, [s](Engine& e, const Radix& x) { return radix_scalar_shr(e, x, s); });
+}
+int fhe_radix_scalar_shl(fhe_ctx* c, const fhe_radix* a, uint32_t shift, fhe_radix** out) {
+    if (!a) return FHE_ERR_INVALID;
+    const uint32_t s = shift % a->bits;
+    return unop(c, a, out, [s](Engine& e, const Radix& x) { return radix_scalar_shl(e, x, s); });
+}
+int fhe_radix_scalar_add(fhe_ctx* c, const fhe_radix* a, uint64_t s, fhe_radix** out) {
+    return unop(c, a, out, [s](Engine& e, const Radix& x) { return radix_scalar_add(e, x, s); });
+}
+int fhe_radix_scalar_mul(fhe_ctx* c, const fhe_radix* a, uint64_t s, fhe_radix** out) {
+    return unop(c, a, out, [s](Engine& e, const Radix& x) { return radix_scalar_mul(e, x, s); });
+}
+int fhe_radix_scalar_div(fhe_ctx* c, const fhe_radix* a, uint64_t d, fhe_radix** out) {
+    if (d == 0) {
+        set_error("division by zero");
+        return FHE_ERR_INVALID;
+    }
+    return unop(c, a, out, [d](Engine& e, const Radix& x) { return radix_scalar_div(e, x, d); });
+}
+int fhe_radix_scalar_rem(fhe_ctx* c, const fhe_radix* a, uint64_t d, fhe_radix** out) {
+    if (d == 0) {
+        set_error("division by zero");
+        return FHE_ERR_INVALID;
+    }
+    return unop(c, a, out, [d](Engine& e, const Radix& x) { return radix_scalar_rem(e, x, d); });
+}
+int fhe_radix_cast(fhe_ctx* c, const fhe_radix* a, uint32_t bits, fhe_radix** out) {
+    if (!a || !out || !valid_bits(bits)) return FHE_ERR_INVALID;
+    *out = wrap(radix_resize(a->r, bits / 2), bits);
+    (void)c;
+    return FHE_OK;
+}
+int fhe_ctx_stats(fhe_ctx* c, uint64_t* pbs, uint64_t* levels) {
+    if (!c) return FHE_ERR_INVALID;
+    if (pbs) *pbs = c->engine ? c->engine->pbs_count : 0;
+    if (levels) *levels = c->engine ? c->engine->levels : 0;
+    return FHE_OK;
+}
+
+// --------------------------------------------------------------------------- BigUintFHE
+int fhe_biguint_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint32_t* limbs, size_t n, fhe_biguint** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!ck || !out || (n && !limbs)) return FHE_ERR_INVALID;
+    return guarded([&] {
+        auto* b = new fhe_biguint();
+        std::vector<uint64_t> ct(kBigCt);
+        for (size_t i = 0; i < n; ++i) {
+            Radix r;
+            for (uint32_t k = 0; k < kLimbBlocks; ++k) {
+                encrypt_big(ck, (uint64_t)((limbs[i] >> (2 * k)) & 3u) * ck->params.delta(), ct.data());
+                r.blocks.push_back(c->engine->upload(ct.data(), 3));
+            }
+            b->v.digits.push_back(std::move(r));
+        }
+        *out = b;
+        return FHE_OK;
+    });
+}
+
+int fhe_biguint_from_digits(const fhe_radix* const* digits, size_t n, fhe_biguint** out) {
+    if (!out || (n && !digits)) return FHE_ERR_INVALID;
+    auto* b = new fhe_biguint();
+    for (size_t i = 0; i < n; ++i) {
+        if (!digits[i] || digits[i]->bits != 32) {
+            delete b;
+            set_error("BigUintFHE digits must be FheUint32");
+            return FHE_ERR_INVALID;
+        }
+        b->v.digits.push_back(digits[i]->r);
+    }
+    *out = b;
+    return FHE_OK;
+}
+
+int fhe_biguint_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_biguint* x, uint32_t* limbs, size_t cap,
+                        size_t* n) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!ck || !x || !n) return FHE_ERR_INVALID;
+    *n = x->v.digits.size();
+    if (cap < *n || (*n && !limbs)) {
+        set_error("limb buffer too small");
+        return FHE_ERR_INVALID;
+    }
+    for (size_t i = 0; i < *n; ++i) {
+        fhe_radix tmp;
+        tmp.r = x->v.digits[i];
+        tmp.bits = 32;
+        uint64_t w = 0;
+        rc = fhe_radix_decrypt(c, ck, &tmp, &w, 1);
+        if (rc) return rc;
+        limbs[i] = (uint32_t)w;
+    }
+    return FHE_OK;
+}
+
+int fhe_biguint_len(const fhe_biguint* x, size_t* n) {
+    if (!x || !n) return FHE_ERR_INVALID;
+    *n = x->v.digits.size();
+    return FHE_OK;
+}
+
+int fhe_biguint_digit(const fhe_biguint* x, size_t i, fhe_radix** out) {
+    if (!x || !out || i >= x->v.digits.size()) return FHE_ERR_INVALID;
+    *out = wrap(x->v.digits[i], 32);
+    return FHE_OK;
+}
+
+int fhe_biguint_clone(const fhe_biguint* x, fhe_biguint** out) {
+    if (!x || !out) return FHE_ERR_INVALID;
+    *out = new fhe_biguint(*x);
+    return FHE_OK;
+}
+
+void fhe_biguint_destroy(fhe_biguint* x) { delete x; }
+
+int fhe_biguint_add(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, int mode, fhe_biguint** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !b || !out) return FHE_ERR_INVALID;
+    return guarded([&] {
+        auto* r = new fhe_biguint();
+        r->v = biguint_add(*c->engine, a->v, b->v, mode);
+        *out = r;
+        return FHE_OK;
+    });
+}
+
+int fhe_biguint_mul(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, int mode, fhe_biguint** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !b || !out) return FHE_ERR_INVALID;
+    return guarded([&] {
+        auto* r = new fhe_biguint();
+        r->v = biguint_mul(*c->engine, a->v, b->v, mode);
+        *out = r;
+        return FHE_OK;
+    });
+}
+
+}  // extern "C"

@@ -5,6 +5,7 @@
 #include <cstring>
 
 #include "kernels.h"
+#include "radix.h"
 
 namespace fhe {
 
@@ -64,7 +65,10 @@ using namespace fhe;
 
 int fhe_ctx::ensure_ms(size_t count) {
     if (count <= ms_cap) return FHE_OK;
-    if (d_ms) FHE_HIP_CHECK(hipFree(d_ms));
+    if (d_ms) {
+        FHE_HIP_CHECK(hipStreamSynchronize(stream));  // previous levels may still read it
+        FHE_HIP_CHECK(hipFree(d_ms));
+    }
     size_t cap = count < 256 ? 256 : count;
     ms_stride = (int)((p.n + 1 + 7) / 8 * 8);
     FHE_HIP_CHECK(hipMalloc(&d_ms, cap * ms_stride * sizeof(uint16_t)));
@@ -74,6 +78,7 @@ int fhe_ctx::ensure_ms(size_t count) {
 
 int fhe_ctx::ensure_stage(size_t count) {
     if (count <= stage_cap) return FHE_OK;
+    FHE_HIP_CHECK(hipStreamSynchronize(stream));
     if (d_stage_in) FHE_HIP_CHECK(hipFree(d_stage_in));
     if (d_stage_out) FHE_HIP_CHECK(hipFree(d_stage_out));
     if (d_stage_lut) FHE_HIP_CHECK(hipFree(d_stage_lut));
@@ -268,6 +273,8 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    delete c->engine;
+    c->engine = nullptr;
     void* ptrs[] = {c->d_ksk, c->d_bsk, c->d_W, c->d_psi, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out,
                     c->d_stage_lut};
     for (void* p : ptrs)
@@ -307,6 +314,14 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     }
     c->p = p;
     c->has_key = true;
+    if (!c->engine) {
+        try {
+            c->engine = new fhe::Engine(c);
+        } catch (const std::exception& ex) {
+            set_error(ex.what());
+            return FHE_ERR_HIP;
+        }
+    }
     return FHE_OK;
 }
 

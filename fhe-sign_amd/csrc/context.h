@@ -11,6 +11,7 @@
 
 namespace fhe {
 
+class Engine;
 void set_error(const std::string& msg);
 #define FHE_HIP_CHECK(expr)                                                                   \
     do {                                                                                      \
@@ -57,6 +58,8 @@ struct fhe_ctx {
     bool timing = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     float last_ks_ms = 0.f, last_br_ms = 0.f;
+    // radix-layer executor (created with the server key)
+    fhe::Engine* engine = nullptr;
 
     int ensure_ms(size_t count);
     int ensure_stage(size_t count);

@@ -5,12 +5,31 @@
 
 namespace fhe {
 
+// A bootstrapped block: dst = PBS_lut( sum_t coef[t] * src[t] + cst )   (big-key LWE, 2049 words)
+constexpr int kMaxTerms = 6;
+struct PbsDesc {
+    const uint64_t* src[kMaxTerms];
+    int32_t coef[kMaxTerms];
+    uint32_t nterms;
+    uint32_t lut;
+    uint64_t cst;  // plaintext constant added to the body
+    uint64_t* dst;
+};
+
 // ---- PBS pipeline (pbs_kernels.hip)
 hipError_t launch_keyswitch(const uint64_t* in, int count, const uint64_t* ksk, uint16_t* ms,
                             int ms_stride, int n, hipStream_t s);
 hipError_t launch_blind_rotate(const uint16_t* ms, int ms_stride, const uint32_t* lut_idx,
                                const uint64_t* luts, const double2* bsk, const double2* W,
                                const double2* psi, uint64_t* out, int count, int n, hipStream_t s);
+// descriptor-driven variants (radix layer): fused linear prologue in KS, per-item dst/LUT in BR
+hipError_t launch_keyswitch_desc(const PbsDesc* desc, int count, const uint64_t* ksk, uint16_t* ms,
+                                 int ms_stride, int n, hipStream_t s);
+hipError_t launch_blind_rotate_desc(const uint16_t* ms, int ms_stride, const PbsDesc* desc,
+                                    const uint64_t* luts, const double2* bsk, const double2* W,
+                                    const double2* psi, int count, int n, hipStream_t s);
+// dst_i = sum_t coef * src + cst, no bootstrap (linear radix ops)
+hipError_t launch_lincomb(const PbsDesc* desc, int count, hipStream_t s);
 hipError_t launch_bsk_to_fourier(const uint64_t* bsk, int npoly, const double2* W,
                                  const double2* psi, double2* out, hipStream_t s);
 

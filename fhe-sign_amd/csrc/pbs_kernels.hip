@@ -24,7 +24,19 @@ constexpr int KS_J = 16;   // input coefficients per LDS chunk
 constexpr int KS_LVL = 5;  // gadget levels (base 2^3)
 constexpr int KS_BL = 3;
 
-__global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ in, int count,
+// Input coefficient j of ciphertext ct: either a contiguous batch or a linear combination.
+template <bool DESC>
+FHE_DEV uint64_t ks_input(const uint64_t* __restrict__ in, const PbsDesc* __restrict__ desc, int ct, int j) {
+    if (!DESC) return in[(size_t)ct * 2049 + j];
+    const PbsDesc& d = desc[ct];
+    uint64_t a = (j == 2048) ? d.cst : 0ull;
+    for (uint32_t t = 0; t < d.nterms; ++t) a += (uint64_t)(int64_t)d.coef[t] * d.src[t][j];
+    return a;
+}
+
+template <bool DESC>
+__global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ in,
+                                                  const PbsDesc* __restrict__ desc, int count,
                                                   const uint64_t* __restrict__ ksk,
                                                   uint16_t* __restrict__ ms, int ms_stride,
                                                   int n) {
@@ -37,12 +49,12 @@ __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ 
     for (int c = 0; c < KS_C; ++c) acc[c] = 0;
 
     const int tid = threadIdx.x;
-    const int dc = tid & (KS_C - 1), dj = tid >> 4;  // digit-producer mapping
+    const int dc = tid >> 4, dj = tid & (KS_J - 1);  // digit producer: 16 consecutive j per ct
     const size_t row_stride = (size_t)(n + 1);
     for (int j0 = 0; j0 < 2048; j0 += KS_J) {
         {
             const int ct = c0 + dc;
-            uint64_t a = (ct < count) ? in[(size_t)ct * 2049 + j0 + dj] : 0ull;
+            uint64_t a = (ct < count) ? ks_input<DESC>(in, desc, ct, j0 + dj) : 0ull;
             uint64_t v = (((a >> (63 - KS_BL * KS_LVL)) + 1) >> 1) & ((1ull << (KS_BL * KS_LVL)) - 1);
 #pragma unroll
             for (int l = KS_LVL - 1; l >= 0; --l) {
@@ -75,7 +87,7 @@ __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ 
         const int ct = c0 + c;
         if (ct >= count) break;
         uint64_t v = acc[c];
-        if (k == n) v += in[(size_t)ct * 2049 + 2048];
+        if (k == n) v += ks_input<DESC>(in, desc, ct, 2048);
         ms[(size_t)ct * ms_stride + k] = (uint16_t)modswitch_2n(v);
     }
 }
@@ -105,8 +117,10 @@ FHE_DEV void pointwise_mac(cplx (&x)[16], const cplx* __restrict__ other,
     }
 }
 
+template <bool DESC>
 __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restrict__ ms, int ms_stride,
                                                      const uint32_t* __restrict__ lut_idx,
+                                                     const PbsDesc* __restrict__ desc,
                                                      const uint64_t* __restrict__ luts,
                                                      const cplx* __restrict__ bsk,
                                                      const cplx* __restrict__ W,
@@ -124,7 +138,7 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restr
     {
         const uint32_t bt = a_ct[n];
         const int rot = (int)((4096u - bt) & 4095u);  // X^{-b}
-        const uint64_t* lut = luts + (size_t)lut_idx[ct] * 2048;
+        const uint64_t* lut = luts + (size_t)(DESC ? desc[ct].lut : lut_idx[ct]) * 2048;
 #pragma unroll
         for (int t = 0; t < 32; ++t) {
             uint64_t v = 0;
@@ -203,7 +217,7 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restr
     }
 
     // ---- sample extract (coefficient 0)
-    uint64_t* o = out + (size_t)ct * 2049;
+    uint64_t* o = DESC ? desc[ct].dst : out + (size_t)ct * 2049;
     if (w == 0) {
 #pragma unroll
         for (int t = 0; t < 32; ++t) {
@@ -245,7 +259,15 @@ hipError_t launch_keyswitch(const uint64_t* in, int count, const uint64_t* ksk, 
                             int ms_stride, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     dim3 grid((count + KS_C - 1) / KS_C, (n + 1 + 255) / 256);
-    hipLaunchKernelGGL(k_keyswitch, grid, dim3(256), 0, s, in, count, ksk, ms, ms_stride, n);
+    hipLaunchKernelGGL(k_keyswitch<false>, grid, dim3(256), 0, s, in, nullptr, count, ksk, ms, ms_stride, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_keyswitch_desc(const PbsDesc* desc, int count, const uint64_t* ksk, uint16_t* ms,
+                                 int ms_stride, int n, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    dim3 grid((count + KS_C - 1) / KS_C, (n + 1 + 255) / 256);
+    hipLaunchKernelGGL(k_keyswitch<true>, grid, dim3(256), 0, s, nullptr, desc, count, ksk, ms, ms_stride, n);
     return hipGetLastError();
 }
 
@@ -253,8 +275,36 @@ hipError_t launch_blind_rotate(const uint16_t* ms, int ms_stride, const uint32_t
                                const uint64_t* luts, const cplx* bsk, const cplx* W,
                                const cplx* psi, uint64_t* out, int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blind_rotate, dim3(count), dim3(128), 0, s, ms, ms_stride, lut_idx, luts, bsk,
-                       W, psi, out, n);
+    hipLaunchKernelGGL(k_blind_rotate<false>, dim3(count), dim3(128), 0, s, ms, ms_stride, lut_idx, nullptr,
+                       luts, bsk, W, psi, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_desc(const uint16_t* ms, int ms_stride, const PbsDesc* desc,
+                                    const uint64_t* luts, const cplx* bsk, const cplx* W,
+                                    const cplx* psi, int count, int n, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_blind_rotate<true>, dim3(count), dim3(128), 0, s, ms, ms_stride, nullptr, desc,
+                       luts, bsk, W, psi, nullptr, n);
+    return hipGetLastError();
+}
+
+// ============================================================================ linear combination
+// One workgroup per output block: dst = sum_t coef_t * src_t + cst (body), 2049 words.
+__global__ __launch_bounds__(256) void k_lincomb(const PbsDesc* __restrict__ desc, int count) {
+    const int c = blockIdx.x;
+    if (c >= count) return;
+    const PbsDesc& d = desc[c];
+    for (int j = threadIdx.x; j < 2049; j += 256) {
+        uint64_t a = (j == 2048) ? d.cst : 0ull;
+        for (uint32_t t = 0; t < d.nterms; ++t) a += (uint64_t)(int64_t)d.coef[t] * d.src[t][j];
+        d.dst[j] = a;
+    }
+}
+
+hipError_t launch_lincomb(const PbsDesc* desc, int count, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_lincomb, dim3(count), dim3(256), 0, s, desc, count);
     return hipGetLastError();
 }
 

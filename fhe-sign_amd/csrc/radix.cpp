@@ -1,0 +1,883 @@
+// radix.cpp -- radix-integer layer: level executor + integer algorithms (host orchestration;
+// all ciphertext arithmetic runs in the gfx950 kernels of pbs_kernels.hip).
+//
+// Algorithms (published TFHE radix techniques, restated; tfhe 0.10.0 integer layer [ext]):
+//   * carry propagation: block states (generate/propagate/kill) + Hillis-Steele prefix with
+//     bivariate lookups (4*hi + lo), then one final (v + carry) mod 4 bootstrap per block
+//   * multiplication: block-pair products through bivariate LUTs (low/high halves), column
+//     compression (<= 15 in degree per group, msg/carry split), then carry propagation
+//   * scalar division: Granlund-Montgomery multiply-high by a public magic constant
+//   * comparison: borrow-out of a + ~b + 1 via the same prefix machinery
+//   * encrypted shift: barrel shifter, one bivariate "select" level per amount bit
+// Public structure only (degrees, trivial blocks) drives the schedule; no decision ever depends
+// on encrypted data.
+#include "radix.h"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+namespace fhe {
+
+void engine_check(bool ok, const char* what) {
+    if (!ok) throw std::runtime_error(what);
+}
+
+static void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// ============================================================================ block pool
+Slot::~Slot() {
+    if (pool && p) pool->release(p);
+}
+
+BlockPool::~BlockPool() {
+    (void)hipSetDevice(device_);
+    for (void* c : chunks_) (void)hipFree(c);
+}
+
+std::shared_ptr<Slot> BlockPool::alloc() {
+    if (free_.empty()) {
+        const size_t per = 1024;  // 16 MiB chunks
+        void* c = nullptr;
+        hip_check(hipMalloc(&c, per * kBigCt * 8), "block pool hipMalloc");
+        chunks_.push_back(c);
+        for (size_t i = 0; i < per; ++i) free_.push_back((uint64_t*)c + (per - 1 - i) * kBigCt);
+        total_ += per;
+    }
+    auto s = std::make_shared<Slot>();
+    s->p = free_.back();
+    free_.pop_back();
+    s->pool = shared_from_this();
+    return s;
+}
+
+// ============================================================================ engine
+Engine::Engine(fhe_ctx* ctx) : ctx_(ctx) {
+    pool_ = std::make_shared<BlockPool>(ctx->device);
+    for (auto& ev : desc_ev_) hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+}
+
+Engine::~Engine() {
+    (void)hipSetDevice(ctx_->device);
+    (void)hipStreamSynchronize(ctx_->stream);
+    for (auto* h : h_desc_)
+        if (h) (void)hipHostFree(h);
+    for (auto ev : desc_ev_)
+        if (ev) (void)hipEventDestroy(ev);
+    if (d_desc_) (void)hipFree(d_desc_);
+}
+
+void Engine::ensure_desc(size_t n) {
+    if (n > desc_cap_) {
+        size_t cap = std::max<size_t>(n, 4096);
+        for (int i = 0; i < 2; ++i) {
+            if (h_desc_[i]) {
+                hip_check(hipEventSynchronize(desc_ev_[i]), "desc event");
+                hip_check(hipHostFree(h_desc_[i]), "hipHostFree");
+            }
+            hip_check(hipHostMalloc((void**)&h_desc_[i], cap * sizeof(PbsDesc)), "hipHostMalloc");
+        }
+        desc_cap_ = cap;
+    }
+    if (n > d_desc_cap_) {
+        hip_check(hipStreamSynchronize(ctx_->stream), "sync");
+        if (d_desc_) hip_check(hipFree(d_desc_), "hipFree");
+        d_desc_cap_ = std::max<size_t>(n, 4096);
+        hip_check(hipMalloc(&d_desc_, d_desc_cap_ * sizeof(PbsDesc)), "hipMalloc desc");
+    }
+}
+
+// Host staging buffer for n descriptors (double-buffered: wait until its previous copy is done).
+PbsDesc* Engine::stage_desc(size_t n, PbsDesc** dev) {
+    ensure_desc(n);
+    desc_turn_ ^= 1;
+    hip_check(hipEventSynchronize(desc_ev_[desc_turn_]), "desc event");
+    *dev = d_desc_;
+    return h_desc_[desc_turn_];
+}
+
+namespace {
+// reachable plaintexts of sum coef*x_t + cst (x_t in [0, degree_t]) as a bitmask over [0, 64)
+uint64_t reachable(const std::vector<Term>& terms, int64_t cst, bool* ok) {
+    *ok = true;
+    if (cst < 0 || cst >= 64) {
+        *ok = false;
+        return 0;
+    }
+    uint64_t set = 1ull << cst;
+    for (const Term& t : terms) {
+        uint64_t nxt = 0;
+        for (int v = 0; v < 64; ++v) {
+            if (!(set >> v & 1)) continue;
+            for (uint32_t x = 0; x <= t.b.degree; ++x) {
+                int64_t r = v + (int64_t)t.coef * x;
+                if (r < 0 || r >= 64) {
+                    *ok = false;
+                    return 0;
+                }
+                nxt |= 1ull << r;
+            }
+        }
+        set = nxt;
+    }
+    return set;
+}
+}  // namespace
+
+Blocks Engine::run(std::vector<PbsItem>& items) {
+    const Params& p = ctx_->p;
+    const uint32_t mc = p.msg_carry();
+    Blocks out(items.size());
+    std::vector<size_t> gpu;
+    std::vector<std::vector<Term>> live(items.size());
+    std::vector<int64_t> csts(items.size());
+    for (size_t i = 0; i < items.size(); ++i) {
+        PbsItem& it = items[i];
+        engine_check(it.table.size() == mc, "LUT table size");
+        int64_t cst = it.cst;
+        uint32_t noise = 0;
+        for (const Term& t : it.terms) {
+            if (t.coef == 0) continue;
+            if (t.b.trivial())
+                cst += (int64_t)t.coef * t.b.value;
+            else {
+                live[i].push_back(t);
+                noise += (uint32_t)(t.coef * t.coef) * t.b.noise;
+            }
+        }
+        bool ok;
+        const uint64_t reach = reachable(live[i], cst, &ok);
+        engine_check(ok && (reach >> mc) == 0, "PBS input out of the message space (degree overflow)");
+        engine_check(noise <= kMaxNoise, "PBS input noise above the budget");
+        uint32_t lo = 0xffffffffu, hi = 0;
+        bool identity = live[i].size() == 1 && live[i][0].coef == 1 && cst == 0 && live[i][0].b.noise <= 1;
+        for (uint32_t v = 0; v < mc; ++v) {
+            if (!(reach >> v & 1)) continue;
+            const uint32_t f = it.table[v] % mc;
+            lo = std::min(lo, f);
+            hi = std::max(hi, f);
+            if (f != v) identity = false;
+        }
+        if (lo == hi) {
+            out[i] = Block::make_trivial(lo);
+        } else if (identity) {
+            out[i] = live[i][0].b;  // LUT is the identity on every reachable input: alias
+            out[i].degree = hi;
+        } else {
+            out[i].degree = hi;
+            out[i].noise = 1;
+            csts[i] = cst;
+            gpu.push_back(i);
+        }
+    }
+    if (gpu.empty()) return out;
+
+    // register LUTs, allocate destinations, build descriptors
+    PbsDesc* dev = nullptr;
+    PbsDesc* h = stage_desc(gpu.size(), &dev);
+    const uint64_t delta = p.delta();
+    for (size_t g = 0; g < gpu.size(); ++g) {
+        const size_t i = gpu[g];
+        uint32_t lut = 0;
+        engine_check(ctx_->register_lut(items[i].table.data(), &lut) == FHE_OK, "LUT registration");
+        out[i].slot = pool_->alloc();
+        PbsDesc d;
+        std::memset(&d, 0, sizeof d);
+        engine_check(live[i].size() <= (size_t)kMaxTerms, "too many terms in one PBS input");
+        for (size_t t = 0; t < live[i].size(); ++t) {
+            d.src[t] = live[i][t].b.ptr();
+            d.coef[t] = live[i][t].coef;
+        }
+        d.nterms = (uint32_t)live[i].size();
+        d.lut = lut;
+        d.cst = (uint64_t)csts[i] * delta;
+        d.dst = out[i].slot->p;
+        h[g] = d;
+    }
+    engine_check(ctx_->sync_luts() == FHE_OK, "LUT upload");
+    engine_check(ctx_->ensure_ms(gpu.size()) == FHE_OK, "workspace");
+    hip_check(hipMemcpyAsync(dev, h, gpu.size() * sizeof(PbsDesc), hipMemcpyHostToDevice, ctx_->stream), "desc copy");
+    hip_check(hipEventRecord(desc_ev_[desc_turn_], ctx_->stream), "desc event");
+    hip_check(launch_keyswitch_desc(dev, (int)gpu.size(), ctx_->d_ksk, ctx_->d_ms, ctx_->ms_stride, (int)p.n,
+                                    ctx_->stream),
+              "keyswitch");
+    hip_check(launch_blind_rotate_desc(ctx_->d_ms, ctx_->ms_stride, dev, ctx_->d_luts, ctx_->d_bsk, ctx_->d_W,
+                                       ctx_->d_psi, (int)gpu.size(), (int)p.n, ctx_->stream),
+              "blind rotate");
+    pbs_count += gpu.size();
+    levels += 1;
+    return out;
+}
+
+Block Engine::lincomb(const std::vector<Term>& terms, uint32_t cst) {
+    int64_t c = cst;
+    uint32_t noise = 0;
+    std::vector<Term> live;
+    for (const Term& t : terms) {
+        if (t.b.trivial())
+            c += (int64_t)t.coef * t.b.value;
+        else if (t.coef) {
+            live.push_back(t);
+            noise += (uint32_t)(t.coef * t.coef) * t.b.noise;
+        }
+    }
+    bool ok;
+    const uint64_t reach = reachable(live, c, &ok);
+    engine_check(ok && (reach >> ctx_->p.msg_carry()) == 0, "linear combination out of range");
+    uint32_t hi = 63 - __builtin_clzll(reach);
+    if (live.empty()) return Block::make_trivial((uint32_t)c);
+    Block b;
+    b.degree = hi;
+    b.noise = noise;
+    b.slot = pool_->alloc();
+    PbsDesc* dev = nullptr;
+    PbsDesc* h = stage_desc(1, &dev);
+    PbsDesc d;
+    std::memset(&d, 0, sizeof d);
+    for (size_t t = 0; t < live.size(); ++t) {
+        d.src[t] = live[t].b.ptr();
+        d.coef[t] = live[t].coef;
+    }
+    d.nterms = (uint32_t)live.size();
+    d.cst = (uint64_t)c * ctx_->p.delta();
+    d.dst = b.slot->p;
+    h[0] = d;
+    hip_check(hipMemcpyAsync(dev, h, sizeof(PbsDesc), hipMemcpyHostToDevice, ctx_->stream), "desc copy");
+    hip_check(hipEventRecord(desc_ev_[desc_turn_], ctx_->stream), "desc event");
+    hip_check(launch_lincomb(dev, 1, ctx_->stream), "lincomb");
+    return b;
+}
+
+Block Engine::upload(const uint64_t* ct, uint32_t degree) {
+    Block b;
+    b.slot = pool_->alloc();
+    b.degree = degree;
+    b.noise = 1;
+    hip_check(hipMemcpyAsync(b.slot->p, ct, kBigCt * 8, hipMemcpyHostToDevice, ctx_->stream), "upload");
+    hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");
+    return b;
+}
+
+void Engine::download(const Block& b, uint64_t* ct) {
+    engine_check(!b.trivial(), "download of a trivial block");
+    hip_check(hipMemcpyAsync(ct, b.slot->p, kBigCt * 8, hipMemcpyDeviceToHost, ctx_->stream), "download");
+    hip_check(hipStreamSynchronize(ctx_->stream), "download sync");
+}
+
+void Engine::sync() { hip_check(hipStreamSynchronize(ctx_->stream), "sync"); }
+
+// ============================================================================ LUT helpers
+namespace {
+std::vector<uint32_t> lut1(const std::function<uint32_t(uint32_t)>& f) {
+    std::vector<uint32_t> t(16);
+    for (uint32_t x = 0; x < 16; ++x) t[x] = f(x) & 15u;
+    return t;
+}
+// bivariate on 4*hi + lo (hi, lo in [0, 4))
+std::vector<uint32_t> lut2(const std::function<uint32_t(uint32_t, uint32_t)>& f) {
+    std::vector<uint32_t> t(16);
+    for (uint32_t x = 0; x < 16; ++x) t[x] = f(x >> 2, x & 3) & 15u;
+    return t;
+}
+PbsItem item1(const Block& b, std::vector<uint32_t> table) {
+    PbsItem it;
+    it.terms = {{b, 1}};
+    it.table = std::move(table);
+    return it;
+}
+PbsItem item2(const Block& hi, const Block& lo, std::vector<uint32_t> table) {
+    PbsItem it;
+    it.terms = {{hi, 4}, {lo, 1}};
+    it.table = std::move(table);
+    return it;
+}
+const std::vector<uint32_t>& LUT_MOD4() {
+    static auto t = lut1([](uint32_t x) { return x & 3; });
+    return t;
+}
+const std::vector<uint32_t>& LUT_DIV4() {
+    static auto t = lut1([](uint32_t x) { return x >> 2; });
+    return t;
+}
+const std::vector<uint32_t>& LUT_STATE() {  // 2 generate, 1 propagate, 0 kill
+    static auto t = lut1([](uint32_t v) { return v >= 4 ? 2u : (v == 3 ? 1u : 0u); });
+    return t;
+}
+const std::vector<uint32_t>& LUT_GEN() {
+    static auto t = lut1([](uint32_t v) { return v >= 4 ? 1u : 0u; });
+    return t;
+}
+const std::vector<uint32_t>& LUT_PREFIX_BIT() {  // (hi state, lo carry bit) -> carry bit
+    static auto t = lut2([](uint32_t hi, uint32_t lo) { return (hi == 2 || (hi == 1 && lo == 1)) ? 1u : 0u; });
+    return t;
+}
+const std::vector<uint32_t>& LUT_PREFIX_STATE() {  // (hi state, lo state) -> state
+    static auto t = lut2([](uint32_t hi, uint32_t lo) { return hi == 1 ? lo : hi; });
+    return t;
+}
+}  // namespace
+
+// ============================================================================ basics
+Radix radix_trivial(uint64_t lo, uint64_t hi, uint32_t nblocks) {
+    Radix r;
+    r.blocks.resize(nblocks);
+    for (uint32_t k = 0; k < nblocks; ++k) {
+        const uint32_t bit = 2 * k;
+        uint32_t v = 0;
+        if (bit < 64)
+            v = (uint32_t)(lo >> bit) & 3u;
+        else if (bit < 128)
+            v = (uint32_t)(hi >> (bit - 64)) & 3u;
+        r.blocks[k] = Block::make_trivial(v);
+    }
+    return r;
+}
+
+Radix radix_resize(const Radix& a, uint32_t nblocks) {
+    Radix r;
+    r.blocks.resize(nblocks);
+    for (uint32_t k = 0; k < nblocks; ++k) r.blocks[k] = k < a.nblocks() ? a.blocks[k] : Block::make_trivial(0);
+    return r;
+}
+
+// ============================================================================ carry propagation
+// Several independent problems advance level by level together (one launch pair per level).
+struct ColProblem {
+    std::vector<Blocks> cols;  // cols[k]: blocks summing into position k
+    uint32_t nblocks;
+};
+
+static uint32_t col_degree(const Blocks& c) {
+    uint32_t d = 0;
+    for (const Block& b : c) d += b.degree;
+    return d;
+}
+static uint32_t col_noise(const Blocks& c) {
+    uint32_t s = 0;
+    for (const Block& b : c) s += b.noise;
+    return s;
+}
+static bool col_live(const Blocks& c) {
+    for (const Block& b : c)
+        if (!(b.trivial() && b.value == 0)) return true;
+    return false;
+}
+
+// Column compression until every column is a sum <= 6 (<= 7 at position 0) of <= 3 blocks.
+static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
+    for (;;) {
+        std::vector<PbsItem> items;
+        struct Dest {
+            ColProblem* p;
+            uint32_t col;
+        };
+        std::vector<Dest> dests;
+        std::vector<std::vector<Blocks>> next(probs.size());
+        bool any = false;
+        for (size_t pi = 0; pi < probs.size(); ++pi) {
+            ColProblem& P = *probs[pi];
+            next[pi].assign(P.nblocks, {});
+            for (uint32_t k = 0; k < P.nblocks; ++k) {
+                Blocks c;
+                for (Block& b : P.cols[k])
+                    if (!(b.trivial() && b.value == 0)) c.push_back(b);
+                const uint32_t lim = k == 0 ? 7 : 6;
+                if (col_degree(c) <= lim && c.size() <= 3 && col_noise(c) <= kMaxNoise - 1) {
+                    for (auto& b : c) next[pi][k].push_back(b);
+                    continue;
+                }
+                any = true;
+                // greedy groups: degree sum <= 15, noise sum <= kMaxNoise, <= kMaxTerms blocks
+                std::sort(c.begin(), c.end(), [](const Block& a, const Block& b) { return a.degree > b.degree; });
+                size_t s = 0;
+                while (s < c.size()) {
+                    std::vector<Term> g;
+                    uint32_t deg = 0, noi = 0;
+                    while (s < c.size() && g.size() < (size_t)kMaxTerms && deg + c[s].degree <= 15 &&
+                           noi + c[s].noise <= kMaxNoise) {
+                        g.push_back({c[s], 1});
+                        deg += c[s].degree;
+                        noi += c[s].noise;
+                        ++s;
+                    }
+                    engine_check(!g.empty(), "column block too large to compress");
+                    if (g.size() == 1 && deg <= 3 && g[0].b.noise <= 1) {
+                        next[pi][k].push_back(g[0].b);
+                        continue;
+                    }
+                    PbsItem lo;
+                    lo.terms = g;
+                    lo.table = LUT_MOD4();
+                    items.push_back(lo);
+                    dests.push_back({probs[pi], k});
+                    if (deg >= 4 && k + 1 < P.nblocks) {
+                        PbsItem hi;
+                        hi.terms = g;
+                        hi.table = LUT_DIV4();
+                        items.push_back(hi);
+                        dests.push_back({probs[pi], k + 1});
+                    }
+                }
+            }
+        }
+        if (!any) return;
+        Blocks outs = e.run(items);
+        for (size_t i = 0; i < outs.size(); ++i) {
+            size_t pi = std::find(probs.begin(), probs.end(), dests[i].p) - probs.begin();
+            next[pi][dests[i].col].push_back(outs[i]);
+        }
+        for (size_t pi = 0; pi < probs.size(); ++pi) probs[pi]->cols = std::move(next[pi]);
+    }
+}
+
+// Carry-propagate compressed columns (each column sum v_k <= 6, <= 7 at k = 0).
+static std::vector<Radix> propagate_many(Engine& e, std::vector<ColProblem>& probs) {
+    std::vector<ColProblem*> ptrs;
+    for (auto& p : probs) {
+        p.cols.resize(p.nblocks);
+        ptrs.push_back(&p);
+    }
+    compress_columns(e, ptrs);
+
+    // carries c_k (carry out of position k), k < nblocks - 1, for every problem
+    std::vector<Blocks> cur(probs.size());
+    {
+        std::vector<PbsItem> items;
+        for (auto& P : probs) {
+            const uint32_t m = P.nblocks ? P.nblocks - 1 : 0;
+            for (uint32_t k = 0; k < m; ++k) {
+                PbsItem it;
+                for (auto& b : P.cols[k]) it.terms.push_back({b, 1});
+                it.table = k == 0 ? LUT_GEN() : LUT_STATE();
+                items.push_back(it);
+            }
+        }
+        Blocks outs = e.run(items);
+        size_t o = 0;
+        for (size_t pi = 0; pi < probs.size(); ++pi) {
+            const uint32_t m = probs[pi].nblocks ? probs[pi].nblocks - 1 : 0;
+            cur[pi].assign(outs.begin() + o, outs.begin() + o + m);
+            o += m;
+        }
+    }
+    // Hillis-Steele prefix: after the level with span 2^t, positions < 2^(t+1) are carry bits
+    for (uint32_t span = 1;; span <<= 1) {
+        std::vector<PbsItem> items;
+        struct Ref {
+            size_t pi;
+            uint32_t k;
+        };
+        std::vector<Ref> refs;
+        for (size_t pi = 0; pi < probs.size(); ++pi) {
+            const uint32_t m = (uint32_t)cur[pi].size();
+            for (uint32_t k = span; k < m; ++k) {
+                const bool completes = k < 2 * span;
+                items.push_back(item2(cur[pi][k], cur[pi][k - span], completes ? LUT_PREFIX_BIT() : LUT_PREFIX_STATE()));
+                refs.push_back({pi, k});
+            }
+        }
+        if (items.empty()) break;
+        Blocks outs = e.run(items);
+        for (size_t i = 0; i < outs.size(); ++i) cur[refs[i].pi][refs[i].k] = outs[i];
+    }
+    // final: out_k = (v_k + c_{k-1}) mod 4
+    std::vector<PbsItem> items;
+    for (size_t pi = 0; pi < probs.size(); ++pi) {
+        ColProblem& P = probs[pi];
+        for (uint32_t k = 0; k < P.nblocks; ++k) {
+            PbsItem it;
+            for (auto& b : P.cols[k]) it.terms.push_back({b, 1});
+            if (k > 0) it.terms.push_back({cur[pi][k - 1], 1});
+            it.table = LUT_MOD4();
+            items.push_back(it);
+        }
+    }
+    Blocks outs = e.run(items);
+    std::vector<Radix> res(probs.size());
+    size_t o = 0;
+    for (size_t pi = 0; pi < probs.size(); ++pi) {
+        res[pi].blocks.assign(outs.begin() + o, outs.begin() + o + probs[pi].nblocks);
+        o += probs[pi].nblocks;
+    }
+    return res;
+}
+
+Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks) {
+    std::vector<ColProblem> probs(1);
+    probs[0].cols = std::move(cols);
+    probs[0].nblocks = nblocks;
+    return propagate_many(e, probs)[0];
+}
+
+Radix radix_sum(Engine& e, const std::vector<const Radix*>& xs, uint32_t nblocks) {
+    std::vector<Blocks> cols(nblocks);
+    for (const Radix* x : xs)
+        for (uint32_t k = 0; k < nblocks && k < x->nblocks(); ++k) cols[k].push_back(x->blocks[k]);
+    // fast path: a single operand that is already clean
+    bool clean = true;
+    for (auto& c : cols) {
+        uint32_t live = 0;
+        for (auto& b : c)
+            if (!(b.trivial() && b.value == 0)) {
+                ++live;
+                if (b.degree > 3 || b.noise > 1) clean = false;
+            }
+        if (live > 1) clean = false;
+    }
+    if (clean) {
+        Radix r;
+        r.blocks.resize(nblocks);
+        for (uint32_t k = 0; k < nblocks; ++k) {
+            r.blocks[k] = Block::make_trivial(0);
+            for (auto& b : cols[k])
+                if (!(b.trivial() && b.value == 0)) r.blocks[k] = b;
+        }
+        return r;
+    }
+    return radix_propagate_columns(e, std::move(cols), nblocks);
+}
+
+// ============================================================================ multiplication
+static void add_products(const Radix& a, const Radix& b, uint32_t nblocks, std::vector<PbsItem>& items,
+                         std::vector<uint32_t>& cols_of) {
+    static const auto LUT_MUL_LO = lut2([](uint32_t x, uint32_t y) { return (x * y) & 3; });
+    static const auto LUT_MUL_HI = lut2([](uint32_t x, uint32_t y) { return (x * y) >> 2; });
+    for (uint32_t p = 0; p < a.nblocks(); ++p) {
+        const Block& ap = a.blocks[p];
+        if (ap.trivial() && ap.value == 0) continue;
+        for (uint32_t q = 0; q < b.nblocks() && p + q < nblocks; ++q) {
+            const Block& bq = b.blocks[q];
+            if (bq.trivial() && bq.value == 0) continue;
+            engine_check(ap.degree <= 3 && bq.degree <= 3, "mul needs clean operands");
+            items.push_back(item2(ap, bq, LUT_MUL_LO));
+            cols_of.push_back(p + q);
+            if (p + q + 1 < nblocks && ap.degree * bq.degree >= 4) {
+                items.push_back(item2(ap, bq, LUT_MUL_HI));
+                cols_of.push_back(p + q + 1);
+            }
+        }
+    }
+}
+
+std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
+                                  uint32_t nblocks) {
+    std::vector<PbsItem> items;
+    std::vector<uint32_t> cols_of;
+    std::vector<size_t> start(ops.size() + 1, 0);
+    for (size_t i = 0; i < ops.size(); ++i) {
+        start[i] = items.size();
+        add_products(*ops[i].first, *ops[i].second, nblocks, items, cols_of);
+    }
+    start[ops.size()] = items.size();
+    Blocks outs = e.run(items);
+    std::vector<ColProblem> probs(ops.size());
+    for (size_t i = 0; i < ops.size(); ++i) {
+        probs[i].nblocks = nblocks;
+        probs[i].cols.assign(nblocks, {});
+        for (size_t j = start[i]; j < start[i + 1]; ++j) probs[i].cols[cols_of[j]].push_back(outs[j]);
+    }
+    return propagate_many(e, probs);
+}
+
+Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {
+    return radix_mul_many(e, {{&a, &b}}, nblocks)[0];
+}
+
+// ============================================================================ scalar ops
+Radix radix_scalar_and(Engine& e, const Radix& a, uint64_t mlo, uint64_t mhi) {
+    std::vector<PbsItem> items;
+    std::vector<uint32_t> where;
+    Radix r;
+    r.blocks.resize(a.nblocks());
+    for (uint32_t k = 0; k < a.nblocks(); ++k) {
+        const uint32_t bit = 2 * k;
+        const uint32_t m = bit < 64 ? (uint32_t)(mlo >> bit) & 3 : (bit < 128 ? (uint32_t)(mhi >> (bit - 64)) & 3 : 0);
+        const Block& x = a.blocks[k];
+        if (m == 0)
+            r.blocks[k] = Block::make_trivial(0);
+        else if (m == 3)
+            r.blocks[k] = x;
+        else {
+            items.push_back(item1(x, lut1([m](uint32_t v) { return v & m; })));
+            where.push_back(k);
+        }
+    }
+    Blocks outs = e.run(items);
+    for (size_t i = 0; i < outs.size(); ++i) r.blocks[where[i]] = outs[i];
+    return r;
+}
+
+Radix radix_scalar_shr(Engine& e, const Radix& a, uint32_t bits) {
+    const uint32_t n = a.nblocks(), s = bits / 2;
+    auto blk = [&](uint32_t k) { return k < n ? a.blocks[k] : Block::make_trivial(0); };
+    Radix r;
+    r.blocks.resize(n);
+    if (bits % 2 == 0) {
+        for (uint32_t k = 0; k < n; ++k) r.blocks[k] = blk(k + s);
+        return r;
+    }
+    static const auto LUT_SHR1 = lut2([](uint32_t hi, uint32_t lo) { return ((hi & 1) << 1) | (lo >> 1); });
+    std::vector<PbsItem> items;
+    for (uint32_t k = 0; k < n; ++k) items.push_back(item2(blk(k + s + 1), blk(k + s), LUT_SHR1));
+    r.blocks = e.run(items);
+    return r;
+}
+
+Radix radix_scalar_shl(Engine& e, const Radix& a, uint32_t bits) {
+    const uint32_t n = a.nblocks(), s = bits / 2;
+    auto blk = [&](int64_t k) { return (k >= 0 && k < (int64_t)n) ? a.blocks[k] : Block::make_trivial(0); };
+    Radix r;
+    r.blocks.resize(n);
+    if (bits % 2 == 0) {
+        for (uint32_t k = 0; k < n; ++k) r.blocks[k] = blk((int64_t)k - s);
+        return r;
+    }
+    static const auto LUT_SHL1 = lut2([](uint32_t hi, uint32_t lo) { return ((hi << 1) & 3) | (lo >> 1); });
+    std::vector<PbsItem> items;
+    // out_k = ((x_{k-s} << 1) & 3) | (x_{k-s-1} >> 1)
+    for (uint32_t k = 0; k < n; ++k) items.push_back(item2(blk((int64_t)k - s), blk((int64_t)k - s - 1), LUT_SHL1));
+    r.blocks = e.run(items);
+    return r;
+}
+
+Radix radix_scalar_add(Engine& e, const Radix& a, uint64_t s) {
+    Radix t = radix_trivial(s, 0, a.nblocks());
+    return radix_sum(e, {&a, &t}, a.nblocks());
+}
+
+Radix radix_scalar_mul(Engine& e, const Radix& a, uint64_t s) {
+    Radix t = radix_trivial(s, 0, a.nblocks());
+    return radix_mul(e, a, t, a.nblocks());
+}
+
+// Granlund-Montgomery (PLDI 1994, Fig. 6.2) multiplier for N-bit unsigned division by d.
+static void choose_multiplier(uint64_t d, uint32_t N, unsigned __int128* m, uint32_t* sh) {
+    uint32_t l = 0;
+    while (l < 64 && ((unsigned __int128)1 << l) < d) ++l;  // ceil(log2 d)
+    uint32_t shpost = l;
+    // m_low = floor(2^(N+l) / d), m_high = floor((2^(N+l) + 2^l) / d)  (prec = N)
+    unsigned __int128 two = (unsigned __int128)1 << (N + l);
+    unsigned __int128 mlow = two / d;
+    unsigned __int128 mhigh = (two + ((unsigned __int128)1 << l)) / d;
+    while ((mlow >> 1) < (mhigh >> 1) && shpost > 0) {
+        mlow >>= 1;
+        mhigh >>= 1;
+        --shpost;
+    }
+    *m = mhigh;
+    *sh = shpost;
+}
+
+Radix radix_scalar_div(Engine& e, const Radix& a, uint64_t d) {
+    const uint32_t n = a.nblocks(), N = 2 * n;
+    engine_check(d != 0, "division by zero");
+    engine_check(N <= 64, "scalar_div supports up to 64-bit integers");
+    if (d == 1) return a;
+    if ((d & (d - 1)) == 0) return radix_scalar_shr(e, a, (uint32_t)__builtin_ctzll(d));
+    if (N < 64 && d >= (1ull << N)) return radix_trivial(0, 0, n);
+    uint32_t l = 0;
+    while (l < 64 && ((unsigned __int128)1 << l) < d) ++l;
+    engine_check(N + l <= 126, "scalar_div: divisor too large for this width");
+    unsigned __int128 m;
+    uint32_t sh;
+    choose_multiplier(d, N, &m, &sh);
+    // q = floor(a * m / 2^(N + sh)); a < 2^N, m <= 2^(N+1)  =>  a*m < 2^(2N+1): 2n+1 blocks
+    const uint32_t nb = 2 * n + 1;
+    Radix aw = radix_resize(a, nb);
+    Radix mw = radix_trivial((uint64_t)m, (uint64_t)(m >> 64), nb);
+    Radix prod = radix_mul(e, aw, mw, nb);
+    Radix q = radix_scalar_shr(e, prod, N + sh);
+    return radix_resize(q, n);
+}
+
+Radix radix_sub(Engine& e, const Radix& a, const Radix& b) {
+    // a - b = a + ~b + 1 (mod 2^bits): ~b_k = 3 - b_k folded into the column sums
+    const uint32_t n = a.nblocks();
+    std::vector<Blocks> cols(n);
+    std::vector<PbsItem> items;  // complement blocks, materialized through identity-range LUTs
+    for (uint32_t k = 0; k < n; ++k) {
+        cols[k].push_back(a.blocks[k]);
+        const Block bk = k < b.nblocks() ? b.blocks[k] : Block::make_trivial(0);
+        PbsItem it;
+        it.terms = {{bk, -1}};
+        it.cst = 3;
+        it.table = lut1([](uint32_t v) { return v & 3; });
+        items.push_back(it);
+    }
+    Blocks nb = e.run(items);
+    for (uint32_t k = 0; k < n; ++k) cols[k].push_back(nb[k]);
+    cols[0].push_back(Block::make_trivial(1));
+    return radix_propagate_columns(e, std::move(cols), n);
+}
+
+// carry out of the top of a + ~b + 1  (1 iff a >= b)
+static Block carry_out_ge(Engine& e, const Radix& a, const Radix& b) {
+    const uint32_t n = std::max(a.nblocks(), b.nblocks());
+    std::vector<PbsItem> items;
+    // states of (a_k + 3 - b_k [+1 at k = 0]) directly from a and b (no complement materialized)
+    for (uint32_t k = 0; k < n; ++k) {
+        const Block ak = k < a.nblocks() ? a.blocks[k] : Block::make_trivial(0);
+        const Block bk = k < b.nblocks() ? b.blocks[k] : Block::make_trivial(0);
+        PbsItem it;
+        it.terms = {{ak, 1}, {bk, -1}};
+        it.cst = 3 + (k == 0 ? 1 : 0);
+        it.table = k == 0 ? LUT_GEN() : LUT_STATE();
+        items.push_back(it);
+    }
+    Blocks cur = e.run(items);
+    for (uint32_t span = 1; span < n; span <<= 1) {
+        std::vector<PbsItem> its;
+        std::vector<uint32_t> ks;
+        for (uint32_t k = span; k < n; ++k) {
+            its.push_back(item2(cur[k], cur[k - span], k < 2 * span ? LUT_PREFIX_BIT() : LUT_PREFIX_STATE()));
+            ks.push_back(k);
+        }
+        Blocks outs = e.run(its);
+        for (size_t i = 0; i < outs.size(); ++i) cur[ks[i]] = outs[i];
+    }
+    return cur[n - 1];
+}
+
+Block radix_lt(Engine& e, const Radix& a, const Radix& b) {
+    Block ge = carry_out_ge(e, a, b);
+    std::vector<PbsItem> items{item1(ge, lut1([](uint32_t v) { return v ? 0u : 1u; }))};
+    return e.run(items)[0];
+}
+
+// out_k = cond ? x_k : y_k   (two half-selects per block, summed, then one cleaning bootstrap)
+Radix radix_select(Engine& e, const Block& cond, const Radix& x, const Radix& y) {
+    static const auto LUT_IF = lut2([](uint32_t c, uint32_t v) { return c ? v : 0u; });
+    static const auto LUT_IFNOT = lut2([](uint32_t c, uint32_t v) { return c ? 0u : v; });
+    const uint32_t n = std::max(x.nblocks(), y.nblocks());
+    std::vector<PbsItem> items;
+    for (uint32_t k = 0; k < n; ++k) {
+        const Block xk = k < x.nblocks() ? x.blocks[k] : Block::make_trivial(0);
+        const Block yk = k < y.nblocks() ? y.blocks[k] : Block::make_trivial(0);
+        items.push_back(item2(cond, xk, LUT_IF));
+        items.push_back(item2(cond, yk, LUT_IFNOT));
+    }
+    Blocks h = e.run(items);
+    std::vector<PbsItem> fin;
+    for (uint32_t k = 0; k < n; ++k) {
+        PbsItem it;
+        it.terms = {{h[2 * k], 1}, {h[2 * k + 1], 1}};
+        it.table = LUT_MOD4();
+        fin.push_back(it);
+    }
+    Radix r;
+    r.blocks = e.run(fin);
+    for (auto& b : r.blocks) b.degree = std::min<uint32_t>(b.degree, 3);
+    return r;
+}
+
+Radix radix_min(Engine& e, const Radix& a, const Radix& b) { return radix_select(e, radix_lt(e, a, b), a, b); }
+Radix radix_max(Engine& e, const Radix& a, const Radix& b) { return radix_select(e, radix_lt(e, a, b), b, a); }
+
+// Barrel shifter (amount taken mod the bit width, tfhe semantics).  Each stage: out_k =
+// c ? x_{k+s} : x_k as two half-selects whose sum feeds the next stage's lookups directly
+// (noise 16 + 2 <= budget), one final cleaning level.
+static Radix barrel(Engine& e, const Radix& a, const Radix& amount, bool right) {
+    const uint32_t n = a.nblocks(), bitsw = 2 * n;
+    uint32_t stages = 0;
+    while ((1u << stages) < bitsw) ++stages;
+    // amount bits (one level) together with the 1-bit shifted copy of a
+    std::vector<PbsItem> items;
+    for (uint32_t i = 0; i < stages; ++i) {
+        const uint32_t blk = i / 2;
+        const Block src = blk < amount.nblocks() ? amount.blocks[blk] : Block::make_trivial(0);
+        const uint32_t sh = i % 2;
+        items.push_back(item1(src, lut1([sh](uint32_t v) { return (v >> sh) & 1u; })));
+    }
+    auto blk = [&](int64_t k) { return (k >= 0 && k < (int64_t)n) ? a.blocks[k] : Block::make_trivial(0); };
+    static const auto LUT_SHR1 = lut2([](uint32_t hi, uint32_t lo) { return ((hi & 1) << 1) | (lo >> 1); });
+    static const auto LUT_SHL1 = lut2([](uint32_t hi, uint32_t lo) { return ((hi << 1) & 3) | (lo >> 1); });
+    for (uint32_t k = 0; k < n; ++k) {
+        if (right)
+            items.push_back(item2(blk(k + 1), blk(k), LUT_SHR1));
+        else
+            items.push_back(item2(blk(k), blk((int64_t)k - 1), LUT_SHL1));
+    }
+    Blocks o = e.run(items);
+    Blocks bits(o.begin(), o.begin() + stages);
+    Blocks sh1(o.begin() + stages, o.end());
+    // state: each position is a pending sum of up to two half-select outputs
+    std::vector<std::vector<Block>> cur(n);
+    for (uint32_t k = 0; k < n; ++k) cur[k] = {a.blocks[k]};
+    static const auto LUT_IF = lut2([](uint32_t c, uint32_t v) { return c ? v : 0u; });
+    static const auto LUT_IFNOT = lut2([](uint32_t c, uint32_t v) { return c ? 0u : v; });
+    auto pend = [&](const std::vector<Block>& v, uint32_t c_lut_which, const Block& c) {
+        PbsItem it;
+        it.terms.push_back({c, 4});
+        for (auto& b : v) it.terms.push_back({b, 1});
+        it.table = c_lut_which ? LUT_IF : LUT_IFNOT;
+        return it;
+    };
+    for (uint32_t i = 0; i < stages; ++i) {
+        std::vector<PbsItem> its;
+        for (uint32_t k = 0; k < n; ++k) {
+            its.push_back(pend(cur[k], 0, bits[i]));  // keep when bit = 0
+            std::vector<Block> moved;
+            if (i == 0) {
+                moved = {sh1[k]};
+            } else {
+                const int64_t s = (int64_t)1 << (i - 1);  // 2^i bits = 2^(i-1) blocks
+                const int64_t src = right ? (int64_t)k + s : (int64_t)k - s;
+                if (src >= 0 && src < (int64_t)n)
+                    moved = cur[src];
+                else
+                    moved = {Block::make_trivial(0)};
+            }
+            its.push_back(pend(moved, 1, bits[i]));
+        }
+        Blocks h = e.run(its);
+        for (uint32_t k = 0; k < n; ++k) {
+            cur[k] = {h[2 * k], h[2 * k + 1]};
+            for (auto& b : cur[k]) b.degree = std::min<uint32_t>(b.degree, 3);
+        }
+    }
+    std::vector<PbsItem> fin;
+    for (uint32_t k = 0; k < n; ++k) {
+        PbsItem it;
+        for (auto& b : cur[k]) it.terms.push_back({b, 1});
+        it.table = LUT_MOD4();
+        fin.push_back(it);
+    }
+    Radix r;
+    r.blocks = e.run(fin);
+    for (auto& b : r.blocks) b.degree = std::min<uint32_t>(b.degree, 3);
+    return r;
+}
+
+Radix radix_shr(Engine& e, const Radix& a, const Radix& amount) { return barrel(e, a, amount, true); }
+Radix radix_shl(Engine& e, const Radix& a, const Radix& amount) { return barrel(e, a, amount, false); }
+
+Radix radix_bitand(Engine& e, const Radix& a, const Radix& b) {
+    static const auto LUT_AND = lut2([](uint32_t x, uint32_t y) { return x & y; });
+    std::vector<PbsItem> items;
+    for (uint32_t k = 0; k < a.nblocks(); ++k)
+        items.push_back(item2(a.blocks[k], k < b.nblocks() ? b.blocks[k] : Block::make_trivial(0), LUT_AND));
+    Radix r;
+    r.blocks = e.run(items);
+    return r;
+}
+
+Radix radix_clean(Engine& e, const Radix& a) {
+    std::vector<PbsItem> items;
+    for (auto& b : a.blocks) {
+        PbsItem it = item1(b, LUT_MOD4());
+        items.push_back(it);
+    }
+    Radix r;
+    r.blocks = e.run(items);
+    return r;
+}
+
+Radix radix_scalar_rem(Engine& e, const Radix& a, uint64_t d) {
+    Radix q = radix_scalar_div(e, a, d);
+    Radix qd = radix_scalar_mul(e, q, d);
+    return radix_sub(e, a, qd);
+}
+
+}  // namespace fhe

@@ -1,0 +1,149 @@
+// radix.h -- radix-integer layer over the GPU PBS pipeline.
+//
+// Replaces tfhe 0.10.0's integer layer under the FheUint{8,32,64} operators the reference calls
+// (src/biguint.rs:135-143,221-248; src/perf_test.rs:28-54).  A radix integer of B bits is B/2
+// blocks (2-bit message + 2-bit carry space), least significant first, each a big-key LWE in a
+// fixed-size device slot.  Host-side metadata per block:
+//   degree   -- largest plaintext the block can hold (public, from the op structure)
+//   noise    -- variance in units of one fresh bootstrap output
+//   trivial  -- a publicly known value with no device storage (zero-extension, masks, constants)
+// Every bootstrap is a PbsItem: LUT( sum coef_t * block_t + cst ).  Items of one dependency level
+// run as ONE batched keyswitch (with the linear combination fused in) + ONE blind-rotate launch.
+// Items whose LUT is constant over the reachable inputs fold to trivial blocks on the host.
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <vector>
+
+#include "context.h"
+#include "kernels.h"
+
+namespace fhe {
+
+constexpr uint32_t kMsgBits = 2;
+constexpr uint32_t kMsgMod = 4;
+constexpr uint32_t kMaxNoise = 20;  // variance units; bivariate 4a+b of fresh blocks = 17
+
+class BlockPool;
+
+struct Slot {
+    uint64_t* p = nullptr;
+    std::shared_ptr<BlockPool> pool;
+    ~Slot();
+};
+
+struct Block {
+    std::shared_ptr<Slot> slot;  // null => trivial
+    uint32_t value = 0;          // trivial value
+    uint32_t degree = 0;
+    uint32_t noise = 0;
+    bool trivial() const { return !slot; }
+    const uint64_t* ptr() const { return slot ? slot->p : nullptr; }
+    static Block make_trivial(uint32_t v) {
+        Block b;
+        b.value = v;
+        b.degree = v;
+        return b;
+    }
+};
+
+using Blocks = std::vector<Block>;
+
+class BlockPool : public std::enable_shared_from_this<BlockPool> {
+public:
+    explicit BlockPool(int device) : device_(device) {}
+    ~BlockPool();
+    std::shared_ptr<Slot> alloc();
+    void release(uint64_t* p) { free_.push_back(p); }
+    size_t live() const { return total_ - free_.size(); }
+
+private:
+    int device_;
+    std::vector<void*> chunks_;
+    std::vector<uint64_t*> free_;
+    size_t total_ = 0;
+};
+
+struct Term {
+    Block b;
+    int32_t coef;
+};
+
+struct PbsItem {
+    std::vector<Term> terms;
+    uint32_t cst = 0;             // plaintext constant (units of one message step)
+    std::vector<uint32_t> table;  // LUT over [0, msg*carry)
+};
+
+// Executes dependency levels of PBS items on a context.
+class Engine {
+public:
+    explicit Engine(fhe_ctx* ctx);
+    ~Engine();
+    fhe_ctx* ctx() const { return ctx_; }
+    // Runs one level; returns one output block per item (possibly trivial).  Throws on error.
+    Blocks run(std::vector<PbsItem>& items);
+    // Linear combination without bootstrap (caller guarantees degree/noise stay legal).
+    Block lincomb(const std::vector<Term>& terms, uint32_t cst);
+    // Upload client-encrypted blocks.
+    Block upload(const uint64_t* ct, uint32_t degree);
+    void download(const Block& b, uint64_t* ct);
+    void sync();
+    // statistics
+    uint64_t pbs_count = 0, levels = 0;
+
+private:
+    fhe_ctx* ctx_;
+    std::shared_ptr<BlockPool> pool_;
+    PbsDesc* h_desc_[2] = {nullptr, nullptr};  // pinned, double-buffered
+    hipEvent_t desc_ev_[2] = {nullptr, nullptr};
+    size_t desc_cap_ = 0;
+    int desc_turn_ = 0;
+    PbsDesc* d_desc_ = nullptr;
+    size_t d_desc_cap_ = 0;
+    void ensure_desc(size_t n);
+    PbsDesc* stage_desc(size_t n, PbsDesc** dev);
+};
+
+void engine_check(bool ok, const char* what);
+
+// ----------------------------------------------------------------------------- radix ops
+// All take/return clean blocks (degree <= 3, noise <= 1) unless stated; widths in blocks.
+struct Radix {
+    Blocks blocks;
+    uint32_t nblocks() const { return (uint32_t)blocks.size(); }
+};
+
+Radix radix_trivial(uint64_t value_lo, uint64_t value_hi, uint32_t nblocks);
+Radix radix_resize(const Radix& a, uint32_t nblocks);  // cast: truncate / zero-extend
+
+// Sum of several radix integers (wrapping at `nblocks`; carries propagated).  Used for every add.
+Radix radix_sum(Engine& e, const std::vector<const Radix*>& xs, uint32_t nblocks);
+// Carry propagation of raw column blocks (each column may hold several blocks).
+Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks);
+// Wrapping product.
+Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks);
+// Batched independent products (one level schedule for all).
+std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
+                                  uint32_t nblocks);
+Radix radix_scalar_and(Engine& e, const Radix& a, uint64_t mask_lo, uint64_t mask_hi);
+Radix radix_scalar_shr(Engine& e, const Radix& a, uint32_t bits);
+Radix radix_scalar_shl(Engine& e, const Radix& a, uint32_t bits);
+Radix radix_scalar_add(Engine& e, const Radix& a, uint64_t s);
+Radix radix_scalar_mul(Engine& e, const Radix& a, uint64_t s);
+Radix radix_scalar_div(Engine& e, const Radix& a, uint64_t d);
+Radix radix_scalar_rem(Engine& e, const Radix& a, uint64_t d);
+Radix radix_sub(Engine& e, const Radix& a, const Radix& b);
+// encrypted boolean (one block, value 0/1)
+Block radix_lt(Engine& e, const Radix& a, const Radix& b);
+Radix radix_select(Engine& e, const Block& cond, const Radix& if_true, const Radix& if_false);
+Radix radix_min(Engine& e, const Radix& a, const Radix& b);
+Radix radix_max(Engine& e, const Radix& a, const Radix& b);
+Radix radix_shr(Engine& e, const Radix& a, const Radix& amount);
+Radix radix_shl(Engine& e, const Radix& a, const Radix& amount);
+Radix radix_bitand(Engine& e, const Radix& a, const Radix& b);
+// refresh every block through an identity bootstrap (noise reset)
+Radix radix_clean(Engine& e, const Radix& a);
+
+}  // namespace fhe

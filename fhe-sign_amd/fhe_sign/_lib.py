@@ -51,6 +51,40 @@ _SIGNATURES = [
     ("fhe_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     ("fhe_ctx_last_pbs_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("fhe_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("fhe_radix_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u64p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_trivial", C.c_int, [C.c_void_p, u64p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u64p, C.c_size_t]),
+    ("fhe_radix_num_bits", C.c_int, [C.c_void_p, u32p]),
+    ("fhe_radix_clone", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_destroy", None, [C.c_void_p]),
+    ("fhe_radix_export", C.c_int, [C.c_void_p, C.c_void_p, u64p, C.c_size_t]),
+    ("fhe_radix_add", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_sub", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_mul", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_and", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_shr", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_shl", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_add", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_mul", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_div", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_rem", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_cast", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_min", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_max", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_lt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_shr", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_shl", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_bitand", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_ctx_stats", C.c_int, [C.c_void_p, u64p, u64p]),
+    ("fhe_biguint_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_biguint_from_digits", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_biguint_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("fhe_biguint_len", C.c_int, [C.c_void_p, C.POINTER(C.c_size_t)]),
+    ("fhe_biguint_digit", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_biguint_clone", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_biguint_destroy", None, [C.c_void_p]),
+    ("fhe_biguint_add", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    ("fhe_biguint_mul", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
 ]
 
 _lib = None

@@ -107,6 +107,75 @@ int fhe_memcpy_d2h(fhe_ctx* ctx, void* dst, const void* src, size_t bytes);
 int fhe_ctx_last_pbs_timing(fhe_ctx* ctx, float* ks_ms, float* br_ms);
 int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 
+/* ------------------------------------------------------------------- radix integers */
+/* FheUint<num_bits> (num_bits even, <= 128): num_bits/2 radix blocks, device-resident.
+ * Replaces tfhe's FheUint8/32/64 as used at src/biguint.rs:26,135-143,221-248 and
+ * src/perf_test.rs:19-54.  Arithmetic wraps modulo 2^num_bits (tfhe semantics). */
+typedef struct fhe_radix fhe_radix;
+/* FheUint::try_encrypt (src/biguint.rs:26, src/perf_test.rs:19-21); words little-endian */
+int fhe_radix_encrypt(fhe_ctx* ctx, fhe_client_key* ck, const uint64_t* words, uint32_t num_bits,
+                      fhe_radix** out);
+/* trivial (unencrypted-noise-free) constant, e.g. FheUint::encrypt_trivial */
+int fhe_radix_trivial(fhe_ctx* ctx, const uint64_t* words, uint32_t num_bits, fhe_radix** out);
+/* FheDecrypt (src/biguint.rs:70): nwords >= ceil(num_bits/64) */
+int fhe_radix_decrypt(fhe_ctx* ctx, const fhe_client_key* ck, const fhe_radix* x, uint64_t* words,
+                      size_t nwords);
+int fhe_radix_num_bits(const fhe_radix* x, uint32_t* num_bits);
+int fhe_radix_clone(const fhe_radix* x, fhe_radix** out);
+void fhe_radix_destroy(fhe_radix* x);
+/* raw block ciphertexts (num_bits/2 x 2049 words; trivial blocks are materialized) */
+int fhe_radix_export(fhe_ctx* ctx, const fhe_radix* x, uint64_t* cts, size_t nwords);
+/* FheUint + FheUint (src/biguint.rs:138,236,243,248; src/perf_test.rs:28) */
+int fhe_radix_add(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+int fhe_radix_sub(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+/* FheUint * FheUint (src/biguint.rs:223; src/perf_test.rs:32) */
+int fhe_radix_mul(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+/* &FheUint & u64 (src/biguint.rs:116,143; src/perf_test.rs:48) */
+int fhe_radix_scalar_and(fhe_ctx* ctx, const fhe_radix* a, uint64_t mask, fhe_radix** out);
+/* &FheUint >> u64 (src/biguint.rs:110,141); shift taken mod num_bits (src/biguint.rs:494-498) */
+int fhe_radix_scalar_shr(fhe_ctx* ctx, const fhe_radix* a, uint32_t shift, fhe_radix** out);
+int fhe_radix_scalar_shl(fhe_ctx* ctx, const fhe_radix* a, uint32_t shift, fhe_radix** out);
+int fhe_radix_scalar_add(fhe_ctx* ctx, const fhe_radix* a, uint64_t s, fhe_radix** out);
+/* FheUint * clear (src/schnorr.rs:588) */
+int fhe_radix_scalar_mul(fhe_ctx* ctx, const fhe_radix* a, uint64_t s, fhe_radix** out);
+/* FheUint / clear (src/perf_test.rs:54); divisor 0 -> FHE_ERR_INVALID */
+int fhe_radix_scalar_div(fhe_ctx* ctx, const fhe_radix* a, uint64_t d, fhe_radix** out);
+int fhe_radix_scalar_rem(fhe_ctx* ctx, const fhe_radix* a, uint64_t d, fhe_radix** out);
+/* FheUint::cast_from / cast_into (src/biguint.rs:110,116,221; src/perf_test.rs:40) */
+int fhe_radix_cast(fhe_ctx* ctx, const fhe_radix* a, uint32_t num_bits, fhe_radix** out);
+/* FheUint::min (src/perf_test.rs:44), max, lt (encrypted bool returned as a 2-bit radix) */
+int fhe_radix_min(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+int fhe_radix_max(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+int fhe_radix_lt(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+/* &FheUint >> &FheUint (src/perf_test.rs:36), amount mod num_bits; and << */
+int fhe_radix_shr(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* amount, fhe_radix** out);
+int fhe_radix_shl(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* amount, fhe_radix** out);
+int fhe_radix_bitand(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+/* engine statistics since context creation: bootstraps executed and dependency levels */
+int fhe_ctx_stats(fhe_ctx* ctx, uint64_t* pbs_count, uint64_t* levels);
+
+/* ------------------------------------------------------------------- BigUintFHE */
+/* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */
+typedef struct fhe_biguint fhe_biguint;
+#define FHE_BIGUINT_COMPAT 0 /* exact reference limb loop incl. src/biguint.rs:247-249 wrap */
+#define FHE_BIGUINT_FAST 1   /* true sum/product, one wide carry propagation */
+/* BigUintFHE::new (src/biguint.rs:17-31): limbs = value.to_u32_digits() (LSB first, no
+ * leading zeros; nlimbs 0 encodes zero as an empty vector) */
+int fhe_biguint_encrypt(fhe_ctx* ctx, fhe_client_key* ck, const uint32_t* limbs, size_t nlimbs,
+                        fhe_biguint** out);
+/* BigUintFHE::from_encrypted_digits (src/biguint.rs:46-48) */
+int fhe_biguint_from_digits(const fhe_radix* const* digits, size_t n, fhe_biguint** out);
+/* to_biguint (src/biguint.rs:61-76): decrypted limbs; *nlimbs = digit count */
+int fhe_biguint_decrypt(fhe_ctx* ctx, const fhe_client_key* ck, const fhe_biguint* x, uint32_t* limbs,
+                        size_t cap, size_t* nlimbs);
+int fhe_biguint_len(const fhe_biguint* x, size_t* nlimbs);
+int fhe_biguint_digit(const fhe_biguint* x, size_t i, fhe_radix** out);
+int fhe_biguint_clone(const fhe_biguint* x, fhe_biguint** out);
+void fhe_biguint_destroy(fhe_biguint* x);
+/* impl Add / impl Mul for BigUintFHE (src/biguint.rs:120-265); inputs are not consumed */
+int fhe_biguint_add(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, int mode, fhe_biguint** out);
+int fhe_biguint_mul(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, int mode, fhe_biguint** out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,168 @@
+"""GPU radix layer (FheUint ops) and BigUintFHE against the reference semantics.
+
+Parity bar: decrypted values equal the reference's (tfhe wrapping semantics; BigUintFHE limb
+loop of src/biguint.rs:120-265 incl. the :247-249 wrap) on the reference's known answers and on
+seeded random inputs.  Ciphertext bytes vs tfhe-rs: parity unpinned."""
+import json
+import os
+import random
+
+import pytest
+
+import ref_semantics as R
+from conftest import ROOT
+from fhe_sign import (COMPAT, FAST, BigUintFHE, Context, FheUint8, FheUint32, FheUint64, generate_keys,
+                      set_server_key, stats)
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(ROOT, "tests", "golden")
+
+
+@pytest.fixture(scope="module")
+def keys():
+    ck, sk = generate_keys(seed=0xB16)
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    set_server_key(ctx)
+    yield ck, ctx
+    set_server_key(None)
+    ctx.close()
+
+
+def test_fheuint_known_answers(keys):
+    ck, _ = keys
+    for c in json.load(open(os.path.join(G, "known_answers.json")))["fheuint"]:
+        T = FheUint64 if c["bits"] == 64 else FheUint32
+        a = T.try_encrypt(c["a"], ck)
+        if c["op"] == "add_split":  # extract_upper_bits / extract_lower_bits (src/biguint.rs:108-117)
+            s = a + T.try_encrypt(c["b"], ck)
+            hi = FheUint32.cast_from(s >> 32)
+            lo = FheUint32.cast_from(s & 0xFFFFFFFF)
+            assert (hi.decrypt(ck), lo.decrypt(ck)) == (c["hi"], c["lo"]), c["test"]
+        elif c["op"] == "add_shr_and":  # &sum >> 32, &sum & mask on the same width
+            s = a + T.try_encrypt(c["b"], ck)
+            assert ((s >> 32).decrypt(ck), (s & 0xFFFFFFFF).decrypt(ck)) == (c["hi"], c["lo"]), c["test"]
+        elif c["op"] == "scalar_mul":
+            assert (a * c["b"]).decrypt(ck) == c["value"], c["test"]
+        elif c["op"] == "scalar_add":
+            assert (a + c["b"]).decrypt(ck) == c["value"], c["test"]
+        elif c["op"] == "add":
+            assert (a + T.try_encrypt(c["b"], ck)).decrypt(ck) == c["value"], c["test"]
+        elif c["op"] == "mul":
+            assert (a * T.try_encrypt(c["b"], ck)).decrypt(ck) == c["value"], c["test"]
+        elif c["op"] == "scalar_div":
+            assert (a / c["b"]).decrypt(ck) == c["value"], c["test"]
+        elif c["op"] == "perf_chain":  # src/perf_test.rs:36-63
+            b = T.try_encrypt(c["b"], ck)
+            shifted = a >> b
+            casted = shifted.cast_into(FheUint8)
+            m = casted.min(FheUint8.try_encrypt(c["c"], ck))
+            assert (m & 1).decrypt(ck) == c["value"], c["test"]
+
+
+def test_fheuint32_random_ops(keys):
+    ck, _ = keys
+    rng = random.Random(7)
+    M = 1 << 32
+    for _ in range(3):
+        x, y = rng.getrandbits(32), rng.getrandbits(32)
+        a, b = FheUint32.try_encrypt(x, ck), FheUint32.try_encrypt(y, ck)
+        assert (a + b).decrypt(ck) == (x + y) % M
+        assert (a - b).decrypt(ck) == (x - y) % M
+        assert (a * b).decrypt(ck) == (x * y) % M
+        s = rng.randrange(64)
+        assert (a >> s).decrypt(ck) == x >> (s % 32)
+        assert (a << s).decrypt(ck) == (x << (s % 32)) % M
+        m = rng.getrandbits(32)
+        assert (a & m).decrypt(ck) == x & m
+        d = rng.randrange(1, 1 << 20)
+        assert (a / d).decrypt(ck) == x // d
+        assert (a % d).decrypt(ck) == x % d
+        assert a.min(b).decrypt(ck) == min(x, y)
+        assert a.max(b).decrypt(ck) == max(x, y)
+        assert a.lt(b).decrypt(ck) == int(x < y)
+        sh = rng.randrange(32)
+        assert (a >> FheUint32.try_encrypt(sh, ck)).decrypt(ck) == x >> sh
+
+
+def test_fheuint_edge_cases(keys):
+    ck, _ = keys
+    M = 1 << 32
+    z, f = FheUint32.try_encrypt(0, ck), FheUint32.try_encrypt(M - 1, ck)
+    assert (f + f).decrypt(ck) == (2 * M - 2) % M
+    assert (f * f).decrypt(ck) == 1
+    assert (z - f).decrypt(ck) == 1
+    assert z.lt(z).decrypt(ck) == 0 and z.lt(f).decrypt(ck) == 1 and f.lt(z).decrypt(ck) == 0
+    assert (f / 3).decrypt(ck) == (M - 1) // 3
+    assert (f >> 32).decrypt(ck) == M - 1  # shift mod width (src/biguint.rs:494-498)
+    with pytest.raises(Exception):
+        f / 0
+    e8 = FheUint8.try_encrypt(255, ck)
+    assert (e8 + FheUint8.try_encrypt(1, ck)).decrypt(ck) == 0
+    assert FheUint64.cast_from(f).decrypt(ck) == M - 1
+    assert FheUint8.cast_from(f).decrypt(ck) == 255
+
+
+def _big(ck, limbs):
+    return BigUintFHE.new(R.from_limbs(limbs), ck)
+
+
+def test_biguint_known_answers(keys):
+    ck, _ = keys
+    for c in json.load(open(os.path.join(G, "known_answers.json")))["biguint"]:
+        a = BigUintFHE.new(c["a"], ck)
+        if c["op"] == "roundtrip":
+            assert a.to_biguint(ck) == c["value"]
+            continue
+        b = BigUintFHE.new(c["b"], ck)
+        out = a + b if c["op"] == "add" else a * b
+        if "limbs" in c:
+            assert out.decrypt_limbs(ck) == c["limbs"], c["test"]
+        else:
+            assert out.to_biguint(ck) == c["value"], c["test"]
+
+
+def test_biguint_add_256_compat_and_fast(keys):
+    ck, _ = keys
+    g = json.load(open(os.path.join(G, "biguint_vectors.json")))
+    for v in g["add"][:3]:
+        a, b = _big(ck, v["a"]), _big(ck, v["b"])
+        assert a.add(b, COMPAT).decrypt_limbs(ck) == v["out"]
+        assert a.add(b, FAST).decrypt_limbs(ck) == v["out"]
+    for v in g["edge"]:
+        a, b = _big(ck, v["a"]), _big(ck, v["b"])
+        out = (a.add(b) if v["op"] == "add" else a.mul(b)).decrypt_limbs(ck)
+        assert out == v["out"]
+
+
+def test_biguint_mul_256_compat(keys):
+    """config 2: 8x8-limb BigUintFHE mul, exact reference limb loop (src/biguint.rs:214-254)."""
+    ck, ctx = keys
+    g = json.load(open(os.path.join(G, "biguint_vectors.json")))
+    v = g["mul"][0]
+    p0, l0 = stats(ctx)
+    out = _big(ck, v["a"]).mul(_big(ck, v["b"]), COMPAT)
+    assert out.decrypt_limbs(ck) == v["out"]
+    p1, l1 = stats(ctx)
+    assert p1 > p0 and l1 > l0
+
+
+def test_biguint_mul_quirk_compat_vs_fast(keys):
+    """F7: (2^256-1)^2 -- compat reproduces the reference's lost carry, fast gives the true product."""
+    ck, _ = keys
+    q = json.load(open(os.path.join(G, "biguint_vectors.json")))["quirk_mul"][0]
+    a, b = _big(ck, q["a"]), _big(ck, q["b"])
+    assert a.mul(b, COMPAT).decrypt_limbs(ck) == q["out"]
+    assert a.mul(b, FAST).decrypt_limbs(ck) == q["true_product"]
+
+
+def test_sign_fhe_with_k0_vector0_limb_flow(keys):
+    """config 4 FHE block (src/schnorr.rs:272-275) on BIP-340 vector 0: e*d' (8x1 limbs) then k + ."""
+    ck, _ = keys
+    v = json.load(open(os.path.join(G, "sign_vectors.json")))["vectors"][0]
+    e, d, k = _big(ck, v["e"]), _big(ck, v["d"]), _big(ck, v["k"])
+    prod = e * d.clone()
+    assert prod.decrypt_limbs(ck) == v["prod"]
+    s = k + prod
+    assert s.decrypt_limbs(ck) == v["sum"]
+    assert s.to_biguint(ck) % R.N == int(v["s"], 16)
