@@ -1,0 +1,59 @@
+"""Schnorr / BIP-340 signer (src/schnorr.rs) over the C ABI.
+
+`Schnorr` mirrors the reference struct: sign, sign_with_k0, sign_fhe, sign_fhe_with_k0, verify,
+plus compute_nonce / get_public_key_with_even_y.  Scalars are Python ints; signatures bytes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from ._lib import check, load
+from .integer import COMPAT, _ctx
+
+
+def _b32(x: int) -> bytes:
+    return int(x).to_bytes(32, "big")
+
+
+def _buf(b: bytes):
+    return (C.c_uint8 * max(len(b), 1)).from_buffer_copy(b if b else b"\0")
+
+
+def public_key_x(privkey: int) -> bytes:
+    out = (C.c_uint8 * 32)()
+    check(load().fhe_schnorr_public_key(_buf(_b32(privkey)), out))
+    return bytes(out)
+
+
+def compute_nonce(privkey: int, message: bytes, aux_rand: bytes) -> int:
+    out = (C.c_uint8 * 32)()
+    check(load().fhe_schnorr_compute_nonce(_buf(_b32(privkey)), _buf(message), len(message), _buf(aux_rand), out))
+    return int.from_bytes(bytes(out), "big")
+
+
+class Schnorr:
+    def sign(self, message: bytes, aux_rand: bytes, privkey: int) -> bytes:
+        sig = (C.c_uint8 * 64)()
+        check(load().fhe_schnorr_sign(_buf(message), len(message), _buf(aux_rand), _buf(_b32(privkey)), sig))
+        return bytes(sig)
+
+    def sign_with_k0(self, message: bytes, k0: int, privkey: int) -> bytes:
+        sig = (C.c_uint8 * 64)()
+        check(load().fhe_schnorr_sign_with_k0(_buf(message), len(message), _buf(_b32(k0)), _buf(_b32(privkey)), sig))
+        return bytes(sig)
+
+    def sign_fhe_with_k0(self, message: bytes, k0: int, privkey: int, privkey_fhe, client_key, mode: int = COMPAT) -> bytes:
+        sig = (C.c_uint8 * 64)()
+        check(load().fhe_schnorr_sign_fhe_with_k0(_ctx().handle, client_key.handle, _buf(message), len(message),
+                                                  _buf(_b32(k0)), _buf(_b32(privkey)), privkey_fhe.handle, mode, sig))
+        return bytes(sig)
+
+    def sign_fhe(self, message: bytes, aux_rand: bytes, privkey: int, client_key, mode: int = COMPAT) -> bytes:
+        sig = (C.c_uint8 * 64)()
+        check(load().fhe_schnorr_sign_fhe(_ctx().handle, client_key.handle, _buf(message), len(message),
+                                          _buf(aux_rand), _buf(_b32(privkey)), mode, sig))
+        return bytes(sig)
+
+    @staticmethod
+    def verify(message: bytes, pubkey: bytes, sig: bytes) -> bool:
+        return load().fhe_schnorr_verify(_buf(message), len(message), _buf(pubkey), len(pubkey), _buf(sig), len(sig)) == 1

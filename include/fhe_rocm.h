@@ -176,6 +176,29 @@ void fhe_biguint_destroy(fhe_biguint* x);
 int fhe_biguint_add(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, int mode, fhe_biguint** out);
 int fhe_biguint_mul(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, int mode, fhe_biguint** out);
 
+/* ------------------------------------------------------------------- Schnorr / BIP-340 */
+/* The caller of the hot path (src/schnorr.rs).  32-byte scalars are big-endian.  The plaintext
+ * EC / hash steps run on the host; the FHE block s = k + e*d runs on the GPU engine. */
+int fhe_schnorr_public_key(const uint8_t privkey[32], uint8_t pubkey_x[32]);
+/* compute_nonce (src/schnorr.rs:394-401) */
+int fhe_schnorr_compute_nonce(const uint8_t privkey[32], const uint8_t* msg, size_t msg_len,
+                              const uint8_t aux_rand[32], uint8_t k0[32]);
+/* Schnorr::sign_with_k0 / sign (src/schnorr.rs:75-141), plaintext comparator */
+int fhe_schnorr_sign_with_k0(const uint8_t* msg, size_t msg_len, const uint8_t k0[32],
+                             const uint8_t privkey[32], uint8_t sig[64]);
+int fhe_schnorr_sign(const uint8_t* msg, size_t msg_len, const uint8_t aux_rand[32],
+                     const uint8_t privkey[32], uint8_t sig[64]);
+/* Schnorr::sign_fhe_with_k0 (src/schnorr.rs:235-290): privkey_fhe = BigUintFHE::new(privkey) */
+int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t msg_len,
+                                 const uint8_t k0[32], const uint8_t privkey[32],
+                                 const fhe_biguint* privkey_fhe, int mode, uint8_t sig[64]);
+/* Schnorr::sign_fhe (src/schnorr.rs:154-211) */
+int fhe_schnorr_sign_fhe(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t msg_len,
+                         const uint8_t aux_rand[32], const uint8_t privkey[32], int mode, uint8_t sig[64]);
+/* Schnorr::verify (src/schnorr.rs:301-347): 1 valid, 0 invalid */
+int fhe_schnorr_verify(const uint8_t* msg, size_t msg_len, const uint8_t* pubkey, size_t pubkey_len,
+                       const uint8_t* sig, size_t sig_len);
+
 #ifdef __cplusplus
 }
 #endif

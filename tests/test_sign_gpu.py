@@ -1,0 +1,58 @@
+"""config 4: Schnorr::sign_fhe_with_k0 on the GPU engine == sign_with_k0 byte-for-byte
+(test_schnorr_fhe_with_k0, src/schnorr.rs:469-492) and == the CSV signature (test_schnorr_fhe,
+src/schnorr.rs:440-466)."""
+import csv
+import os
+
+import pytest
+
+from conftest import ROOT
+from fhe_sign import COMPAT, FAST, BigUintFHE, Context, Schnorr, compute_nonce, generate_keys, public_key_x, set_server_key
+
+pytestmark = pytest.mark.gpu
+ROWS = {r["index"]: r for r in csv.DictReader(open(os.path.join(ROOT, "tests", "golden", "bip340_vectors.csv")))}
+
+
+@pytest.fixture(scope="module")
+def env():
+    ck, sk = generate_keys(seed=0x5167)
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    set_server_key(ctx)
+    yield ck
+    set_server_key(None)
+    ctx.close()
+
+
+def _sign_case(ck, idx, mode):
+    row = ROWS[idx]
+    d = int(row["secret key"], 16)
+    msg, aux = bytes.fromhex(row["message"]), bytes.fromhex(row["aux_rand"])
+    k0 = compute_nonce(d, msg, aux)
+    s = Schnorr()
+    d_fhe = BigUintFHE.new(d, ck)
+    sig_fhe = s.sign_fhe_with_k0(msg, k0, d, d_fhe, ck, mode)
+    assert sig_fhe == s.sign_with_k0(msg, k0, d)
+    assert Schnorr.verify(msg, public_key_x(d), sig_fhe)
+    return sig_fhe, row
+
+
+def test_sign_fhe_with_k0_vector0(env):
+    sig, row = _sign_case(env, "0", COMPAT)
+    assert sig.hex().upper() == row["signature"].upper()
+
+
+def test_sign_fhe_with_k0_vector1_8x8_limbs(env):
+    sig, row = _sign_case(env, "1", COMPAT)
+    assert sig.hex().upper() == row["signature"].upper()
+
+
+def test_sign_fhe_fast_mode_vector15(env):
+    sig, row = _sign_case(env, "15", FAST)
+    assert sig.hex().upper() == row["signature"].upper()
+
+
+def test_sign_fhe_vector0(env):
+    """sign_fhe (src/schnorr.rs:154): encrypts the private key itself."""
+    sig = Schnorr().sign_fhe(bytes(32), bytes(32), 3, env)
+    assert sig.hex().upper() == ROWS["0"]["signature"].upper()
