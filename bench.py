@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0xF11E51)
+    ap.add_argument("--no-ops", action="store_true", help="skip the 256-bit mul / sign wall-clock legs")
     return ap.parse_args()
 
 
@@ -88,6 +89,45 @@ def cpu_baseline(seed, target_s):
     return {"value": count / dt, "unit": "PBS/s", "cores": threads, "kind": "port",
             "sample": f"{count} PBS (KS+BR+SE, same params/keys shape) with the C oracle, "
                       f"OpenMP {threads} threads, {dt:.1f} s"}
+
+
+def ops_legs(ck, ctx, seed):
+    """configs 2 and 4: BigUintFHE 256-bit mul wall-clock and sign_fhe_with_k0 seconds (every rank
+    runs its own replica: the N-GPU line is the 'one sign per GPU' batch of configs[4])."""
+    import random
+    from fhe_sign import COMPAT, FAST, BigUintFHE, Schnorr, compute_nonce, set_server_key, stats
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    set_server_key(ctx)
+    rng = random.Random(seed)
+    a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(256) | 1 << 255
+    A, B = BigUintFHE.new(a, ck), BigUintFHE.new(b, ck)
+    out = {}
+
+    def leg(name, fn, check):
+        p0, l0 = stats(ctx)
+        t0 = time.perf_counter()
+        r = fn()
+        ctx.sync()
+        dt = time.perf_counter() - t0
+        p1, l1 = stats(ctx)
+        if not check(r):
+            raise SystemExit(f"bench: {name} result mismatch")
+        out[name] = {"seconds": dt, "pbs": p1 - p0, "levels": l1 - l0}
+
+    A.add(B, FAST)  # warm-up (LUT registration, pools)
+    import ref_semantics as R
+    leg("biguint256_mul_compat", lambda: A.mul(B, COMPAT),
+        lambda r: r.decrypt_limbs(ck) == R.biguint_mul(R.to_u32_digits(a), R.to_u32_digits(b)))
+    leg("biguint256_mul_fast", lambda: A.mul(B, FAST), lambda r: r.to_biguint(ck) == a * b)
+    leg("biguint256_add_fast", lambda: A.add(B, FAST), lambda r: r.to_biguint(ck) == a + b)
+    d, msg = 3, bytes(32)  # BIP-340 vector 0 (tests/golden/bip340_vectors.csv row 0)
+    k0 = compute_nonce(d, msg, bytes(32))
+    dF = BigUintFHE.new(d, ck)
+    s = Schnorr()
+    ref = s.sign_with_k0(msg, k0, d)
+    leg("sign_fhe_with_k0_v0_compat", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT), lambda r: r == ref)
+    leg("sign_fhe_with_k0_v0_fast", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, FAST), lambda r: r == ref)
+    return out
 
 
 def main():
@@ -143,6 +183,11 @@ def main():
     if not ok:
         raise SystemExit("bench: decryption check failed")
 
+    ops = None if a.no_ops else ops_legs(ck, ctx, a.seed)
+    if ops is not None and dist is not None:
+        for k in ops:
+            ops[k]["seconds"] = allmax(dist, ops[k]["seconds"])
+
     total = world * B * a.steps
     br_ms = float(np.mean(br_t))
     ks_ms = float(np.mean(ks_t))
@@ -184,6 +229,10 @@ def main():
                     "unit": "GB/s", "frac": hbm_bytes / (br_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
         },
     }
+    if ops is not None:
+        res["ops"] = ops
+        res["biguint256_mul_seconds"] = ops["biguint256_mul_compat"]["seconds"]
+        res["sign_fhe_with_k0_seconds"] = ops["sign_fhe_with_k0_v0_compat"]["seconds"]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_seconds)
     if rank == 0:
