@@ -1,0 +1,284 @@
+// br_wide.hip -- latency-optimised blind rotate: one ciphertext per 512-thread workgroup.
+//
+// Same arithmetic as k_blind_rotate (device_math.h contract; bit-exact vs oracle/tfhe_oracle.c:
+// fho_blind_rotate) but the per-ciphertext work is spread over 8 waves (4 per GLWE polynomial,
+// 4 FFT points per lane), so a small dependency level of the radix layer (tens to hundreds of
+// bootstraps, e.g. the serial window adds of BigUintFHE::mul, src/biguint.rs:232-249) finishes in
+// ~1/8 of the time a 2-wave ciphertext needs.  Used when a level has fewer ciphertexts than the
+// chip has CUs x 2; the 2-wave kernel stays the throughput kernel.
+//
+// Index bits b9..b0 of the 1024-point transform per phase (r = register 0..3, L = lane,
+// q = wave within the polynomial 0..3):
+//   A  regs (b9,b8)   idx = 256 r + 4 L + q            DIF stages 0,1
+//   B  regs (b7,b6)   idx = 256 (L>>4) + 64 r + 4 (L&15) + q   stages 2,3
+//   C  regs (b5,b4)   idx = 64 (L>>2) + 16 r + 4 (L&3) + q     stages 4,5
+//   D  regs (b3,b2)   idx = 16 L + 4 r + q                     stages 6,7
+//   E  regs (b1,b0)   idx = 256 q + 4 L + r  (= the BSK layout R = 4q + r)  stages 8,9
+// A<->B<->C<->D keep (b1,b0) = q fixed, so those exchanges are wave-private (no barrier); only
+// D<->E crosses waves.  LDS layouts: linear bit-weight maps found by tools/lds_layout_search.py.
+#include "device_math.h"
+#include "kernels.h"
+
+namespace fhe {
+
+namespace {
+// intra-wave region (256 entries + pad): weights of e-bits 0..7
+constexpr int WI[8] = {1, 2, 4, 8, 16, 34, 69, 136};
+constexpr int INTRA_SZ = 272;
+// cross-wave region per polynomial (1024 entries + pad): weights of idx-bits 0..9
+constexpr int WX[10] = {1, 2, 4, 8, 16, 32, 66, 131, 264, 528};
+constexpr int CROSS_SZ = 1056;
+constexpr int ROT_SZ = 2560;  // u64 accumulator staging: pos(c) = c + (c >> 2)
+
+FHE_DEV constexpr int fi(int e) {
+    return ((e & 1) ? WI[0] : 0) + ((e & 2) ? WI[1] : 0) + ((e & 4) ? WI[2] : 0) + ((e & 8) ? WI[3] : 0) +
+           ((e & 16) ? WI[4] : 0) + ((e & 32) ? WI[5] : 0) + ((e & 64) ? WI[6] : 0) + ((e & 128) ? WI[7] : 0);
+}
+FHE_DEV constexpr int fx(int x) {
+    return ((x & 1) ? WX[0] : 0) + ((x & 2) ? WX[1] : 0) + ((x & 4) ? WX[2] : 0) + ((x & 8) ? WX[3] : 0) +
+           ((x & 16) ? WX[4] : 0) + ((x & 32) ? WX[5] : 0) + ((x & 64) ? WX[6] : 0) + ((x & 128) ? WX[7] : 0) +
+           ((x & 256) ? WX[8] : 0) + ((x & 512) ? WX[9] : 0);
+}
+
+// radix-2 DIF pair (a, c) -> (a + c, (a - c) w) ; DIT pair (a, c) -> (a + c w~, a - c w~)
+FHE_DEV void dif(cplx& a, cplx& c, cplx w) {
+    cplx s = cadd(a, c), d = csub(a, c);
+    a = s;
+    c = cmul(d, w);
+}
+FHE_DEV void dit(cplx& a, cplx& c, cplx wconj) {
+    cplx t = cmul(c, wconj);
+    cplx s = cadd(a, t), d = csub(a, t);
+    a = s;
+    c = d;
+}
+
+// two DIF stages on regs (r,r+2) then (r,r+1) with twiddles tw0 (r=0), tw1 (r=1), tw2
+FHE_DEV void dif2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
+    dif(x[0], x[2], tw0);
+    dif(x[1], x[3], tw1);
+    dif(x[0], x[1], tw2);
+    dif(x[2], x[3], tw2);
+}
+FHE_DEV void dit2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
+    dit(x[0], x[1], conj_(tw2));
+    dit(x[2], x[3], conj_(tw2));
+    dit(x[0], x[2], conj_(tw0));
+    dit(x[1], x[3], conj_(tw1));
+}
+}  // namespace
+
+// Per-thread twiddle table [12][256] (t = 64 q + L), built on the host (context.cpp:wide_twiddles).
+__global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(const uint64_t* __restrict__ ms, int ms_stride,
+                                                              const PbsDesc* __restrict__ desc,
+                                                              const uint32_t* __restrict__ lut_idx,
+                                                              const uint64_t* __restrict__ luts,
+                                                              const cplx* __restrict__ bsk,
+                                                              const cplx* __restrict__ tw,   // [12][256]
+                                                              const cplx* __restrict__ psiw, // [4][256]
+                                                              uint64_t* __restrict__ out, int n) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_rot[2][ROT_SZ];
+    __shared__ __attribute__((aligned(16))) cplx s_intra[8][INTRA_SZ];
+    __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
+    __shared__ __attribute__((aligned(16))) cplx s_dx[2][1024];
+
+    const int ct = blockIdx.x;
+    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int p = w >> 2, q = w & 3, t = threadIdx.x & 255;
+    const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
+
+    // loop-invariant per-thread twiddles and twist factors (held in registers)
+    cplx T[12], PS[4];
+#pragma unroll
+    for (int s = 0; s < 12; ++s) T[s] = tw[s * 256 + t];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) PS[r] = psiw[r * 256 + t];
+
+    // accumulator: coefficient c = 256 r' + 4 L + q, r' = 0..7
+    uint64_t acc[8];
+    {
+        const uint32_t bt = modswitch_2n(a_ct[n]);
+        const int rot = (int)((4096u - bt) & 4095u);
+        const uint64_t* lut = luts + (size_t)(desc ? desc[ct].lut : lut_idx[ct]) * 2048;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            uint64_t v = 0;
+            if (p == 1) {
+                const uint32_t u = (uint32_t)(256 * r + 4 * L + q - rot) & 4095u;
+                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
+                v = (lut[u & 2047u] ^ neg) - neg;
+            }
+            acc[r] = v;
+        }
+    }
+    uint64_t* rot_me = s_rot[p];
+    cplx* intra = s_intra[w];
+    cplx* cross = s_cross[p];
+    // lane parts of the linear LDS maps
+    const int iA = fi(L), iB = fi(64 * (L >> 4) + (L & 15)), iC = fi(16 * (L >> 2) + (L & 3)), iD = fi(4 * L);
+    const int xD = fx(16 * L + q), xE = fx(256 * q + 4 * L);
+
+    uint32_t a_next = modswitch_2n(a_ct[0]);
+    for (int i = 0; i < n; ++i) {
+        const uint32_t a = a_next;
+        a_next = modswitch_2n(a_ct[i + 1]);
+        if (a == 0) continue;
+
+        // BSK slice for this iteration (issued early; consumed after the forward FFT)
+        cplx B0[4], B1[4];
+        {
+            const cplx* b0 = bsk + ((size_t)((i * 2 + 0) * 2 + p) * 16 + 4 * q) * 64 + L;
+            const cplx* b1 = bsk + ((size_t)((i * 2 + 1) * 2 + p) * 16 + 4 * q) * 64 + L;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                B0[r] = b0[r * 64];
+                B1[r] = b1[r * 64];
+            }
+        }
+
+        // ---- rotate (X^a acc - acc), decompose, twist
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int c = 256 * r + 4 * L + q;
+            rot_me[c + (c >> 2)] = acc[r];
+        }
+        __syncthreads();
+        cplx x[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int32_t d2[2];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int rr = r + 4 * hh;
+                const uint32_t u = (uint32_t)(256 * rr + 4 * L + q - (int)a) & 4095u;
+                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
+                const uint32_t c = u & 2047u;
+                const uint64_t v = (rot_me[c + (c >> 2)] ^ neg) - neg;
+                d2[hh] = decomp1<23>(v - acc[rr]);
+            }
+            x[r] = cmul(make_double2((double)d2[0], (double)d2[1]), PS[r]);
+        }
+
+        // ---- forward FFT: A (stages 0,1) -> B -> C -> D (wave-private) -> E (cross-wave)
+        dif2(x, T[0], T[1], T[2]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) intra[iA + fi(64 * r)] = x[r];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = intra[iB + fi(16 * r)];
+        dif2(x, T[3], T[4], T[5]);
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) intra[iB + fi(16 * r)] = x[r];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = intra[iC + fi(4 * r)];
+        dif2(x, T[6], T[7], T[8]);
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) intra[iC + fi(4 * r)] = x[r];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = intra[iD + fi(r)];
+        dif2(x, T[9], T[10], T[11]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cross[xD + fx(4 * r)] = x[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = cross[xE + fx(r)];
+        // phase E: stage 8 (r=1 twiddle i), stage 9 (twiddle 1)
+        {
+            cplx a0 = x[0], c0 = x[2], a1 = x[1], c1 = x[3];
+            x[0] = cadd(a0, c0); x[2] = csub(a0, c0);
+            x[1] = cadd(a1, c1); x[3] = mul_i(csub(a1, c1));
+            a0 = x[0]; c0 = x[1]; x[0] = cadd(a0, c0); x[1] = csub(a0, c0);
+            a1 = x[2]; c1 = x[3]; x[2] = cadd(a1, c1); x[3] = csub(a1, c1);
+        }
+
+        // ---- swap Fourier digits between the two polynomials, pointwise MAC
+        cplx* dx_me = s_dx[p] + 4 * q * 64 + L;
+        const cplx* dx_other = s_dx[p ^ 1] + 4 * q * 64 + L;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dx_me[r * 64] = x[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const cplx oth = dx_other[r * 64];
+            const cplx d0 = (p == 0) ? x[r] : oth;
+            const cplx d1 = (p == 0) ? oth : x[r];
+            cplx o;
+            o.x = __fma_rn(d0.x, B0[r].x, __fma_rn(-d0.y, B0[r].y, __fma_rn(d1.x, B1[r].x, -(d1.y * B1[r].y))));
+            o.y = __fma_rn(d0.x, B0[r].y, __fma_rn(d0.y, B0[r].x, __fma_rn(d1.x, B1[r].y, d1.y * B1[r].x)));
+            x[r] = o;
+        }
+
+        // ---- inverse FFT: E -> D (cross-wave) -> C -> B -> A (wave-private)
+        {
+            cplx a0 = x[0], c0 = x[1], a1 = x[2], c1 = x[3];
+            x[0] = cadd(a0, c0); x[1] = csub(a0, c0);
+            x[2] = cadd(a1, c1); x[3] = csub(a1, c1);
+            a0 = x[0]; c0 = x[2]; x[0] = cadd(a0, c0); x[2] = csub(a0, c0);
+            a1 = x[1]; c1 = mul_negi(x[3]); x[1] = cadd(a1, c1); x[3] = csub(a1, c1);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cross[xE + fx(r)] = x[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = cross[xD + fx(4 * r)];
+        dit2(x, T[9], T[10], T[11]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) intra[iD + fi(r)] = x[r];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = intra[iC + fi(4 * r)];
+        dit2(x, T[6], T[7], T[8]);
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) intra[iC + fi(4 * r)] = x[r];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = intra[iB + fi(16 * r)];
+        dit2(x, T[3], T[4], T[5]);
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) intra[iB + fi(16 * r)] = x[r];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = intra[iA + fi(64 * r)];
+        wave_sync();
+        dit2(x, T[0], T[1], T[2]);
+
+        // ---- untwist, round, accumulate (x[r] = idx 256 r + 4 L + q -> coefs idx, idx + 1024)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const cplx u = make_double2(PS[r].x * 0.0009765625, -PS[r].y * 0.0009765625);
+            const cplx y = cmul(x[r], u);
+            acc[r] += f64_to_torus(y.x);
+            acc[r + 4] += f64_to_torus(y.y);
+        }
+    }
+
+    // ---- sample extract
+    uint64_t* o = desc ? desc[ct].dst : out + (size_t)ct * 2049;
+    if (p == 0) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int j = 256 * r + 4 * L + q;
+            if (j == 0) o[0] = acc[r];
+            else o[2048 - j] = 0ull - acc[r];
+        }
+    } else if (t == 0) {
+        o[2048] = acc[0];
+    }
+}
+
+hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
+                                    const uint64_t* luts, const double2* bsk, const double2* tw, const double2* psiw,
+                                    uint64_t* out, int count, int n, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_blind_rotate_wide, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk, tw,
+                       psiw, out, n);
+    return hipGetLastError();
+}
+
+}  // namespace fhe

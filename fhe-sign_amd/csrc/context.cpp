@@ -2,6 +2,7 @@
 #include "context.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "kernels.h"
@@ -47,6 +48,20 @@ void lane_twiddles(const std::vector<double2>& W, std::vector<double2>* Wl) {
     }
 }
 
+void wide_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,
+                 std::vector<double2>* psiw) {
+    tw->assign(12 * 256, make_double2(0.0, 0.0));
+    psiw->assign(4 * 256, make_double2(0.0, 0.0));
+    for (int t = 0; t < 256; ++t) {
+        const int q = t >> 6, L = t & 63;
+        const int a = 4 * L + q, b = 4 * (L & 15) + q, c = 4 * (L & 3) + q;
+        const int slot[12] = {a, 256 + a, a << 1, b << 2, (64 + b) << 2, b << 3,
+                              c << 4, (16 + c) << 4, c << 5, q << 6, (4 + q) << 6, q << 7};
+        for (int s = 0; s < 12; ++s) (*tw)[s * 256 + t] = W[slot[s]];
+        for (int r = 0; r < 4; ++r) (*psiw)[r * 256 + t] = psi[256 * r + 4 * L + q];
+    }
+}
+
 void make_lut_poly(const Params& p, const uint32_t* f, std::vector<uint64_t>* lut) {
     const uint32_t mods = p.msg_carry();
     const uint32_t box = kPolySize / mods, half = box / 2;
@@ -71,7 +86,7 @@ int fhe_ctx::ensure_ms(size_t count) {
     }
     size_t cap = count < 256 ? 256 : count;
     ms_stride = (int)((p.n + 1 + 7) / 8 * 8);
-    FHE_HIP_CHECK(hipMalloc(&d_ms, cap * ms_stride * sizeof(uint16_t)));
+    FHE_HIP_CHECK(hipMalloc(&d_ms, cap * ms_stride * sizeof(uint64_t)));
     ms_cap = cap;
     return FHE_OK;
 }
@@ -148,8 +163,7 @@ int fhe_ctx::pbs_device(const uint64_t* d_in, size_t count, const uint32_t* d_lu
     if (timing) FHE_HIP_CHECK(hipEventRecord(ev[0], stream));
     FHE_HIP_CHECK(launch_keyswitch(d_in, (int)count, d_ksk, d_ms, ms_stride, (int)p.n, stream));
     if (timing) FHE_HIP_CHECK(hipEventRecord(ev[1], stream));
-    FHE_HIP_CHECK(launch_blind_rotate(d_ms, ms_stride, d_lut, d_luts, d_bsk, d_W, d_psi, d_out, (int)count,
-                                      (int)p.n, stream));
+    FHE_HIP_CHECK(blind_rotate(nullptr, d_lut, d_out, count));
     if (timing) {
         FHE_HIP_CHECK(hipEventRecord(ev[2], stream));
         FHE_HIP_CHECK(hipEventSynchronize(ev[2]));
@@ -157,6 +171,16 @@ int fhe_ctx::pbs_device(const uint64_t* d_in, size_t count, const uint32_t* d_lu
         FHE_HIP_CHECK(hipEventElapsedTime(&last_br_ms, ev[1], ev[2]));
     }
     return FHE_OK;
+}
+
+hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_idx, uint64_t* out, size_t count) {
+    if ((int)count <= wide_threshold)
+        return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide, out,
+                                        (int)count, (int)p.n, stream);
+    if (desc)
+        return launch_blind_rotate_desc(d_ms, ms_stride, desc, d_luts, d_bsk, d_W, d_psi, (int)count, (int)p.n,
+                                        stream);
+    return launch_blind_rotate(d_ms, ms_stride, lut_idx, d_luts, d_bsk, d_W, d_psi, out, (int)count, (int)p.n, stream);
 }
 
 // =========================================================================== C ABI (core)
@@ -258,9 +282,15 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
         return FHE_ERR_HIP;
     }
     for (auto& ev : c->ev) FHE_HIP_CHECK(hipEventCreate(&ev));
-    std::vector<double2> W0, W, psi;
+    std::vector<double2> W0, W, psi, tww, psiw;
     fft_tables(&W0, &psi);
     lane_twiddles(W0, &W);
+    wide_tables(W0, psi, &tww, &psiw);
+    FHE_HIP_CHECK(hipMalloc(&c->d_tw_wide, tww.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMalloc(&c->d_psi_wide, psiw.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMemcpy(c->d_tw_wide, tww.data(), tww.size() * sizeof(double2), hipMemcpyHostToDevice));
+    FHE_HIP_CHECK(hipMemcpy(c->d_psi_wide, psiw.data(), psiw.size() * sizeof(double2), hipMemcpyHostToDevice));
+    if (const char* e = getenv("FHE_WIDE_THRESHOLD")) c->wide_threshold = atoi(e);
     FHE_HIP_CHECK(hipMalloc(&c->d_W, W.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMalloc(&c->d_psi, psi.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_W, W.data(), W.size() * sizeof(double2), hipMemcpyHostToDevice));
@@ -275,7 +305,7 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     delete c->engine;
     c->engine = nullptr;
-    void* ptrs[] = {c->d_ksk, c->d_bsk, c->d_W, c->d_psi, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out,
+    void* ptrs[] = {c->d_ksk, c->d_bsk, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out,
                     c->d_stage_lut};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -415,6 +445,12 @@ int fhe_memcpy_d2h(fhe_ctx* c, void* dst, const void* src, size_t bytes) {
     FHE_HIP_CHECK(hipSetDevice(c->device));
     FHE_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return FHE_OK;
+}
+
+int fhe_ctx_set_wide_threshold(fhe_ctx* c, int threshold) {
+    if (!c) return FHE_ERR_INVALID;
+    c->wide_threshold = threshold;
     return FHE_OK;
 }
 

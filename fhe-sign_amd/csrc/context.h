@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "keys.h"
+#include "kernels.h"
 
 namespace fhe {
 
@@ -26,6 +27,9 @@ void set_error(const std::string& msg);
 void fft_tables(std::vector<double2>* W, std::vector<double2>* psi);
 // Per-lane twiddle table [slot][lane] (device_math.h:tw_slot) built from W.
 void lane_twiddles(const std::vector<double2>& W, std::vector<double2>* Wl);
+// Per-thread tables of the wide (latency) blind rotate: tw[12][256], psi[4][256] (br_wide.hip).
+void wide_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,
+                 std::vector<double2>* psiw);
 // Accumulator polynomial of a univariate LUT (tfhe shortint box encoding, padding bit).
 void make_lut_poly(const Params& p, const uint32_t* f, std::vector<uint64_t>* lut);
 
@@ -40,6 +44,10 @@ struct fhe_ctx {
     double2* d_bsk = nullptr;  // Fourier BSK, blind-rotate layout
     double2* d_W = nullptr;    // per-lane twiddle table [30][64]
     double2* d_psi = nullptr;
+    double2* d_tw_wide = nullptr;   // [12][256]
+    double2* d_psi_wide = nullptr;  // [4][256]
+    // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU)
+    int wide_threshold = 1024;
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;
@@ -47,7 +55,7 @@ struct fhe_ctx {
     size_t d_luts_cap = 0;  // in LUTs
     bool luts_dirty = false;
     // PBS workspace
-    uint16_t* d_ms = nullptr;
+    uint64_t* d_ms = nullptr;  // keyswitched small LWE (u64, stride ms_stride >= n+1)
     size_t ms_cap = 0;  // ciphertexts
     int ms_stride = 0;
     uint64_t* d_stage_in = nullptr;
@@ -67,4 +75,6 @@ struct fhe_ctx {
     int register_lut(const uint32_t* table, uint32_t* id);
     // KS + BR(+SE) over device arrays, async on `stream`
     int pbs_device(const uint64_t* d_in, size_t count, const uint32_t* d_lut, uint64_t* d_out);
+    // blind rotate (+SE) of `count` modulus-switched inputs in d_ms, kernel chosen by batch size
+    hipError_t blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_idx, uint64_t* out, size_t count);
 };

@@ -34,16 +34,23 @@ FHE_DEV uint64_t ks_input(const uint64_t* __restrict__ in, const PbsDesc* __rest
     return a;
 }
 
+// The 2048 x 5 gadget rows can be split over gridDim.z workgroups (small batches: enough
+// workgroups to cover the chip); partial sums then meet through 64-bit atomic adds, which are
+// exact and order-independent mod 2^64, so results stay bit-identical.  Output: the small LWE
+// (n+1 words, stride ks_stride) in u64; the blind rotate applies the modulus switch on load.
 template <bool DESC>
 __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ in,
                                                   const PbsDesc* __restrict__ desc, int count,
                                                   const uint64_t* __restrict__ ksk,
-                                                  uint16_t* __restrict__ ms, int ms_stride,
+                                                  uint64_t* __restrict__ small, int ks_stride,
                                                   int n) {
     __shared__ int8_t dig[KS_J][KS_LVL][KS_C];
     const int c0 = blockIdx.x * KS_C;
     const int k = blockIdx.y * 256 + threadIdx.x;
     const bool active = k <= n;
+    const int nsplit = gridDim.z;
+    const int jspan = 2048 / nsplit;
+    const int jbeg = blockIdx.z * jspan, jend = jbeg + jspan;
     uint64_t acc[KS_C];
 #pragma unroll
     for (int c = 0; c < KS_C; ++c) acc[c] = 0;
@@ -51,7 +58,7 @@ __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ 
     const int tid = threadIdx.x;
     const int dc = tid >> 4, dj = tid & (KS_J - 1);  // digit producer: 16 consecutive j per ct
     const size_t row_stride = (size_t)(n + 1);
-    for (int j0 = 0; j0 < 2048; j0 += KS_J) {
+    for (int j0 = jbeg; j0 < jend; j0 += KS_J) {
         {
             const int ct = c0 + dc;
             uint64_t a = (ct < count) ? ks_input<DESC>(in, desc, ct, j0 + dj) : 0ull;
@@ -87,8 +94,12 @@ __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ 
         const int ct = c0 + c;
         if (ct >= count) break;
         uint64_t v = acc[c];
-        if (k == n) v += ks_input<DESC>(in, desc, ct, 2048);
-        ms[(size_t)ct * ms_stride + k] = (uint16_t)modswitch_2n(v);
+        if (k == n && blockIdx.z == 0) v += ks_input<DESC>(in, desc, ct, 2048);
+        uint64_t* dst = small + (size_t)ct * ks_stride + k;
+        if (nsplit == 1)
+            *dst = v;
+        else
+            atomicAdd((unsigned long long*)dst, (unsigned long long)v);
     }
 }
 
@@ -118,7 +129,7 @@ FHE_DEV void pointwise_mac(cplx (&x)[16], const cplx* __restrict__ other,
 }
 
 template <bool DESC>
-__global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restrict__ ms, int ms_stride,
+__global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint64_t* __restrict__ ms, int ms_stride,
                                                      const uint32_t* __restrict__ lut_idx,
                                                      const PbsDesc* __restrict__ desc,
                                                      const uint64_t* __restrict__ luts,
@@ -132,11 +143,11 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restr
     cplx* sc = lds[w];
     cplx* sc_other = lds[w ^ 1];
     uint64_t* scu = reinterpret_cast<uint64_t*>(sc);
-    const uint16_t* a_ct = ms + (size_t)ct * ms_stride;
+    const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
 
     uint64_t acc[32];
     {
-        const uint32_t bt = a_ct[n];
+        const uint32_t bt = modswitch_2n(a_ct[n]);
         const int rot = (int)((4096u - bt) & 4095u);  // X^{-b}
         const uint64_t* lut = luts + (size_t)(DESC ? desc[ct].lut : lut_idx[ct]) * 2048;
 #pragma unroll
@@ -151,10 +162,10 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint16_t* __restr
         }
     }
 
-    uint32_t a_next = a_ct[0];
+    uint32_t a_next = modswitch_2n(a_ct[0]);
     for (int i = 0; i < n; ++i) {
         const uint32_t a = a_next;
-        a_next = a_ct[i + 1];
+        a_next = modswitch_2n(a_ct[i + 1]);
         if (a == 0) continue;  // X^0 - 1 = 0: the external product is exactly zero
         // Keep the twiddle / twist tables out of the register file: re-derive their base pointers
         // every iteration so their (L1-resident) loads are not hoisted out of the loop.
@@ -255,23 +266,40 @@ __global__ __launch_bounds__(64) void k_bsk_to_fourier(const uint64_t* __restric
 }
 
 // ============================================================================ launchers
-hipError_t launch_keyswitch(const uint64_t* in, int count, const uint64_t* ksk, uint16_t* ms,
-                            int ms_stride, int n, hipStream_t s) {
+static int ks_splits(int count, int n) {
+    const int base = ((count + KS_C - 1) / KS_C) * ((n + 1 + 255) / 256);
+    int s = 1;
+    while (s < 64 && base * s * 2 <= 1024) s *= 2;  // aim for ~512-1024 workgroups
+    return s;
+}
+
+hipError_t launch_keyswitch(const uint64_t* in, int count, const uint64_t* ksk, uint64_t* small,
+                            int ks_stride, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    dim3 grid((count + KS_C - 1) / KS_C, (n + 1 + 255) / 256);
-    hipLaunchKernelGGL(k_keyswitch<false>, grid, dim3(256), 0, s, in, nullptr, count, ksk, ms, ms_stride, n);
+    const int z = ks_splits(count, n);
+    if (z > 1) {
+        hipError_t e = hipMemsetAsync(small, 0, (size_t)count * ks_stride * 8, s);
+        if (e != hipSuccess) return e;
+    }
+    dim3 grid((count + KS_C - 1) / KS_C, (n + 1 + 255) / 256, z);
+    hipLaunchKernelGGL(k_keyswitch<false>, grid, dim3(256), 0, s, in, nullptr, count, ksk, small, ks_stride, n);
     return hipGetLastError();
 }
 
-hipError_t launch_keyswitch_desc(const PbsDesc* desc, int count, const uint64_t* ksk, uint16_t* ms,
-                                 int ms_stride, int n, hipStream_t s) {
+hipError_t launch_keyswitch_desc(const PbsDesc* desc, int count, const uint64_t* ksk, uint64_t* small,
+                                 int ks_stride, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    dim3 grid((count + KS_C - 1) / KS_C, (n + 1 + 255) / 256);
-    hipLaunchKernelGGL(k_keyswitch<true>, grid, dim3(256), 0, s, nullptr, desc, count, ksk, ms, ms_stride, n);
+    const int z = ks_splits(count, n);
+    if (z > 1) {
+        hipError_t e = hipMemsetAsync(small, 0, (size_t)count * ks_stride * 8, s);
+        if (e != hipSuccess) return e;
+    }
+    dim3 grid((count + KS_C - 1) / KS_C, (n + 1 + 255) / 256, z);
+    hipLaunchKernelGGL(k_keyswitch<true>, grid, dim3(256), 0, s, nullptr, desc, count, ksk, small, ks_stride, n);
     return hipGetLastError();
 }
 
-hipError_t launch_blind_rotate(const uint16_t* ms, int ms_stride, const uint32_t* lut_idx,
+hipError_t launch_blind_rotate(const uint64_t* ms, int ms_stride, const uint32_t* lut_idx,
                                const uint64_t* luts, const cplx* bsk, const cplx* W,
                                const cplx* psi, uint64_t* out, int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
@@ -280,7 +308,7 @@ hipError_t launch_blind_rotate(const uint16_t* ms, int ms_stride, const uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_blind_rotate_desc(const uint16_t* ms, int ms_stride, const PbsDesc* desc,
+hipError_t launch_blind_rotate_desc(const uint64_t* ms, int ms_stride, const PbsDesc* desc,
                                     const uint64_t* luts, const cplx* bsk, const cplx* W,
                                     const cplx* psi, int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;

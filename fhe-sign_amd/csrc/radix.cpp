@@ -203,9 +203,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     hip_check(launch_keyswitch_desc(dev, (int)gpu.size(), ctx_->d_ksk, ctx_->d_ms, ctx_->ms_stride, (int)p.n,
                                     ctx_->stream),
               "keyswitch");
-    hip_check(launch_blind_rotate_desc(ctx_->d_ms, ctx_->ms_stride, dev, ctx_->d_luts, ctx_->d_bsk, ctx_->d_W,
-                                       ctx_->d_psi, (int)gpu.size(), (int)p.n, ctx_->stream),
-              "blind rotate");
+    hip_check(ctx_->blind_rotate(dev, nullptr, nullptr, gpu.size()), "blind rotate");
     pbs_count += gpu.size();
     levels += 1;
     return out;

@@ -51,6 +51,7 @@ _SIGNATURES = [
     ("fhe_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     ("fhe_ctx_last_pbs_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("fhe_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("fhe_ctx_set_wide_threshold", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_radix_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u64p, C.c_uint32, C.POINTER(C.c_void_p)]),
     ("fhe_radix_trivial", C.c_int, [C.c_void_p, u64p, C.c_uint32, C.POINTER(C.c_void_p)]),
     ("fhe_radix_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u64p, C.c_size_t]),

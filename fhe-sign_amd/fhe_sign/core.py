@@ -149,6 +149,9 @@ class Context:
     def sync(self) -> None:
         check(load().fhe_ctx_sync(self._h))
 
+    def set_wide_threshold(self, threshold: int) -> None:
+        check(load().fhe_ctx_set_wide_threshold(self._h, int(threshold)))
+
     def enable_timing(self, on: bool = True) -> None:
         check(load().fhe_ctx_enable_timing(self._h, 1 if on else 0))
 

@@ -85,3 +85,24 @@ def test_pbs_empty_batch(env):
     _, _, _, ctx = env
     out = ctx.pbs(np.zeros((0, 2049), np.uint64), 0)
     assert out.shape == (0, 2049)
+
+
+def test_wide_and_narrow_kernels_bit_identical(env):
+    """The latency kernel (br_wide.hip, 8 waves per ciphertext) and the throughput kernel
+    (2 waves per ciphertext) implement the same arithmetic: identical output words."""
+    _, _, ok, ctx = env
+    tables = _luts()
+    ids = [ctx.lut(t) for t in tables]
+    r = ok.rng(777)
+    cts = np.stack([ok.encrypt(r, i % 16) for i in range(24)])
+    lut_ids = np.array([ids[i % len(ids)] for i in range(24)], np.uint32)
+    try:
+        ctx.set_wide_threshold(0)
+        narrow = ctx.pbs(cts, lut_ids)
+        ctx.set_wide_threshold(1 << 30)
+        wide = ctx.pbs(cts, lut_ids)
+    finally:
+        ctx.set_wide_threshold(1024)
+    assert np.array_equal(narrow, wide)
+    ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
+    assert np.array_equal(wide[:6], ref)
