@@ -14,26 +14,21 @@
 //   C  regs (b5,b4)   idx = 64 (L>>2) + 16 r + 4 (L&3) + q     stages 4,5
 //   D  regs (b3,b2)   idx = 16 L + 4 r + q                     stages 6,7
 //   E  regs (b1,b0)   idx = 256 q + 4 L + r  (= the BSK layout R = 4q + r)  stages 8,9
-// A<->B<->C<->D keep (b1,b0) = q fixed, so those exchanges are wave-private (no barrier); only
-// D<->E crosses waves.  LDS layouts: linear bit-weight maps found by tools/lds_layout_search.py.
+// A<->B<->C<->D keep (b1,b0) = q fixed, so those exchanges are wave-private 2x2 transposes of
+// register bits with lane bits, done in registers: v_permlane32_swap / v_permlane16_swap for lane
+// bits 5,4 and DPP row shifts + select for lane bits 3..0.  Only D<->E crosses waves (LDS, linear
+// bit-weight layout found by tools/lds_layout_search.py).
 #include "device_math.h"
 #include "kernels.h"
 
 namespace fhe {
 
 namespace {
-// intra-wave region (256 entries + pad): weights of e-bits 0..7
-constexpr int WI[8] = {1, 2, 4, 8, 16, 34, 69, 136};
-constexpr int INTRA_SZ = 272;
 // cross-wave region per polynomial (1024 entries + pad): weights of idx-bits 0..9
 constexpr int WX[10] = {1, 2, 4, 8, 16, 32, 66, 131, 264, 528};
 constexpr int CROSS_SZ = 1056;
 constexpr int ROT_SZ = 2560;  // u64 accumulator staging: pos(c) = c + (c >> 2)
 
-FHE_DEV constexpr int fi(int e) {
-    return ((e & 1) ? WI[0] : 0) + ((e & 2) ? WI[1] : 0) + ((e & 4) ? WI[2] : 0) + ((e & 8) ? WI[3] : 0) +
-           ((e & 16) ? WI[4] : 0) + ((e & 32) ? WI[5] : 0) + ((e & 64) ? WI[6] : 0) + ((e & 128) ? WI[7] : 0);
-}
 FHE_DEV constexpr int fx(int x) {
     return ((x & 1) ? WX[0] : 0) + ((x & 2) ? WX[1] : 0) + ((x & 4) ? WX[2] : 0) + ((x & 8) ? WX[3] : 0) +
            ((x & 16) ? WX[4] : 0) + ((x & 32) ? WX[5] : 0) + ((x & 64) ? WX[6] : 0) + ((x & 128) ? WX[7] : 0) +
@@ -51,6 +46,70 @@ FHE_DEV void dit(cplx& a, cplx& c, cplx wconj) {
     cplx s = cadd(a, t), d = csub(a, t);
     a = s;
     c = d;
+}
+
+// ---- in-register 2x2 transposes between a register bit and a lane bit (wave-private exchanges)
+// X holds register bit 0, Y register bit 1; afterwards the register bit and lane bit k are swapped.
+FHE_DEV void u64_split(double d, uint32_t& lo, uint32_t& hi) {
+    const uint64_t b = (uint64_t)__double_as_longlong(d);
+    lo = (uint32_t)b;
+    hi = (uint32_t)(b >> 32);
+}
+FHE_DEV double u64_join(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int K>  // K = 5 (v_permlane32_swap) or 4 (v_permlane16_swap)
+FHE_DEV void xpose_permlane(cplx& X, cplx& Y) {
+    uint32_t x[4], y[4];
+    u64_split(X.x, x[0], x[1]);
+    u64_split(X.y, x[2], x[3]);
+    u64_split(Y.x, y[0], y[1]);
+    u64_split(Y.y, y[2], y[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        auto r = K == 5 ? __builtin_amdgcn_permlane32_swap(x[d], y[d], false, false)
+                        : __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+        x[d] = r[0];
+        y[d] = r[1];
+    }
+    X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
+    Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
+}
+// K in 0..3: DPP row shifts by 2^K inside 16-lane rows, then a per-lane select
+template <int K>
+FHE_DEV void xpose_dpp(cplx& X, cplx& Y, bool hi) {
+    constexpr int SH = 1 << K;
+    uint32_t x[4], y[4];
+    u64_split(X.x, x[0], x[1]);
+    u64_split(X.y, x[2], x[3]);
+    u64_split(Y.x, y[0], y[1]);
+    u64_split(Y.y, y[2], y[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t ys = (uint32_t)__builtin_amdgcn_mov_dpp((int)y[d], 0x110 + SH, 0xF, 0xF, false);  // row_shr: y[l - SH]
+        const uint32_t xs = (uint32_t)__builtin_amdgcn_mov_dpp((int)x[d], 0x100 + SH, 0xF, 0xF, false);  // row_shl: x[l + SH]
+        const uint32_t nx = hi ? ys : x[d];
+        const uint32_t ny = hi ? y[d] : xs;
+        x[d] = nx;
+        y[d] = ny;
+    }
+    X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
+    Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
+}
+// register bits (1, 0) <-> lane bits (KH, KL): pairs (x0,x2),(x1,x3) for bit 1; (x0,x1),(x2,x3) for bit 0
+FHE_DEV void xpose_AB(cplx (&x)[4]) {
+    xpose_permlane<5>(x[0], x[2]);
+    xpose_permlane<5>(x[1], x[3]);
+    xpose_permlane<4>(x[0], x[1]);
+    xpose_permlane<4>(x[2], x[3]);
+}
+template <int KH, int KL>
+FHE_DEV void xpose_dpp2(cplx (&x)[4], int L) {
+    const bool h = (L >> KH) & 1, l = (L >> KL) & 1;
+    xpose_dpp<KH>(x[0], x[2], h);
+    xpose_dpp<KH>(x[1], x[3], h);
+    xpose_dpp<KL>(x[0], x[1], l);
+    xpose_dpp<KL>(x[2], x[3], l);
 }
 
 // two DIF stages on regs (r,r+2) then (r,r+1) with twiddles tw0 (r=0), tw1 (r=1), tw2
@@ -78,7 +137,6 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(const uint64_t* __
                                                               const cplx* __restrict__ psiw, // [4][256]
                                                               uint64_t* __restrict__ out, int n) {
     __shared__ __attribute__((aligned(16))) uint64_t s_rot[2][ROT_SZ];
-    __shared__ __attribute__((aligned(16))) cplx s_intra[8][INTRA_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_dx[2][1024];
 
@@ -112,10 +170,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(const uint64_t* __
         }
     }
     uint64_t* rot_me = s_rot[p];
-    cplx* intra = s_intra[w];
     cplx* cross = s_cross[p];
     // lane parts of the linear LDS maps
-    const int iA = fi(L), iB = fi(64 * (L >> 4) + (L & 15)), iC = fi(16 * (L >> 2) + (L & 3)), iD = fi(4 * L);
     const int xD = fx(16 * L + q), xE = fx(256 * q + 4 * L);
 
     uint32_t a_next = modswitch_2n(a_ct[0]);
@@ -161,25 +217,11 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(const uint64_t* __
 
         // ---- forward FFT: A (stages 0,1) -> B -> C -> D (wave-private) -> E (cross-wave)
         dif2(x, T[0], T[1], T[2]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) intra[iA + fi(64 * r)] = x[r];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = intra[iB + fi(16 * r)];
+        xpose_AB(x);                 // A -> B: regs <-> lane bits 5,4
         dif2(x, T[3], T[4], T[5]);
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) intra[iB + fi(16 * r)] = x[r];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = intra[iC + fi(4 * r)];
+        xpose_dpp2<3, 2>(x, L);      // B -> C: regs <-> lane bits 3,2
         dif2(x, T[6], T[7], T[8]);
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) intra[iC + fi(4 * r)] = x[r];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = intra[iD + fi(r)];
+        xpose_dpp2<1, 0>(x, L);      // C -> D: regs <-> lane bits 1,0
         dif2(x, T[9], T[10], T[11]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) cross[xD + fx(4 * r)] = x[r];
@@ -226,26 +268,11 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = cross[xD + fx(4 * r)];
         dit2(x, T[9], T[10], T[11]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) intra[iD + fi(r)] = x[r];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = intra[iC + fi(4 * r)];
+        xpose_dpp2<1, 0>(x, L);      // D -> C
         dit2(x, T[6], T[7], T[8]);
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) intra[iC + fi(4 * r)] = x[r];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = intra[iB + fi(16 * r)];
+        xpose_dpp2<3, 2>(x, L);      // C -> B
         dit2(x, T[3], T[4], T[5]);
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) intra[iB + fi(16 * r)] = x[r];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = intra[iA + fi(64 * r)];
-        wave_sync();
+        xpose_AB(x);                 // B -> A
         dit2(x, T[0], T[1], T[2]);
 
         // ---- untwist, round, accumulate (x[r] = idx 256 r + 4 L + q -> coefs idx, idx + 1024)
