@@ -128,7 +128,7 @@ FHE_DEV void dit2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
 }  // namespace
 
 // Per-thread twiddle table [12][256] (t = 64 q + L), built on the host (context.cpp:wide_twiddles).
-__global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(const uint64_t* __restrict__ ms, int ms_stride,
+__global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
                                                               const uint32_t* __restrict__ lut_idx,
                                                               const uint64_t* __restrict__ luts,

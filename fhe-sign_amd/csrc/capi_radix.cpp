@@ -56,7 +56,9 @@ fhe_radix* wrap(Radix r, uint32_t bits) {
     return x;
 }
 
-bool valid_bits(uint32_t bits) { return bits >= 2 && bits <= 128 && bits % 2 == 0; }
+bool valid_bits(uint32_t bits) { return bits >= 2 && bits <= FHE_RADIX_MAX_BITS && bits % 2 == 0; }
+
+BigConst words_of(const uint64_t* s, size_t nwords) { return BigConst(s, s + nwords); }
 
 // run a binary op on two radix of equal width
 template <class F>
@@ -247,7 +249,7 @@ int fhe_radix_shl(fhe_ctx* c, const fhe_radix* a, const fhe_radix* amount, fhe_r
     });
 }
 int fhe_radix_scalar_and(fhe_ctx* c, const fhe_radix* a, uint64_t mask, fhe_radix** out) {
-    return unop(c, a, out, [mask](Engine& e, const Radix& x) { return radix_scalar_and(e, x, mask, 0); });
+    return unop(c, a, out, [mask](Engine& e, const Radix& x) { return radix_scalar_and(e, x, mask); });
 }
 int fhe_radix_scalar_shr(fhe_ctx* c, const fhe_radix* a, uint32_t shift, fhe_radix** out) {
     if (!a) return FHE_ERR_INVALID;
@@ -278,6 +280,43 @@ int fhe_radix_scalar_rem(fhe_ctx* c, const fhe_radix* a, uint64_t d, fhe_radix**
         return FHE_ERR_INVALID;
     }
     return unop(c, a, out, [d](Engine& e, const Radix& x) { return radix_scalar_rem(e, x, d); });
+}
+// ---- wide clear operands (little-endian u64 words)
+int fhe_radix_scalar_and_words(fhe_ctx* c, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out) {
+    if (!s && nwords) return FHE_ERR_INVALID;
+    const BigConst v = words_of(s, nwords);
+    return unop(c, a, out, [&v](Engine& e, const Radix& x) { return radix_scalar_and(e, x, v); });
+}
+int fhe_radix_scalar_add_words(fhe_ctx* c, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out) {
+    if (!s && nwords) return FHE_ERR_INVALID;
+    const BigConst v = words_of(s, nwords);
+    return unop(c, a, out, [&v](Engine& e, const Radix& x) { return radix_scalar_add(e, x, v); });
+}
+int fhe_radix_scalar_mul_words(fhe_ctx* c, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out) {
+    if (!s && nwords) return FHE_ERR_INVALID;
+    const BigConst v = words_of(s, nwords);
+    return unop(c, a, out, [&v](Engine& e, const Radix& x) { return radix_scalar_mul(e, x, v); });
+}
+static bool all_zero(const uint64_t* s, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (s[i]) return false;
+    return true;
+}
+int fhe_radix_scalar_div_words(fhe_ctx* c, const fhe_radix* a, const uint64_t* d, size_t nwords, fhe_radix** out) {
+    if (!d || all_zero(d, nwords)) {
+        set_error("division by zero");
+        return FHE_ERR_INVALID;
+    }
+    const BigConst v = words_of(d, nwords);
+    return unop(c, a, out, [&v](Engine& e, const Radix& x) { return radix_scalar_div(e, x, v); });
+}
+int fhe_radix_scalar_rem_words(fhe_ctx* c, const fhe_radix* a, const uint64_t* d, size_t nwords, fhe_radix** out) {
+    if (!d || all_zero(d, nwords)) {
+        set_error("division by zero");
+        return FHE_ERR_INVALID;
+    }
+    const BigConst v = words_of(d, nwords);
+    return unop(c, a, out, [&v](Engine& e, const Radix& x) { return radix_scalar_rem(e, x, v); });
 }
 int fhe_radix_cast(fhe_ctx* c, const fhe_radix* a, uint32_t bits, fhe_radix** out) {
     if (!a || !out || !valid_bits(bits)) return FHE_ERR_INVALID;

@@ -47,7 +47,7 @@ struct fhe_ctx {
     double2* d_tw_wide = nullptr;   // [12][256]
     double2* d_psi_wide = nullptr;  // [4][256]
     // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU)
-    int wide_threshold = 768;  // crossover measured in profiles/r1/latency_sweep_r1d.txt
+    int wide_threshold = 640;  // crossover measured in profiles/r1/latency_sweep_r1e.txt
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;

@@ -81,44 +81,70 @@ FHE_DEV int swz_ab(int idx) { return idx + 4 * (idx >> 6); }
 FHE_DEV int swz_bc(int idx) { return idx + (idx >> 4); }
 
 // ---------------------------------------------------------------- forward FFT (DIF)
+// Read-only tables in global memory.  Explicit address space: a generic pointer would lower to
+// flat loads, which also count against lgkmcnt and so stall every LDS wait behind them.
+typedef double __attribute__((ext_vector_type(2))) dvec2;
+struct gcptr {
+    const __attribute__((address_space(1))) dvec2* p;
+    FHE_DEV cplx operator[](long i) const {
+        const dvec2 v = p[i];
+        return make_double2(v.x, v.y);
+    }
+    FHE_DEV gcptr operator+(long i) const { return gcptr{p + i}; }
+};
+FHE_DEV gcptr as_global(const cplx* p) { return gcptr{(const __attribute__((address_space(1))) dvec2*)p}; }
+
 // Twiddles come from a per-lane table Wl[slot * 64] (Wl = table + lane), slot = tw_slot(s, g):
 // phase A (stages 0-3) slot(s, g) = 16 - 2 hd + g holds W[(L + 64 g) << s]; phase B (stages 4-7)
 // slot 15 + (16 - 2 hd + g) holds W[(r + 4 g) << s] (r = L & 3).  Exact copies of W entries.
 constexpr int TW_SLOTS = 30;
 FHE_DEV int tw_slot(int hd, int g) { return 16 - 2 * hd + g; }
 
-FHE_DEV void dif_phase_a(cplx (&x)[16], const cplx* __restrict__ Wl) {
+// DIF / DIT stage S of phase A (S = 0..3; Wl = table + L) or B (S = 4..7; Wl = table + L + 15*64),
+// half-distance hd = 8 >> (S & 3).  Twiddles are loaded where they are used: holding a phase's 15
+// twiddles in registers costs 60 VGPRs, which the blind-rotate kernel spends on its BSK ring instead.
+template <int S>
+FHE_DEV void dif_stage(cplx (&x)[16], gcptr Wl) {
+    constexpr int hd = 8 >> (S & 3);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int hd = 8 >> s;
+    for (int g = 0; g < hd; ++g) {
+        const cplx tw = Wl[tw_slot(hd, g) * 64];
 #pragma unroll
-        for (int g = 0; g < hd; ++g) {  // distinct twiddles of this stage
-            const cplx w = Wl[tw_slot(hd, g) * 64];
+        for (int t = g; t < 16; t += 2 * hd) {
+            cplx a = x[t], c = x[t + hd];
+            x[t] = cadd(a, c);
+            x[t + hd] = cmul(csub(a, c), tw);
+        }
+    }
+}
+template <int S>
+FHE_DEV void dit_stage(cplx (&x)[16], gcptr Wl) {
+    constexpr int hd = 8 >> (S & 3);
 #pragma unroll
-            for (int t = g; t < 16; t += 2 * hd) {
-                cplx a = x[t], c = x[t + hd];
-                x[t] = cadd(a, c);
-                x[t + hd] = cmul(csub(a, c), w);
-            }
+    for (int g = 0; g < hd; ++g) {
+        const cplx tw = conj_(Wl[tw_slot(hd, g) * 64]);
+#pragma unroll
+        for (int t = g; t < 16; t += 2 * hd) {
+            cplx a = x[t], c = cmul(x[t + hd], tw);
+            x[t] = cadd(a, c);
+            x[t + hd] = csub(a, c);
         }
     }
 }
 
-FHE_DEV void dif_phase_b(cplx (&x)[16], const cplx* __restrict__ Wl) {
-#pragma unroll
-    for (int s = 4; s < 8; ++s) {
-        const int hd = 8 >> (s - 4);
-#pragma unroll
-        for (int g = 0; g < hd; ++g) {
-            const cplx w = Wl[(15 + tw_slot(hd, g)) * 64];
-#pragma unroll
-            for (int u = g; u < 16; u += 2 * hd) {
-                cplx a = x[u], c = x[u + hd];
-                x[u] = cadd(a, c);
-                x[u + hd] = cmul(csub(a, c), w);
-            }
-        }
-    }
+FHE_DEV void dif_phase_a(cplx (&x)[16], gcptr Wl) {
+    dif_stage<0>(x, Wl);
+    dif_stage<1>(x, Wl);
+    dif_stage<2>(x, Wl);
+    dif_stage<3>(x, Wl);
+}
+
+FHE_DEV void dif_phase_b(cplx (&x)[16], gcptr Wl) {
+    const gcptr Wb = Wl + 15 * 64;
+    dif_stage<4>(x, Wb);
+    dif_stage<5>(x, Wb);
+    dif_stage<6>(x, Wb);
+    dif_stage<7>(x, Wb);
 }
 
 FHE_DEV void dif_phase_c(cplx (&x)[16]) {
@@ -150,38 +176,19 @@ FHE_DEV void dit_phase_c(cplx (&x)[16]) {
     }
 }
 
-FHE_DEV void dit_phase_b(cplx (&x)[16], const cplx* __restrict__ Wl) {
-#pragma unroll
-    for (int s = 7; s >= 4; --s) {
-        const int hd = 8 >> (s - 4);
-#pragma unroll
-        for (int g = 0; g < hd; ++g) {
-            const cplx w = conj_(Wl[(15 + tw_slot(hd, g)) * 64]);
-#pragma unroll
-            for (int u = g; u < 16; u += 2 * hd) {
-                cplx a = x[u], c = cmul(x[u + hd], w);
-                x[u] = cadd(a, c);
-                x[u + hd] = csub(a, c);
-            }
-        }
-    }
+FHE_DEV void dit_phase_b(cplx (&x)[16], gcptr Wl) {
+    const gcptr Wb = Wl + 15 * 64;
+    dit_stage<7>(x, Wb);
+    dit_stage<6>(x, Wb);
+    dit_stage<5>(x, Wb);
+    dit_stage<4>(x, Wb);
 }
 
-FHE_DEV void dit_phase_a(cplx (&x)[16], const cplx* __restrict__ Wl) {
-#pragma unroll
-    for (int s = 3; s >= 0; --s) {
-        const int hd = 8 >> s;
-#pragma unroll
-        for (int g = 0; g < hd; ++g) {
-            const cplx w = conj_(Wl[tw_slot(hd, g) * 64]);
-#pragma unroll
-            for (int t = g; t < 16; t += 2 * hd) {
-                cplx a = x[t], c = cmul(x[t + hd], w);
-                x[t] = cadd(a, c);
-                x[t + hd] = csub(a, c);
-            }
-        }
-    }
+FHE_DEV void dit_phase_a(cplx (&x)[16], gcptr Wl) {
+    dit_stage<3>(x, Wl);
+    dit_stage<2>(x, Wl);
+    dit_stage<1>(x, Wl);
+    dit_stage<0>(x, Wl);
 }
 
 // ---------------------------------------------------------------- exchanges (per-wave LDS)
@@ -236,7 +243,7 @@ FHE_DEV void xchg_c_to_b(cplx (&x)[16], cplx* sc, int L) {
 }
 
 // Wl = per-lane twiddle table + L (see tw_slot)
-FHE_DEV void fft_forward(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ Wl) {
+FHE_DEV void fft_forward(cplx (&x)[16], cplx* sc, int L, gcptr Wl) {
     dif_phase_a(x, Wl);
     xchg_a_to_b(x, sc, L);
     dif_phase_b(x, Wl);
@@ -244,7 +251,7 @@ FHE_DEV void fft_forward(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict_
     dif_phase_c(x);
 }
 // phase C layout (bit-reversed) -> natural order in phase A layout, unscaled
-FHE_DEV void fft_inverse(cplx (&x)[16], cplx* sc, int L, const cplx* __restrict__ Wl) {
+FHE_DEV void fft_inverse(cplx (&x)[16], cplx* sc, int L, gcptr Wl) {
     dit_phase_c(x);
     xchg_c_to_b(x, sc, L);
     dit_phase_b(x, Wl);

@@ -109,39 +109,56 @@ __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ 
 // in registers with two swizzled LDS exchanges, and the two waves swap their Fourier-domain
 // digit polynomials through LDS once per CMUX.
 constexpr int BR_PBS_BL = 23;
+constexpr int kRing = 2;
+constexpr int kBrGroup = 1;  // ciphertexts per workgroup; measured per 8192: G=1 101 ms, G=2 157, G=4 108
 
 // out[R] = D0[R] * B0[R] + D1[R] * B1[R] (fused chain identical to the oracle), in place in x.
+// The BSK rows stream through a register ring of depth kRing (Bq0/Bq1 hold R < kRing on entry): each
+// step consumes slot R % kRing and refills it with R + kRing.  kRing = 2 is what fits beside the
+// accumulator and FFT state in 256 VGPRs (deeper rings spill: measured 146 ms vs 102 ms per 8192).
 template <bool OWN_IS_MASK>
-FHE_DEV void pointwise_mac(cplx (&x)[16], const cplx* __restrict__ other,
-                           const cplx* __restrict__ b0, const cplx* __restrict__ b1) {
+FHE_DEV void pointwise_mac(cplx (&x)[16], const cplx* __restrict__ other, cplx (&Bq0)[kRing], cplx (&Bq1)[kRing],
+                           gcptr b0, gcptr b1) {
 #pragma unroll
     for (int R = 0; R < 16; ++R) {
+        const cplx B0 = Bq0[R % kRing], B1 = Bq1[R % kRing];
+        if (R + kRing < 16) {
+            Bq0[R % kRing] = b0[(R + kRing) * 64];
+            Bq1[R % kRing] = b1[(R + kRing) * 64];
+        }
         const cplx mine = x[R];
         const cplx oth = other[R * 64];
         const cplx d0 = OWN_IS_MASK ? mine : oth;
         const cplx d1 = OWN_IS_MASK ? oth : mine;
-        const cplx B0 = b0[R * 64], B1 = b1[R * 64];
         cplx o;
         o.x = __fma_rn(d0.x, B0.x, __fma_rn(-d0.y, B0.y, __fma_rn(d1.x, B1.x, -(d1.y * B1.y))));
         o.y = __fma_rn(d0.x, B0.y, __fma_rn(d0.y, B0.x, __fma_rn(d1.x, B1.y, d1.y * B1.x)));
         x[R] = o;
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <bool DESC>
-__global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint64_t* __restrict__ ms, int ms_stride,
-                                                     const uint32_t* __restrict__ lut_idx,
-                                                     const PbsDesc* __restrict__ desc,
-                                                     const uint64_t* __restrict__ luts,
-                                                     const cplx* __restrict__ bsk,
-                                                     const cplx* __restrict__ W,
-                                                     const cplx* __restrict__ psi,
-                                                     uint64_t* __restrict__ out, int n) {
-    __shared__ __attribute__((aligned(16))) cplx lds[2][FFT_SCRATCH];
-    const int ct = blockIdx.x;
-    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
-    cplx* sc = lds[w];
-    cplx* sc_other = lds[w ^ 1];
+// G ciphertexts per workgroup run in lockstep (their per-iteration barriers are shared), so the
+// G reads of each BSK slice land together and are served once from L1/L2 instead of G times.
+// Direct (lut_idx/out) or descriptor-driven (desc) launches share one instantiation: desc is a
+// uniform runtime choice read only before and after the CMUX loop.  (Two template copies of the
+// loop were scheduled differently enough that the descriptor copy ran 35% slower.)
+template <int G>
+__global__ __launch_bounds__(128 * G, 2) void k_blind_rotate(const uint64_t* __restrict__ ms, int ms_stride,
+                                                         const uint32_t* __restrict__ lut_idx,
+                                                         const PbsDesc* __restrict__ desc,
+                                                         const uint64_t* __restrict__ luts,
+                                                         const cplx* __restrict__ bsk,
+                                                         const cplx* __restrict__ W,
+                                                         const cplx* __restrict__ psi,
+                                                         uint64_t* __restrict__ out, int n, int count) {
+    __shared__ __attribute__((aligned(16))) cplx lds[2 * G][FFT_SCRATCH];
+    const int g = threadIdx.x >> 7;
+    const bool live = G == 1 || (int)blockIdx.x * G + g < count;
+    const int ct = live ? (int)blockIdx.x * G + g : count - 1;  // tail slots recompute the last one
+    const int w = (threadIdx.x >> 6) & 1, L = threadIdx.x & 63;
+    cplx* sc = lds[2 * g + w];
+    cplx* sc_other = lds[2 * g + (w ^ 1)];
     uint64_t* scu = reinterpret_cast<uint64_t*>(sc);
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
 
@@ -149,7 +166,7 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint64_t* __restr
     {
         const uint32_t bt = modswitch_2n(a_ct[n]);
         const int rot = (int)((4096u - bt) & 4095u);  // X^{-b}
-        const uint64_t* lut = luts + (size_t)(DESC ? desc[ct].lut : lut_idx[ct]) * 2048;
+        const uint64_t* lut = luts + (size_t)(desc ? desc[ct].lut : lut_idx[ct]) * 2048;
 #pragma unroll
         for (int t = 0; t < 32; ++t) {
             uint64_t v = 0;
@@ -166,12 +183,23 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint64_t* __restr
     for (int i = 0; i < n; ++i) {
         const uint32_t a = a_next;
         a_next = modswitch_2n(a_ct[i + 1]);
-        if (a == 0) continue;  // X^0 - 1 = 0: the external product is exactly zero
-        // Keep the twiddle / twist tables out of the register file: re-derive their base pointers
-        // every iteration so their (L1-resident) loads are not hoisted out of the loop.
-        const cplx* Wi = W;
-        const cplx* psii = psi;
-        asm volatile("" : "+s"(Wi), "+s"(psii));
+        // X^0 - 1 = 0: the external product is exactly zero (skipping it is bit-identical); only a
+        // lone ciphertext may skip, a lockstep group shares its barriers
+        if (G == 1 && a == 0) continue;
+        // Tables are re-derived every iteration (kept out of the register file across iterations)
+        // and every batch of loads is issued well ahead of its use; sched_barriers pin the order.
+        const cplx* Wg = W;
+        const cplx* Pg = psi;
+        asm volatile("" : "+s"(Wg), "+s"(Pg));
+        const gcptr Wl = as_global(Wg) + L, Pl = as_global(Pg) + L;
+        const gcptr b0 = as_global(bsk) + ((size_t)((i * 2 + 0) * 2 + w) * 16) * 64 + L;
+        const gcptr b1 = as_global(bsk) + ((size_t)((i * 2 + 1) * 2 + w) * 16) * 64 + L;
+
+        // ---- twist factors in flight while the accumulator goes through LDS
+        cplx ps[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) ps[t] = Pl[64 * t];
+        __builtin_amdgcn_sched_barrier(0);
 
         // ---- rotate, subtract, decompose, twist
 #pragma unroll
@@ -190,35 +218,56 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint64_t* __restr
                 const uint64_t v = (scu[u & 2047u] ^ neg) - neg;
                 d2[hh] = decomp1<BR_PBS_BL>(v - acc[tt]);
             }
-            x[t] = cmul(make_double2((double)d2[0], (double)d2[1]), psii[L + 64 * t]);
+            x[t] = cmul(make_double2((double)d2[0], (double)d2[1]), ps[t]);
             if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         wave_sync();
 
         // ---- forward FFT of this wave's digit polynomial
-        fft_forward(x, sc, L, Wi + L);
+        dif_phase_a(x, Wl);
+        xchg_a_to_b(x, sc, L);
+        dif_phase_b(x, Wl);
+        // head of the BSK ring, in flight across the B->C exchange, phase C and the barrier
+        cplx Bq0[kRing], Bq1[kRing];
+#pragma unroll
+        for (int R = 0; R < kRing; ++R) {
+            Bq0[R] = b0[R * 64];
+            Bq1[R] = b1[R * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        xchg_b_to_c(x, sc, L);
+        dif_phase_c(x);
 
         // ---- swap Fourier digits with the partner wave, pointwise MAC with the BSK
 #pragma unroll
         for (int R = 0; R < 16; ++R) sc[R * 64 + L] = x[R];
         __syncthreads();
-        {
-            // row 0 multiplies the mask digits D0, row 1 the body digits D1 (oracle order); the
-            // branch is wave-uniform so both waves evaluate the identical expression tree.
-            const cplx* b0 = bsk + ((size_t)((i * 2 + 0) * 2 + w) * 16) * 64 + L;
-            const cplx* b1 = bsk + ((size_t)((i * 2 + 1) * 2 + w) * 16) * 64 + L;
-            if (__builtin_amdgcn_readfirstlane(w) == 0)
-                pointwise_mac<true>(x, sc_other + L, b0, b1);
-            else
-                pointwise_mac<false>(x, sc_other + L, b0, b1);
-        }
+        // row 0 multiplies the mask digits D0, row 1 the body digits D1 (oracle order); the branch
+        // is wave-uniform so both waves evaluate the identical expression tree.
+        if (__builtin_amdgcn_readfirstlane(w) == 0)
+            pointwise_mac<true>(x, sc_other + L, Bq0, Bq1, b0, b1);
+        else
+            pointwise_mac<false>(x, sc_other + L, Bq0, Bq1, b0, b1);
         __syncthreads();
 
-        // ---- inverse FFT, untwist, round, accumulate
-        fft_inverse(x, sc, L, Wi + L);
+        // ---- inverse FFT (untwist factors issued before its last stage)
+        dit_phase_c(x);
+        xchg_c_to_b(x, sc, L);
+        dit_phase_b(x, Wl);
+        xchg_b_to_a(x, sc, L);
+        dit_stage<3>(x, Wl);
+        dit_stage<2>(x, Wl);
+        dit_stage<1>(x, Wl);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) ps[t] = Pl[64 * t];
+        __builtin_amdgcn_sched_barrier(0);
+        dit_stage<0>(x, Wl);
+
+        // ---- untwist, round, accumulate
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-            const cplx p = psii[L + 64 * t];
+            const cplx p = ps[t];
             const cplx u = make_double2(p.x * 0.0009765625, -p.y * 0.0009765625);
             const cplx y = cmul(x[t], u);
             acc[t] += f64_to_torus(y.x);
@@ -228,7 +277,8 @@ __global__ __launch_bounds__(128, 2) void k_blind_rotate(const uint64_t* __restr
     }
 
     // ---- sample extract (coefficient 0)
-    uint64_t* o = DESC ? desc[ct].dst : out + (size_t)ct * 2049;
+    if (!live) return;
+    uint64_t* o = desc ? desc[ct].dst : out + (size_t)ct * 2049;
     if (w == 0) {
 #pragma unroll
         for (int t = 0; t < 32; ++t) {
@@ -259,7 +309,7 @@ __global__ __launch_bounds__(64) void k_bsk_to_fourier(const uint64_t* __restric
         const double im = (double)(int64_t)p[L + 64 * t + 1024];
         x[t] = cmul(make_double2(re, im), psi[L + 64 * t]);
     }
-    fft_forward(x, sc, L, W + L);
+    fft_forward(x, sc, L, as_global(W) + L);
     cplx* o = out + (size_t)q * 1024 + L;
 #pragma unroll
     for (int R = 0; R < 16; ++R) o[R * 64] = x[R];
@@ -303,8 +353,9 @@ hipError_t launch_blind_rotate(const uint64_t* ms, int ms_stride, const uint32_t
                                const uint64_t* luts, const cplx* bsk, const cplx* W,
                                const cplx* psi, uint64_t* out, int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blind_rotate<false>, dim3(count), dim3(128), 0, s, ms, ms_stride, lut_idx, nullptr,
-                       luts, bsk, W, psi, out, n);
+    hipLaunchKernelGGL((k_blind_rotate<kBrGroup>), dim3((count + kBrGroup - 1) / kBrGroup),
+                       dim3(128 * kBrGroup), 0, s, ms, ms_stride, lut_idx, nullptr, luts, bsk, W, psi, out, n,
+                       count);
     return hipGetLastError();
 }
 
@@ -312,8 +363,9 @@ hipError_t launch_blind_rotate_desc(const uint64_t* ms, int ms_stride, const Pbs
                                     const uint64_t* luts, const cplx* bsk, const cplx* W,
                                     const cplx* psi, int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blind_rotate<true>, dim3(count), dim3(128), 0, s, ms, ms_stride, nullptr, desc,
-                       luts, bsk, W, psi, nullptr, n);
+    hipLaunchKernelGGL((k_blind_rotate<kBrGroup>), dim3((count + kBrGroup - 1) / kBrGroup),
+                       dim3(128 * kBrGroup), 0, s, ms, ms_stride, nullptr, desc, luts, bsk, W, psi, nullptr, n,
+                       count);
     return hipGetLastError();
 }
 

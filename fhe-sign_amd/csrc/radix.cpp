@@ -333,6 +333,16 @@ Radix radix_trivial(uint64_t lo, uint64_t hi, uint32_t nblocks) {
     return r;
 }
 
+Radix radix_trivial(const BigConst& v, uint32_t nblocks) {
+    Radix r;
+    r.blocks.resize(nblocks);
+    for (uint32_t k = 0; k < nblocks; ++k) {
+        const uint32_t bit = 2 * k, w = bit / 64;
+        r.blocks[k] = Block::make_trivial(w < v.size() ? (uint32_t)(v[w] >> (bit % 64)) & 3u : 0u);
+    }
+    return r;
+}
+
 Radix radix_resize(const Radix& a, uint32_t nblocks) {
     Radix r;
     r.blocks.resize(nblocks);
@@ -584,14 +594,14 @@ Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {
 }
 
 // ============================================================================ scalar ops
-Radix radix_scalar_and(Engine& e, const Radix& a, uint64_t mlo, uint64_t mhi) {
+Radix radix_scalar_and(Engine& e, const Radix& a, const BigConst& mask) {
     std::vector<PbsItem> items;
     std::vector<uint32_t> where;
     Radix r;
     r.blocks.resize(a.nblocks());
+    const Radix mb = radix_trivial(mask, a.nblocks());
     for (uint32_t k = 0; k < a.nblocks(); ++k) {
-        const uint32_t bit = 2 * k;
-        const uint32_t m = bit < 64 ? (uint32_t)(mlo >> bit) & 3 : (bit < 128 ? (uint32_t)(mhi >> (bit - 64)) & 3 : 0);
+        const uint32_t m = mb.blocks[k].value;
         const Block& x = a.blocks[k];
         if (m == 0)
             r.blocks[k] = Block::make_trivial(0);
@@ -640,51 +650,120 @@ Radix radix_scalar_shl(Engine& e, const Radix& a, uint32_t bits) {
     return r;
 }
 
-Radix radix_scalar_add(Engine& e, const Radix& a, uint64_t s) {
-    Radix t = radix_trivial(s, 0, a.nblocks());
+Radix radix_scalar_add(Engine& e, const Radix& a, const BigConst& s) {
+    Radix t = radix_trivial(s, a.nblocks());
     return radix_sum(e, {&a, &t}, a.nblocks());
 }
 
-Radix radix_scalar_mul(Engine& e, const Radix& a, uint64_t s) {
-    Radix t = radix_trivial(s, 0, a.nblocks());
+Radix radix_scalar_mul(Engine& e, const Radix& a, const BigConst& s) {
+    Radix t = radix_trivial(s, a.nblocks());
     return radix_mul(e, a, t, a.nblocks());
 }
 
-// Granlund-Montgomery (PLDI 1994, Fig. 6.2) multiplier for N-bit unsigned division by d.
-static void choose_multiplier(uint64_t d, uint32_t N, unsigned __int128* m, uint32_t* sh) {
-    uint32_t l = 0;
-    while (l < 64 && ((unsigned __int128)1 << l) < d) ++l;  // ceil(log2 d)
+// ---- clear multi-word arithmetic for the division constants (host only, a few hundred bits)
+namespace {
+BigConst big_norm(BigConst v) {
+    while (!v.empty() && v.back() == 0) v.pop_back();
+    return v;
+}
+uint32_t big_bitlen(const BigConst& v) {
+    for (size_t w = v.size(); w-- > 0;)
+        if (v[w]) return (uint32_t)(64 * w + 64 - __builtin_clzll(v[w]));
+    return 0;
+}
+bool big_bit(const BigConst& v, uint32_t i) { return i / 64 < v.size() && ((v[i / 64] >> (i % 64)) & 1); }
+int big_cmp(const BigConst& a, const BigConst& b) {
+    const size_t n = std::max(a.size(), b.size());
+    for (size_t w = n; w-- > 0;) {
+        const uint64_t x = w < a.size() ? a[w] : 0, y = w < b.size() ? b[w] : 0;
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return 0;
+}
+BigConst big_pow2(uint32_t e) {
+    BigConst v(e / 64 + 1, 0);
+    v[e / 64] = 1ull << (e % 64);
+    return v;
+}
+BigConst big_add(const BigConst& a, const BigConst& b) {
+    BigConst r(std::max(a.size(), b.size()) + 1, 0);
+    unsigned __int128 c = 0;
+    for (size_t w = 0; w < r.size(); ++w) {
+        c += (unsigned __int128)(w < a.size() ? a[w] : 0) + (w < b.size() ? b[w] : 0);
+        r[w] = (uint64_t)c;
+        c >>= 64;
+    }
+    return big_norm(r);
+}
+void big_sub_inplace(BigConst& a, const BigConst& b) {  // a >= b
+    uint64_t borrow = 0;
+    for (size_t w = 0; w < a.size(); ++w) {
+        const uint64_t y = w < b.size() ? b[w] : 0;
+        const uint64_t d = a[w] - y - borrow;
+        borrow = (a[w] < y || (a[w] == y && borrow)) ? 1 : 0;
+        a[w] = d;
+    }
+}
+BigConst big_shr1(BigConst v) {
+    for (size_t w = 0; w < v.size(); ++w) v[w] = (v[w] >> 1) | (w + 1 < v.size() ? v[w + 1] << 63 : 0);
+    return big_norm(v);
+}
+// floor(num / den), binary long division
+BigConst big_div(const BigConst& num, const BigConst& den) {
+    const uint32_t nb = big_bitlen(num);
+    BigConst q((nb + 63) / 64 + 1, 0), r;
+    for (uint32_t i = nb; i-- > 0;) {
+        uint64_t carry = big_bit(num, i) ? 1 : 0;  // r = 2 r + bit i of num
+        for (size_t w = 0; w < r.size(); ++w) {
+            const uint64_t nc = r[w] >> 63;
+            r[w] = (r[w] << 1) | carry;
+            carry = nc;
+        }
+        if (carry) r.push_back(carry);
+        if (big_cmp(r, den) >= 0) {
+            big_sub_inplace(r, den);
+            r = big_norm(r);
+            q[i / 64] |= 1ull << (i % 64);
+        }
+    }
+    return big_norm(q);
+}
+}  // namespace
+
+// Granlund-Montgomery (PLDI 1994, Fig. 6.2) multiplier for N-bit unsigned division by d
+// (d not a power of two): m = floor((2^(N+l) + 2^l) / d) reduced while m_low/2 < m_high/2.
+static void choose_multiplier(const BigConst& d, uint32_t N, BigConst* m, uint32_t* sh) {
+    BigConst dm1 = d;
+    big_sub_inplace(dm1, BigConst{1});
+    const uint32_t l = big_bitlen(big_norm(dm1));  // ceil(log2 d)
     uint32_t shpost = l;
-    // m_low = floor(2^(N+l) / d), m_high = floor((2^(N+l) + 2^l) / d)  (prec = N)
-    unsigned __int128 two = (unsigned __int128)1 << (N + l);
-    unsigned __int128 mlow = two / d;
-    unsigned __int128 mhigh = (two + ((unsigned __int128)1 << l)) / d;
-    while ((mlow >> 1) < (mhigh >> 1) && shpost > 0) {
-        mlow >>= 1;
-        mhigh >>= 1;
+    const BigConst two = big_pow2(N + l);
+    BigConst mlow = big_div(two, d);
+    BigConst mhigh = big_div(big_add(two, big_pow2(l)), d);
+    while (big_cmp(big_shr1(mlow), big_shr1(mhigh)) < 0 && shpost > 0) {
+        mlow = big_shr1(mlow);
+        mhigh = big_shr1(mhigh);
         --shpost;
     }
     *m = mhigh;
     *sh = shpost;
 }
 
-Radix radix_scalar_div(Engine& e, const Radix& a, uint64_t d) {
+Radix radix_scalar_div(Engine& e, const Radix& a, const BigConst& dd) {
     const uint32_t n = a.nblocks(), N = 2 * n;
-    engine_check(d != 0, "division by zero");
-    engine_check(N <= 64, "scalar_div supports up to 64-bit integers");
-    if (d == 1) return a;
-    if ((d & (d - 1)) == 0) return radix_scalar_shr(e, a, (uint32_t)__builtin_ctzll(d));
-    if (N < 64 && d >= (1ull << N)) return radix_trivial(0, 0, n);
-    uint32_t l = 0;
-    while (l < 64 && ((unsigned __int128)1 << l) < d) ++l;
-    engine_check(N + l <= 126, "scalar_div: divisor too large for this width");
-    unsigned __int128 m;
+    const BigConst d = big_norm(dd);
+    engine_check(!d.empty(), "division by zero");
+    const uint32_t dl = big_bitlen(d);
+    if (dl == 1) return a;                                                   // d = 1
+    if (big_cmp(d, big_pow2(dl - 1)) == 0) return radix_scalar_shr(e, a, dl - 1);  // 2^k
+    if (dl > N) return radix_trivial(0, 0, n);                               // d >= 2^N > a
+    BigConst m;
     uint32_t sh;
     choose_multiplier(d, N, &m, &sh);
-    // q = floor(a * m / 2^(N + sh)); a < 2^N, m <= 2^(N+1)  =>  a*m < 2^(2N+1): 2n+1 blocks
+    // q = floor(a * m / 2^(N + sh)); a < 2^N, m < 2^(N+1)  =>  a*m < 2^(2N+1): 2n+1 blocks
     const uint32_t nb = 2 * n + 1;
     Radix aw = radix_resize(a, nb);
-    Radix mw = radix_trivial((uint64_t)m, (uint64_t)(m >> 64), nb);
+    Radix mw = radix_trivial(m, nb);
     Radix prod = radix_mul(e, aw, mw, nb);
     Radix q = radix_scalar_shr(e, prod, N + sh);
     return radix_resize(q, n);
@@ -872,7 +951,7 @@ Radix radix_clean(Engine& e, const Radix& a) {
     return r;
 }
 
-Radix radix_scalar_rem(Engine& e, const Radix& a, uint64_t d) {
+Radix radix_scalar_rem(Engine& e, const Radix& a, const BigConst& d) {
     Radix q = radix_scalar_div(e, a, d);
     Radix qd = radix_scalar_mul(e, q, d);
     return radix_sub(e, a, qd);

@@ -115,7 +115,12 @@ struct Radix {
     uint32_t nblocks() const { return (uint32_t)blocks.size(); }
 };
 
+// Clear operand of any width: little-endian 64-bit words (tfhe's scalar ops take u64/u128/U256
+// scalars; the wide forms back 256-bit division by a 128-bit clear divisor, BASELINE config 3).
+using BigConst = std::vector<uint64_t>;
+
 Radix radix_trivial(uint64_t value_lo, uint64_t value_hi, uint32_t nblocks);
+Radix radix_trivial(const BigConst& value, uint32_t nblocks);
 Radix radix_resize(const Radix& a, uint32_t nblocks);  // cast: truncate / zero-extend
 
 // Sum of several radix integers (wrapping at `nblocks`; carries propagated).  Used for every add.
@@ -127,13 +132,19 @@ Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks);
 // Batched independent products (one level schedule for all).
 std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                   uint32_t nblocks);
-Radix radix_scalar_and(Engine& e, const Radix& a, uint64_t mask_lo, uint64_t mask_hi);
+Radix radix_scalar_and(Engine& e, const Radix& a, const BigConst& mask);
 Radix radix_scalar_shr(Engine& e, const Radix& a, uint32_t bits);
 Radix radix_scalar_shl(Engine& e, const Radix& a, uint32_t bits);
-Radix radix_scalar_add(Engine& e, const Radix& a, uint64_t s);
-Radix radix_scalar_mul(Engine& e, const Radix& a, uint64_t s);
-Radix radix_scalar_div(Engine& e, const Radix& a, uint64_t d);
-Radix radix_scalar_rem(Engine& e, const Radix& a, uint64_t d);
+Radix radix_scalar_add(Engine& e, const Radix& a, const BigConst& s);
+Radix radix_scalar_mul(Engine& e, const Radix& a, const BigConst& s);
+// floor(a / d) and a mod d for a clear divisor d != 0 of any width (Granlund-Montgomery multiply)
+Radix radix_scalar_div(Engine& e, const Radix& a, const BigConst& d);
+Radix radix_scalar_rem(Engine& e, const Radix& a, const BigConst& d);
+inline Radix radix_scalar_and(Engine& e, const Radix& a, uint64_t mask) { return radix_scalar_and(e, a, BigConst{mask}); }
+inline Radix radix_scalar_add(Engine& e, const Radix& a, uint64_t s) { return radix_scalar_add(e, a, BigConst{s}); }
+inline Radix radix_scalar_mul(Engine& e, const Radix& a, uint64_t s) { return radix_scalar_mul(e, a, BigConst{s}); }
+inline Radix radix_scalar_div(Engine& e, const Radix& a, uint64_t d) { return radix_scalar_div(e, a, BigConst{d}); }
+inline Radix radix_scalar_rem(Engine& e, const Radix& a, uint64_t d) { return radix_scalar_rem(e, a, BigConst{d}); }
 Radix radix_sub(Engine& e, const Radix& a, const Radix& b);
 // encrypted boolean (one block, value 0/1)
 Block radix_lt(Engine& e, const Radix& a, const Radix& b);

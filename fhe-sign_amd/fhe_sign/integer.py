@@ -57,7 +57,7 @@ class FheUint:
 
     @classmethod
     def _wrap(cls, h, bits):
-        kind = {8: FheUint8, 32: FheUint32, 64: FheUint64, 2: FheBool}.get(bits, FheUint)
+        kind = {8: FheUint8, 32: FheUint32, 64: FheUint64, 128: FheUint128, 256: FheUint256, 2: FheBool}.get(bits, FheUint)
         obj = kind.__new__(kind)
         FheUint.__init__(obj, h, bits)
         return obj
@@ -109,18 +109,32 @@ class FheUint:
         check(getattr(load(), fn)(_ctx().handle, self._h, s, C.byref(h)))
         return self._wrap(h, self.bits)
 
+    def _scalar_any(self, fn, s: int, wrap: bool = True):
+        """u64 entry point when the clear operand fits, the _words one otherwise (wide FheUint)."""
+        s = int(s)
+        if wrap:
+            s %= 1 << self.bits
+        if s < 0:
+            raise ValueError("clear operand must be non-negative")
+        if s < 2**64:
+            return self._scalar(fn, s)
+        w = _words(s, max(64, s.bit_length()))
+        h = C.c_void_p()
+        check(getattr(load(), fn + "_words")(_ctx().handle, self._h, ptr(w), w.size, C.byref(h)))
+        return self._wrap(h, self.bits)
+
     # ---- operators (tfhe HL API)
     def __add__(self, o):
-        return self._bin("fhe_radix_add", o) if isinstance(o, FheUint) else self._scalar("fhe_radix_scalar_add", int(o) % 2**64)
+        return self._bin("fhe_radix_add", o) if isinstance(o, FheUint) else self._scalar_any("fhe_radix_scalar_add", o)
 
     def __sub__(self, o):
         return self._bin("fhe_radix_sub", o)
 
     def __mul__(self, o):
-        return self._bin("fhe_radix_mul", o) if isinstance(o, FheUint) else self._scalar("fhe_radix_scalar_mul", int(o) % 2**64)
+        return self._bin("fhe_radix_mul", o) if isinstance(o, FheUint) else self._scalar_any("fhe_radix_scalar_mul", o)
 
     def __and__(self, o):
-        return self._bin("fhe_radix_bitand", o) if isinstance(o, FheUint) else self._scalar("fhe_radix_scalar_and", int(o) % 2**64)
+        return self._bin("fhe_radix_bitand", o) if isinstance(o, FheUint) else self._scalar_any("fhe_radix_scalar_and", o)
 
     def __rshift__(self, o):
         if isinstance(o, FheUint):
@@ -133,12 +147,12 @@ class FheUint:
         return self._scalar("fhe_radix_scalar_shl", int(o) % 2**32)
 
     def __floordiv__(self, d: int):
-        return self._scalar("fhe_radix_scalar_div", int(d))
+        return self._scalar_any("fhe_radix_scalar_div", d, wrap=False)
 
     __truediv__ = __floordiv__  # tfhe's `&a / 5` on FheUint is integer division (src/perf_test.rs:54)
 
     def __mod__(self, d: int):
-        return self._scalar("fhe_radix_scalar_rem", int(d))
+        return self._scalar_any("fhe_radix_scalar_rem", d, wrap=False)
 
     def min(self, o):
         return self._bin("fhe_radix_min", o)
@@ -176,6 +190,14 @@ class FheUint32(FheUint):
 
 class FheUint64(FheUint):
     BITS = 64
+
+
+class FheUint128(FheUint):
+    BITS = 128
+
+
+class FheUint256(FheUint):
+    BITS = 256
 
 
 def to_u32_digits(value: int) -> list[int]:

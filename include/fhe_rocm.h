@@ -107,14 +107,15 @@ int fhe_memcpy_d2h(fhe_ctx* ctx, void* dst, const void* src, size_t bytes);
 int fhe_ctx_last_pbs_timing(fhe_ctx* ctx, float* ks_ms, float* br_ms);
 int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
- * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 768. */
+ * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 640. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
 
 /* ------------------------------------------------------------------- radix integers */
-/* FheUint<num_bits> (num_bits even, <= 128): num_bits/2 radix blocks, device-resident.
+/* FheUint<num_bits> (num_bits even, <= FHE_RADIX_MAX_BITS): num_bits/2 radix blocks, device-resident.
  * Replaces tfhe's FheUint8/32/64 as used at src/biguint.rs:26,135-143,221-248 and
  * src/perf_test.rs:19-54.  Arithmetic wraps modulo 2^num_bits (tfhe semantics). */
 typedef struct fhe_radix fhe_radix;
+#define FHE_RADIX_MAX_BITS 4096
 /* FheUint::try_encrypt (src/biguint.rs:26, src/perf_test.rs:19-21); words little-endian */
 int fhe_radix_encrypt(fhe_ctx* ctx, fhe_client_key* ck, const uint64_t* words, uint32_t num_bits,
                       fhe_radix** out);
@@ -144,6 +145,14 @@ int fhe_radix_scalar_mul(fhe_ctx* ctx, const fhe_radix* a, uint64_t s, fhe_radix
 /* FheUint / clear (src/perf_test.rs:54); divisor 0 -> FHE_ERR_INVALID */
 int fhe_radix_scalar_div(fhe_ctx* ctx, const fhe_radix* a, uint64_t d, fhe_radix** out);
 int fhe_radix_scalar_rem(fhe_ctx* ctx, const fhe_radix* a, uint64_t d, fhe_radix** out);
+/* The same scalar ops with a clear operand of any width (little-endian u64 words), as tfhe's
+ * scalar ops on FheUint256 take U256/u128 scalars.  BASELINE config 3: 256-bit radix divided by a
+ * clear u32 / 128-bit divisor (src/perf_test.rs:54 at 256 bits).  Divisor 0 -> FHE_ERR_INVALID. */
+int fhe_radix_scalar_and_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out);
+int fhe_radix_scalar_add_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out);
+int fhe_radix_scalar_mul_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out);
+int fhe_radix_scalar_div_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* d, size_t nwords, fhe_radix** out);
+int fhe_radix_scalar_rem_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* d, size_t nwords, fhe_radix** out);
 /* FheUint::cast_from / cast_into (src/biguint.rs:110,116,221; src/perf_test.rs:40) */
 int fhe_radix_cast(fhe_ctx* ctx, const fhe_radix* a, uint32_t num_bits, fhe_radix** out);
 /* FheUint::min (src/perf_test.rs:44), max, lt (encrypted bool returned as a 2-bit radix) */

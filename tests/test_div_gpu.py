@@ -1,0 +1,69 @@
+"""BASELINE config 3 on the GPU: 256-bit radix divided by a clear divisor (src/perf_test.rs:54 at
+256 bits) plus the wide clear-operand scalar ops it rests on.
+
+Parity bar: decrypted quotient / remainder equal floor division of the plaintexts (tfhe scalar div
+semantics, 1344 / 5 = 268 at src/perf_test.rs:75), on seeded random 256-bit dividends with the
+divisors SURVEY.md 8d names (5, a random u32, a random 128-bit value) and the edge cases (1, powers
+of two, divisor wider than the dividend)."""
+import random
+
+import pytest
+
+from fhe_sign import Context, FheUint32, FheUint128, FheUint256, generate_keys, set_server_key
+
+pytestmark = pytest.mark.gpu
+M256 = (1 << 256) - 1
+
+
+@pytest.fixture(scope="module")
+def keys():
+    ck, sk = generate_keys(seed=0xD1)
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    set_server_key(ctx)
+    yield ck, ctx
+    set_server_key(None)
+    ctx.close()
+
+
+def test_perf_test_div_known_answer(keys):
+    ck, _ = keys
+    assert (FheUint32.try_encrypt(1344, ck) / 5).decrypt(ck) == 268  # src/perf_test.rs:54,75
+
+
+@pytest.mark.parametrize("kind", ["5", "u32", "u128"])
+def test_div256_by_clear(keys, kind):
+    ck, _ = keys
+    rng = random.Random(0xF11E51)
+    a = rng.getrandbits(256) | 1 << 255
+    d = {"5": 5, "u32": rng.getrandbits(32) | 1 << 31, "u128": rng.getrandbits(128) | 1 << 127}[kind]
+    A = FheUint256.try_encrypt(a, ck)
+    assert (A / d).decrypt(ck) == a // d
+    if kind != "5":
+        assert (A % d).decrypt(ck) == a % d
+
+
+def test_div256_edge_divisors(keys):
+    ck, _ = keys
+    rng = random.Random(7)
+    a = rng.getrandbits(256)
+    A = FheUint256.try_encrypt(a, ck)
+    assert (A / 1).decrypt(ck) == a
+    assert (A / (1 << 77)).decrypt(ck) == a >> 77
+    assert (A / (1 << 300)).decrypt(ck) == 0
+    assert (A % (1 << 300)).decrypt(ck) == a
+    small = FheUint256.try_encrypt(12345, ck)
+    assert (small / ((1 << 200) + 3)).decrypt(ck) == 0
+    with pytest.raises(Exception):
+        A / 0
+
+
+def test_wide_scalar_ops(keys):
+    ck, _ = keys
+    rng = random.Random(11)
+    a, s = rng.getrandbits(128), rng.getrandbits(128) | 1 << 100
+    A = FheUint128.try_encrypt(a, ck)
+    m = (1 << 128) - 1
+    assert (A & s).decrypt(ck) == a & s
+    assert (A + s).decrypt(ck) == (a + s) & m
+    assert (A * s).decrypt(ck) == (a * s) & m

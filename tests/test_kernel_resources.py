@@ -1,0 +1,45 @@
+"""Occupancy guard for the blind-rotate kernels (CPU: compiles device code, reads the code-object
+descriptors).  Both kernels are designed for 2 waves per SIMD: a register total
+(arch VGPR + AGPR) above 256 silently halves occupancy -- it happened once through a VGPR->AGPR
+spill (next_free_vgpr 258) and cost 50% of throughput -- and scratch spills in the CMUX loop
+stall it.  Both are checked here so such a change fails a test instead of a benchmark."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+CSRC = os.path.join(ROOT, "fhe-sign_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def descriptors(src, tmp_path):
+    out = tmp_path / (os.path.basename(src) + ".s")
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "--cuda-device-only",
+                    "-S", "-I", os.path.join(ROOT, "include"), "-I", CSRC, src, "-o", str(out)],
+                   check=True, capture_output=True)
+    s = out.read_text()
+    res = {}
+    for m in re.finditer(r"\.amdhsa_kernel (\S+)\n(.*?)\.end_amdhsa_kernel", s, re.S):
+        f = dict(re.findall(r"\.amdhsa_(\w+) (\d+)", m.group(2)))
+        res[m.group(1)] = {k: int(v) for k, v in f.items()}
+    return res
+
+
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src,kernel,lds_per_cu_ok", [
+    ("pbs_kernels.hip", "k_blind_rotate", 4),        # 4 two-wave workgroups per CU
+    ("br_wide.hip", "k_blind_rotate_wide", 1),        # one 8-wave workgroup per CU
+])
+def test_blind_rotate_two_waves_per_simd(tmp_path, src, kernel, lds_per_cu_ok):
+    d = descriptors(os.path.join(CSRC, src), tmp_path)
+    ks = [v for k, v in d.items() if kernel in k and (kernel != "k_blind_rotate" or "wide" not in k)]
+    assert ks, f"{kernel} not found in {src}"
+    for f in ks:
+        total = max(f["next_free_vgpr"], f["accum_offset"])
+        assert total <= 256, f"{kernel}: {f['next_free_vgpr']} registers -> below 2 waves/SIMD"
+        assert f["private_segment_fixed_size"] == 0, f"{kernel}: scratch spill"
+        assert f["group_segment_fixed_size"] * lds_per_cu_ok <= 160 * 1024, f"{kernel}: LDS limits occupancy"

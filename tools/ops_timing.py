@@ -1,7 +1,10 @@
-"""Wall-clock of the reference-level operations (configs 2-4) with engine statistics."""
+"""Wall-clock of the reference-level operations (configs 2-4) with engine statistics.
+usage: python3 tools/ops_timing.py [package_dir]   (package_dir: a build_variants/NAME copy; default
+the in-tree fhe-sign_amd package)"""
 import json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd")); sys.path.insert(0, os.path.join(ROOT, "oracle"))
+PKG = os.path.abspath(sys.argv[1]) if len(sys.argv) > 1 else os.path.join(ROOT, "fhe-sign_amd")
+sys.path.insert(0, PKG); sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import random
 import ref_semantics as R
 from fhe_sign import *
