@@ -27,7 +27,8 @@ sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
 import numpy as np  # noqa: E402
 
 METRIC = "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds @1/2/4/8 GPU"
-FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector, spec (= FP32 vector rate / 2)
+FP64_PEAK_TFLOPS = 78.6        # MI355X dense FP64 peak (matrix = vector on gfx950), spec
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "r1f_pmc_summary.json")  # tools/profile_round.sh
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FLOPS_PER_CMUX = 4 * 51200 + 4 * 6144 + 32768   # 4 FFT-1024 (5 N log N), 4 twist/untwist, MAC
 
@@ -91,11 +92,24 @@ def cpu_baseline(seed, target_s):
                       f"OpenMP {threads} threads, {dt:.1f} s"}
 
 
+def pmc_traffic(batch):
+    """HBM-side bytes per launch of the blind-rotate kernel at this batch, from the committed PMC
+    summary of the same kernel (tools/profile_round.sh; FETCH_SIZE x2 + WRITE_SIZE, gfx950
+    correction of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits included)"""
+    try:
+        d = json.load(open(PMC_SUMMARY))["pmc"][f"B={batch}"]
+        k = next(v for k, v in d.items() if "k_blind_rotate" in k and "wide" not in k)
+        return k["hbm_side_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
+    except (OSError, KeyError, StopIteration, ValueError):
+        return None, None
+
+
 def ops_legs(ck, ctx, seed):
     """configs 2 and 4: BigUintFHE 256-bit mul wall-clock and sign_fhe_with_k0 seconds (every rank
     runs its own replica: the N-GPU line is the 'one sign per GPU' batch of configs[4])."""
     import random
-    from fhe_sign import COMPAT, FAST, BigUintFHE, Schnorr, compute_nonce, set_server_key, stats
+    from fhe_sign import (COMPAT, FAST, PUBLIC, BigUintFHE, FheUint32, FheUint256, Schnorr, compute_nonce, set_server_key,
+                          stats)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     set_server_key(ctx)
     rng = random.Random(seed)
@@ -120,6 +134,16 @@ def ops_legs(ck, ctx, seed):
         lambda r: r.decrypt_limbs(ck) == R.biguint_mul(R.to_u32_digits(a), R.to_u32_digits(b)))
     leg("biguint256_mul_fast", lambda: A.mul(B, FAST), lambda r: r.to_biguint(ck) == a * b)
     leg("biguint256_add_fast", lambda: A.add(B, FAST), lambda r: r.to_biguint(ck) == a + b)
+    # config 3: 256-bit radix / clear divisor (src/perf_test.rs:54 at 256 bits)
+    A256 = FheUint256.try_encrypt(a, ck)
+    du32, du128 = rng.getrandbits(32) | 1 << 31, rng.getrandbits(128) | 1 << 127
+    leg("div256_by_5", lambda: A256 / 5, lambda r: r.decrypt(ck) == a // 5)
+    leg("div256_by_u32", lambda: A256 / du32, lambda r: r.decrypt(ck) == a // du32)
+    leg("div256_by_u128", lambda: A256 / du128, lambda r: r.decrypt(ck) == a // du128)
+    X32 = FheUint32.try_encrypt(1344, ck)  # src/perf_test.rs:14-15,54 (README.md:114: 1121 s on CPU)
+    leg("fheuint32_div5", lambda: X32 / 5, lambda r: r.decrypt(ck) == 268)
+    leg("fheuint32_add", lambda: X32 + FheUint32.try_encrypt(5, ck), lambda r: r.decrypt(ck) == 1349)
+    leg("fheuint32_mul", lambda: X32 * FheUint32.try_encrypt(5, ck), lambda r: r.decrypt(ck) == 6720)
     d, msg = 3, bytes(32)  # BIP-340 vector 0 (tests/golden/bip340_vectors.csv row 0)
     k0 = compute_nonce(d, msg, bytes(32))
     dF = BigUintFHE.new(d, ck)
@@ -127,6 +151,7 @@ def ops_legs(ck, ctx, seed):
     ref = s.sign_with_k0(msg, k0, d)
     leg("sign_fhe_with_k0_v0_compat", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT), lambda r: r == ref)
     leg("sign_fhe_with_k0_v0_fast", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, FAST), lambda r: r == ref)
+    leg("sign_fhe_with_k0_v0_public", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, PUBLIC), lambda r: r == ref)
     return out
 
 
@@ -193,6 +218,7 @@ def main():
     ks_ms = float(np.mean(ks_t))
     flops = B * n * FLOPS_PER_CMUX
     achieved = flops / (br_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(B)
     bsk_bytes = n * 4 * 1024 * 16
     hbm_bytes = bsk_bytes + B * ((n + 1) * 2 + 2049 * 8 + 4)
     res = {
@@ -216,13 +242,16 @@ def main():
             "parallelism": f"replicas x{world}",
         },
         "roofline": {
-            "bound": "valu_fp64",
+            "bound": "mfma",
+            "compute_pipe": "fp64 VALU (FFT butterflies; no dense contraction on the path)",
             "kernel": "k_blind_rotate",
             "achieved": achieved,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS,
-            "traffic": None,
+            "flops_per_pbs": n * FLOPS_PER_CMUX,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel_ms": br_ms,
             "keyswitch_ms": ks_ms,
             "hbm": {"bound": "hbm", "achieved": hbm_bytes / (br_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
@@ -233,6 +262,13 @@ def main():
         res["ops"] = ops
         res["biguint256_mul_seconds"] = ops["biguint256_mul_compat"]["seconds"]
         res["sign_fhe_with_k0_seconds"] = ops["sign_fhe_with_k0_v0_compat"]["seconds"]
+        res["div256_seconds"] = ops["div256_by_u32"]["seconds"]
+        # published reference CPU numbers for the same operations (README.md:104-114;
+        # c5.24xlarge, likely a debug build) -- context only, not the headline metric
+        readme = {"fheuint32_add": 25.965747001, "fheuint32_mul": 76.051254698, "fheuint32_div5": 1121.134781795,
+                  "sign_fhe_with_k0_v0_compat": 4269.0}
+        res["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
+                                          "speedup": v / ops[k]["seconds"]} for k, v in readme.items() if k in ops}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_seconds)
     if rank == 0:

@@ -401,6 +401,16 @@ int fhe_biguint_digit(const fhe_biguint* x, size_t i, fhe_radix** out) {
     return FHE_OK;
 }
 
+int fhe_biguint_to_radix(const fhe_biguint* x, uint32_t bits, fhe_radix** out) {
+    if (!x || !out || !valid_bits(bits)) return FHE_ERR_INVALID;
+    return guarded([&] {
+        Radix r;
+        for (const Radix& d : x->v.digits) r.blocks.insert(r.blocks.end(), d.blocks.begin(), d.blocks.end());
+        *out = wrap(radix_resize(r, bits / 2), bits);
+        return FHE_OK;
+    });
+}
+
 int fhe_biguint_clone(const fhe_biguint* x, fhe_biguint** out) {
     if (!x || !out) return FHE_ERR_INVALID;
     *out = new fhe_biguint(*x);

@@ -382,26 +382,54 @@ int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t
                                  const uint8_t privkey[32], const fhe_biguint* privkey_fhe, int mode, uint8_t sig[64]) {
     if (!ctx || !ck || (len && !msg) || !k0 || !privkey || !privkey_fhe || !sig) return FHE_ERR_INVALID;
     SignCore c = core(msg, len, U256::from_be(k0), U256::from_be(privkey));
-    // FHE block (src/schnorr.rs:272-276)
-    std::vector<uint32_t> el = u32_digits(c.e), kl = u32_digits(c.k);
-    fhe_biguint *e_fhe = nullptr, *k_fhe = nullptr, *prod = nullptr, *s_fhe = nullptr;
-    int rc = fhe_biguint_encrypt(ctx, ck, el.data(), el.size(), &e_fhe);
-    if (!rc) rc = fhe_biguint_encrypt(ctx, ck, kl.data(), kl.size(), &k_fhe);
-    if (!rc) rc = fhe_biguint_mul(ctx, e_fhe, privkey_fhe, mode, &prod);
-    if (!rc) rc = fhe_biguint_add(ctx, k_fhe, prod, mode, &s_fhe);
     std::vector<uint32_t> limbs;
-    if (!rc) {
-        size_t n = 0;
-        fhe_biguint_len(s_fhe, &n);
-        limbs.resize(n + 1);
-        rc = fhe_biguint_decrypt(ctx, ck, s_fhe, limbs.data(), limbs.size(), &n);
-        limbs.resize(n);
+    int rc = FHE_OK;
+    if (mode == FHE_SIGN_PUBLIC_OPERANDS) {
+        // s = e * Enc(d') + k with e, k clear: one radix wide enough for the exact value
+        // (d' < 2^(32 L), e, k < 2^256  =>  s < 2^(32 L + 257))
+        size_t L = 0;
+        fhe_biguint_len(privkey_fhe, &L);
+        const uint32_t kBits = (uint32_t)(32 * L + 258);
+        if (kBits > FHE_RADIX_MAX_BITS) return FHE_ERR_INVALID;
+        fhe_radix *d = nullptr, *ed = nullptr, *sr = nullptr;
+        uint64_t ew[4], kw[4];
+        for (int i = 0; i < 4; ++i) {
+            ew[i] = c.e.w[i];
+            kw[i] = c.k.w[i];
+        }
+        rc = fhe_biguint_to_radix(privkey_fhe, kBits, &d);
+        if (!rc) rc = fhe_radix_scalar_mul_words(ctx, d, ew, 4, &ed);
+        if (!rc) rc = fhe_radix_scalar_add_words(ctx, ed, kw, 4, &sr);
+        if (!rc) {
+            std::vector<uint64_t> w((kBits + 63) / 64);
+            rc = fhe_radix_decrypt(ctx, ck, sr, w.data(), w.size());
+            for (uint32_t i = 0; i < kBits / 32 + 1 && !rc; ++i) limbs.push_back((uint32_t)(w[i / 2] >> (32 * (i % 2))));
+        }
+        fhe_radix_destroy(d);
+        fhe_radix_destroy(ed);
+        fhe_radix_destroy(sr);
+        if (rc) return rc;
+    } else {
+        // FHE block (src/schnorr.rs:272-276)
+        std::vector<uint32_t> el = u32_digits(c.e), kl = u32_digits(c.k);
+        fhe_biguint *e_fhe = nullptr, *k_fhe = nullptr, *prod = nullptr, *s_fhe = nullptr;
+        rc = fhe_biguint_encrypt(ctx, ck, el.data(), el.size(), &e_fhe);
+        if (!rc) rc = fhe_biguint_encrypt(ctx, ck, kl.data(), kl.size(), &k_fhe);
+        if (!rc) rc = fhe_biguint_mul(ctx, e_fhe, privkey_fhe, mode, &prod);
+        if (!rc) rc = fhe_biguint_add(ctx, k_fhe, prod, mode, &s_fhe);
+        if (!rc) {
+            size_t n = 0;
+            fhe_biguint_len(s_fhe, &n);
+            limbs.resize(n + 1);
+            rc = fhe_biguint_decrypt(ctx, ck, s_fhe, limbs.data(), limbs.size(), &n);
+            limbs.resize(n);
+        }
+        fhe_biguint_destroy(e_fhe);
+        fhe_biguint_destroy(k_fhe);
+        fhe_biguint_destroy(prod);
+        fhe_biguint_destroy(s_fhe);
+        if (rc) return rc;
     }
-    fhe_biguint_destroy(e_fhe);
-    fhe_biguint_destroy(k_fhe);
-    fhe_biguint_destroy(prod);
-    fhe_biguint_destroy(s_fhe);
-    if (rc) return rc;
     // s = s_without_mod % n (to_biguint then %, src/schnorr.rs:275-276)
     std::vector<uint64_t> big((limbs.size() + 1) / 2 + 1, 0);
     for (size_t i = 0; i < limbs.size(); ++i) big[i / 2] |= (uint64_t)limbs[i] << (32 * (i % 2));

@@ -10,6 +10,6 @@ All ciphertext arithmetic runs on the GPU through lib/libfhe_rocm.so; this packa
 from ._lib import FheError, FheParams, load  # noqa: F401
 from .core import ClientKey, Context, ServerKey, default_params, generate_keys  # noqa: F401
 from .integer import (  # noqa: F401,E402
-    COMPAT, FAST, BigUintFHE, FheBool, FheUint, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, set_server_key,
+    COMPAT, FAST, PUBLIC, BigUintFHE, FheBool, FheUint, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, set_server_key,
     stats, to_u32_digits)
 from .schnorr import Schnorr, compute_nonce, public_key_x  # noqa: F401,E402

@@ -87,6 +87,7 @@ _SIGNATURES = [
     ("fhe_biguint_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("fhe_biguint_len", C.c_int, [C.c_void_p, C.POINTER(C.c_size_t)]),
     ("fhe_biguint_digit", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_biguint_to_radix", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_clone", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_destroy", None, [C.c_void_p]),
     ("fhe_biguint_add", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),

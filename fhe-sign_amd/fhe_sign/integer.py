@@ -17,6 +17,7 @@ from ._lib import check, load, ptr
 
 COMPAT = 0  # exact replay of src/biguint.rs:214-254 incl. the wrapping add at :247-249
 FAST = 1    # true product/sum, single wide carry propagation
+PUBLIC = 2  # signer only: e and k stay clear, s = e * Enc(d') + k as a wide scalar multiply-add
 
 _tls = threading.local()
 
@@ -283,6 +284,12 @@ class BigUintFHE:
         if len(limbs) > 2:
             return None
         return sum(d << (32 * i) for i, d in enumerate(limbs))
+
+    def to_radix(self, bits: int):
+        """the limbs' blocks as one FheUint of `bits` (concatenation, no bootstrap)"""
+        h = C.c_void_p()
+        check(load().fhe_biguint_to_radix(self._h, bits, C.byref(h)))
+        return FheUint._wrap(h, bits)
 
     def clone(self):
         h = C.c_void_p()

@@ -182,6 +182,9 @@ int fhe_biguint_decrypt(fhe_ctx* ctx, const fhe_client_key* ck, const fhe_biguin
                         size_t cap, size_t* nlimbs);
 int fhe_biguint_len(const fhe_biguint* x, size_t* nlimbs);
 int fhe_biguint_digit(const fhe_biguint* x, size_t i, fhe_radix** out);
+/* the limbs' blocks as one FheUint<num_bits> (no bootstrap: blocks are concatenated, then
+ * zero-extended or truncated), e.g. to run wide radix ops on a BigUintFHE value */
+int fhe_biguint_to_radix(const fhe_biguint* x, uint32_t num_bits, fhe_radix** out);
 int fhe_biguint_clone(const fhe_biguint* x, fhe_biguint** out);
 void fhe_biguint_destroy(fhe_biguint* x);
 /* impl Add / impl Mul for BigUintFHE (src/biguint.rs:120-265); inputs are not consumed */
@@ -200,7 +203,12 @@ int fhe_schnorr_sign_with_k0(const uint8_t* msg, size_t msg_len, const uint8_t k
                              const uint8_t privkey[32], uint8_t sig[64]);
 int fhe_schnorr_sign(const uint8_t* msg, size_t msg_len, const uint8_t aux_rand[32],
                      const uint8_t privkey[32], uint8_t sig[64]);
-/* Schnorr::sign_fhe_with_k0 (src/schnorr.rs:235-290): privkey_fhe = BigUintFHE::new(privkey) */
+/* Schnorr::sign_fhe_with_k0 (src/schnorr.rs:235-290): privkey_fhe = BigUintFHE::new(privkey).
+ * mode FHE_BIGUINT_COMPAT / FHE_BIGUINT_FAST run the reference's block (e and k encrypted, BigUintFHE
+ * mul + add); FHE_SIGN_PUBLIC_OPERANDS keeps e and k in the clear (they are public values the
+ * reference encrypts anyway, src/schnorr.rs:272-273): s = e * Enc(d') + k as one wide radix
+ * scalar multiply-add.  All modes decrypt to the same s, hence byte-identical signatures. */
+#define FHE_SIGN_PUBLIC_OPERANDS 2
 int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t msg_len,
                                  const uint8_t k0[32], const uint8_t privkey[32],
                                  const fhe_biguint* privkey_fhe, int mode, uint8_t sig[64]);

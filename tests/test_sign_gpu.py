@@ -7,7 +7,7 @@ import os
 import pytest
 
 from conftest import ROOT
-from fhe_sign import COMPAT, FAST, BigUintFHE, Context, Schnorr, compute_nonce, generate_keys, public_key_x, set_server_key
+from fhe_sign import COMPAT, FAST, PUBLIC, BigUintFHE, Context, Schnorr, compute_nonce, generate_keys, public_key_x, set_server_key
 
 pytestmark = pytest.mark.gpu
 ROWS = {r["index"]: r for r in csv.DictReader(open(os.path.join(ROOT, "tests", "golden", "bip340_vectors.csv")))}
@@ -56,3 +56,17 @@ def test_sign_fhe_vector0(env):
     """sign_fhe (src/schnorr.rs:154): encrypts the private key itself."""
     sig = Schnorr().sign_fhe(bytes(32), bytes(32), 3, env)
     assert sig.hex().upper() == ROWS["0"]["signature"].upper()
+
+
+@pytest.mark.parametrize("idx", ["0", "1", "2", "16", "17", "18"])
+def test_sign_public_operands_mode(env, idx):
+    """e and k kept clear; the signature must not change (CSV rows with a signature)."""
+    sig, row = _sign_case(env, idx, PUBLIC)
+    assert sig.hex().upper() == row["signature"].upper()
+
+
+def test_biguint_to_radix(env):
+    v = (1 << 255) | 0x1234_5678_9ABC
+    x = BigUintFHE.new(v, env)
+    assert x.to_radix(300).decrypt(env) == v
+    assert x.to_radix(64).decrypt(env) == v & (2**64 - 1)
