@@ -29,6 +29,7 @@ import numpy as np  # noqa: E402
 METRIC = "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds @1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6        # MI355X dense FP64 peak (matrix = vector on gfx950), spec
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "r1f_pmc_summary.json")  # tools/profile_round.sh
+FANOUT_MIN = 512  # levels with at least this many bootstraps are split over the GPUs (fan-out legs)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FLOPS_PER_CMUX = 4 * 51200 + 4 * 6144 + 32768   # 4 FFT-1024 (5 N log N), 4 twist/untwist, MAC
 
@@ -155,13 +156,76 @@ def ops_legs(ck, ctx, seed):
     return out
 
 
+def fanout_legs(ck, ctx, dist, rank, world, seed):
+    """config 5 / SURVEY.md 8e: ONE 256-bit mul and ONE sign fanned across all ranks (levels of at
+    least FANOUT_MIN bootstraps split over the GPUs, outputs all-gathered with RCCL).  Identical
+    inputs on every rank; a failure on any rank stops the fan-out legs on all of them."""
+    import random
+    from fhe_sign import COMPAT, FAST, BigUintFHE, Schnorr, compute_nonce, set_server_key
+    from fhe_sign.dist import all_ok, attach_fanout
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_semantics as R
+    out = {"ranks": world, "min_level": FANOUT_MIN}
+    ok, err = attach_fanout(ctx, dist, rank, world, min_level=FANOUT_MIN)
+    if not ok:
+        out["error"] = err
+        return out
+    set_server_key(ctx)
+    rng = random.Random(seed ^ 0xFA)
+    a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(256) | 1 << 255
+    ck.seed_encryption(seed ^ 0x5EED, 100)  # every rank encrypts the same ciphertexts
+    A, B = BigUintFHE.new(a, ck), BigUintFHE.new(b, ck)
+    d, msg = 3, bytes(32)
+    k0 = compute_nonce(d, msg, bytes(32))
+    dF = BigUintFHE.new(d, ck)
+    s = Schnorr()
+    ref = s.sign_with_k0(msg, k0, d)
+    legs = [
+        ("warmup_add_fast", lambda: A.add(B, FAST), lambda r: r.to_biguint(ck) == a + b),
+        ("biguint256_mul_fast", lambda: A.mul(B, FAST), lambda r: r.to_biguint(ck) == a * b),
+        ("biguint256_mul_compat", lambda: A.mul(B, COMPAT),
+         lambda r: r.decrypt_limbs(ck) == R.biguint_mul(R.to_u32_digits(a), R.to_u32_digits(b))),
+        ("sign_fhe_with_k0_v0_compat", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT), lambda r: r == ref),
+        ("sign_fhe_with_k0_v0_fast", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, FAST), lambda r: r == ref),
+    ]
+    for name, fn, check in legs:
+        barrier(dist)
+        ctx.sync()
+        _, _, lv0 = ctx.fanout_info()
+        t0 = time.perf_counter()
+        good, why = False, None
+        try:
+            r = fn()
+            ctx.sync()
+            dt = time.perf_counter() - t0
+            good = bool(check(r))
+            why = None if good else "result mismatch"
+        except Exception as e:  # noqa: BLE001 -- agreed below, reported in the JSON line
+            dt, why = time.perf_counter() - t0, str(e)
+        _, _, lv1 = ctx.fanout_info()
+        agreed = all_ok(dist, good)
+        out[name] = {"seconds": allmax(dist, dt), "ok": agreed, "split_levels": lv1 - lv0}
+        if not agreed:
+            out["error"] = why or "failed on another rank"
+            break
+    try:
+        ctx.detach_comm()
+    except Exception:  # noqa: BLE001
+        pass
+    return out
+
+
 def main():
     a = parse()
     dist, rank, world, local = dist_setup(a.gpus)
     from fhe_sign import Context, generate_keys
 
     ck, sk = generate_keys(seed=a.seed)
-    ctx = Context(local)
+    device = local
+    if dist is not None:  # more ranks than visible GPUs (rehearsals): ranks share devices round-robin
+        import torch
+        device = local % max(1, torch.cuda.device_count())
+    ctx = Context(device)
     ctx.set_server_key(sk)
     n = sk.params.lwe_dimension
     lid = ctx.lut([(m + 1) % 16 for m in range(16)])
@@ -212,6 +276,7 @@ def main():
     if ops is not None and dist is not None:
         for k in ops:
             ops[k]["seconds"] = allmax(dist, ops[k]["seconds"])
+    fan = fanout_legs(ck, ctx, dist, rank, world, a.seed) if (world > 1 and not a.no_ops) else None
 
     total = world * B * a.steps
     br_ms = float(np.mean(br_t))
@@ -269,6 +334,8 @@ def main():
                   "sign_fhe_with_k0_v0_compat": 4269.0}
         res["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
                                           "speedup": v / ops[k]["seconds"]} for k, v in readme.items() if k in ops}
+    if fan is not None:
+        res["fanout"] = fan
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_seconds)
     if rank == 0:

@@ -305,8 +305,9 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     delete c->engine;
     c->engine = nullptr;
+    c->release_comm();
     void* ptrs[] = {c->d_ksk, c->d_bsk, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out,
-                    c->d_stage_lut};
+                    c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)

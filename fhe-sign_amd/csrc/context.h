@@ -68,6 +68,21 @@ struct fhe_ctx {
     float last_ks_ms = 0.f, last_br_ms = 0.f;
     // radix-layer executor (created with the server key)
     fhe::Engine* engine = nullptr;
+    // Multi-GPU fan-out (comm.cpp): every rank runs the same radix program on identical inputs;
+    // a level with at least fanout_min bootstraps is split contiguously over the ranks and its
+    // outputs are all-gathered (RCCL over xGMI) -- smaller levels are computed redundantly, since
+    // one ciphertext per CU is already their latency floor.
+    void* comm = nullptr;       // ncclComm_t
+    int rank = 0, nranks = 1;
+    int fanout_emulate = 0;     // test hook: split levels over this many virtual ranks on one GPU
+    size_t fanout_min = 512;
+    uint64_t* d_gather = nullptr;        // [nranks * chunk][2049]
+    size_t gather_cap = 0;               // ciphertexts
+    int fanout_world() const { return comm ? nranks : (fanout_emulate > 1 ? fanout_emulate : 1); }
+    int ensure_gather(size_t ciphertexts);
+    // in-place all-gather of nranks segments of `words` u64 each (segment `rank` is local)
+    int allgather(uint64_t* buf, size_t words);
+    void release_comm();
 
     int ensure_ms(size_t count);
     int ensure_stage(size_t count);

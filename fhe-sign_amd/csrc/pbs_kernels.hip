@@ -394,4 +394,18 @@ hipError_t launch_bsk_to_fourier(const uint64_t* bsk, int npoly, const cplx* W, 
     return hipGetLastError();
 }
 
+// ============================================================================ fan-out scatter
+// One workgroup per ciphertext: 2049 words from the gather buffer into its block slot.
+__global__ __launch_bounds__(256) void k_scatter_blocks(const uint64_t* __restrict__ src, uint64_t* const* __restrict__ dst) {
+    const uint64_t* s = src + (size_t)blockIdx.x * 2049;
+    uint64_t* d = dst[blockIdx.x];
+    for (int j = threadIdx.x; j < 2049; j += 256) d[j] = s[j];
+}
+
+hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter_blocks, dim3(count), dim3(256), 0, s, src, dst);
+    return hipGetLastError();
+}
+
 }  // namespace fhe

@@ -175,10 +175,18 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     if (gpu.empty()) return out;
 
     // register LUTs, allocate destinations, build descriptors
+    const size_t G = gpu.size();
+    const int W = ctx_->fanout_world();
+    const bool split = W > 1 && G >= ctx_->fanout_min;
+    const size_t chunk = split ? (G + W - 1) / W : G;
+    if (split) engine_check(ctx_->ensure_gather(chunk * W) == FHE_OK, "gather workspace");
+    // descriptors, then (fanned-out levels) the destination slot table, in one pinned staging copy
+    const size_t ndesc = G + (split ? (G * sizeof(uint64_t*) + sizeof(PbsDesc) - 1) / sizeof(PbsDesc) : 0);
     PbsDesc* dev = nullptr;
-    PbsDesc* h = stage_desc(gpu.size(), &dev);
+    PbsDesc* h = stage_desc(ndesc, &dev);
+    uint64_t** h_scat = reinterpret_cast<uint64_t**>(h + G);
     const uint64_t delta = p.delta();
-    for (size_t g = 0; g < gpu.size(); ++g) {
+    for (size_t g = 0; g < G; ++g) {
         const size_t i = gpu[g];
         uint32_t lut = 0;
         engine_check(ctx_->register_lut(items[i].table.data(), &lut) == FHE_OK, "LUT registration");
@@ -193,18 +201,35 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         d.nterms = (uint32_t)live[i].size();
         d.lut = lut;
         d.cst = (uint64_t)csts[i] * delta;
-        d.dst = out[i].slot->p;
+        // fanned-out levels bootstrap into the gather buffer (segment = owning rank), then scatter
+        d.dst = split ? ctx_->d_gather + g * kBigCt : out[i].slot->p;
+        if (split) h_scat[g] = out[i].slot->p;
         h[g] = d;
     }
     engine_check(ctx_->sync_luts() == FHE_OK, "LUT upload");
-    engine_check(ctx_->ensure_ms(gpu.size()) == FHE_OK, "workspace");
-    hip_check(hipMemcpyAsync(dev, h, gpu.size() * sizeof(PbsDesc), hipMemcpyHostToDevice, ctx_->stream), "desc copy");
+    engine_check(ctx_->ensure_ms(chunk) == FHE_OK, "workspace");
+    hip_check(hipMemcpyAsync(dev, h, ndesc * sizeof(PbsDesc), hipMemcpyHostToDevice, ctx_->stream), "desc copy");
     hip_check(hipEventRecord(desc_ev_[desc_turn_], ctx_->stream), "desc event");
-    hip_check(launch_keyswitch_desc(dev, (int)gpu.size(), ctx_->d_ksk, ctx_->d_ms, ctx_->ms_stride, (int)p.n,
-                                    ctx_->stream),
-              "keyswitch");
-    hip_check(ctx_->blind_rotate(dev, nullptr, nullptr, gpu.size()), "blind rotate");
-    pbs_count += gpu.size();
+    auto pbs = [&](size_t lo, size_t hi) {
+        if (hi <= lo) return;
+        hip_check(launch_keyswitch_desc(dev + lo, (int)(hi - lo), ctx_->d_ksk, ctx_->d_ms, ctx_->ms_stride, (int)p.n,
+                                        ctx_->stream),
+                  "keyswitch");
+        hip_check(ctx_->blind_rotate(dev + lo, nullptr, nullptr, hi - lo), "blind rotate");
+    };
+    if (!split) {
+        pbs(0, G);
+    } else {
+        // own slice (every slice when ranks are emulated on one GPU)
+        for (int r = 0; r < W; ++r)
+            if (!ctx_->comm || r == ctx_->rank) pbs(r * chunk, std::min(G, (r + 1) * chunk));
+        engine_check(ctx_->allgather(ctx_->d_gather, chunk * kBigCt) == FHE_OK, "all-gather");
+        hip_check(launch_scatter_blocks(ctx_->d_gather, reinterpret_cast<uint64_t* const*>(dev + G), (int)G,
+                                        ctx_->stream),
+                  "scatter");
+        fanout_levels += 1;
+    }
+    pbs_count += G;
     levels += 1;
     return out;
 }

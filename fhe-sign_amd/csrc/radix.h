@@ -91,7 +91,7 @@ public:
     void download(const Block& b, uint64_t* ct);
     void sync();
     // statistics
-    uint64_t pbs_count = 0, levels = 0;
+    uint64_t pbs_count = 0, levels = 0, fanout_levels = 0;
 
 private:
     fhe_ctx* ctx_;

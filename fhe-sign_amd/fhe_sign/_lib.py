@@ -52,6 +52,11 @@ _SIGNATURES = [
     ("fhe_ctx_last_pbs_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("fhe_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_ctx_set_wide_threshold", C.c_int, [C.c_void_p, C.c_int]),
+    ("fhe_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
+    ("fhe_ctx_attach_comm", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+    ("fhe_ctx_detach_comm", C.c_int, [C.c_void_p]),
+    ("fhe_ctx_set_fanout", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
+    ("fhe_ctx_fanout_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint64)]),
     ("fhe_radix_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u64p, C.c_uint32, C.POINTER(C.c_void_p)]),
     ("fhe_radix_trivial", C.c_int, [C.c_void_p, u64p, C.c_uint32, C.POINTER(C.c_void_p)]),
     ("fhe_radix_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u64p, C.c_size_t]),

@@ -75,6 +75,13 @@ class ServerKey:
         return ksk, bsk
 
 
+def comm_unique_id() -> bytes:
+    """RCCL unique id (rank 0 creates it and shares it out of band, e.g. over torch.distributed)."""
+    buf = (C.c_uint8 * 128)()
+    check(load().fhe_comm_unique_id(buf))
+    return bytes(buf)
+
+
 def generate_keys(params: FheParams | None = None, seed: int = 0):
     """tfhe::generate_keys(ConfigBuilder::default().build()) -- src/schnorr.rs:441-442."""
     p = params or default_params()
@@ -151,6 +158,22 @@ class Context:
 
     def set_wide_threshold(self, threshold: int) -> None:
         check(load().fhe_ctx_set_wide_threshold(self._h, int(threshold)))
+
+    # ---- multi-GPU fan-out (one process per GPU)
+    def attach_comm(self, unique_id: bytes, nranks: int, rank: int) -> None:
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        check(load().fhe_ctx_attach_comm(self._h, buf, nranks, rank))
+
+    def detach_comm(self) -> None:
+        check(load().fhe_ctx_detach_comm(self._h))
+
+    def set_fanout(self, min_level: int = 512, emulate_ranks: int = 0) -> None:
+        check(load().fhe_ctx_set_fanout(self._h, int(min_level), int(emulate_ranks)))
+
+    def fanout_info(self):
+        r, n, lv = C.c_int(), C.c_int(), C.c_uint64()
+        check(load().fhe_ctx_fanout_info(self._h, C.byref(r), C.byref(n), C.byref(lv)))
+        return int(r.value), int(n.value), int(lv.value)
 
     def enable_timing(self, on: bool = True) -> None:
         check(load().fhe_ctx_enable_timing(self._h, 1 if on else 0))

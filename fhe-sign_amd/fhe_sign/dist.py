@@ -1,0 +1,57 @@
+"""Multi-GPU fan-out control plane: one process per GPU.
+
+The data path is the engine's own RCCL communicator (comm.cpp: in-place all-gather of each split
+level on the engine stream).  This module only does the out-of-band part over an already
+initialised torch.distributed process group (gloo is enough): rank 0 creates the RCCL id, every
+rank receives it and attaches, and the ranks agree that all of them succeeded before any
+collective is issued -- a rank that failed alone would otherwise leave the others waiting in an
+all-gather.
+"""
+from __future__ import annotations
+
+from .core import comm_unique_id
+
+
+def all_ok(dist, ok: bool) -> bool:
+    """True iff `ok` holds on every rank (gloo all-reduce MIN)."""
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def share_id(dist, rank: int, make_id=comm_unique_id) -> bytes | None:
+    """Rank 0's RCCL unique id on every rank (None everywhere if rank 0 could not create one)."""
+    import torch
+    buf = torch.zeros(129, dtype=torch.uint8)
+    if rank == 0:
+        try:
+            buf[:128] = torch.tensor(list(make_id()), dtype=torch.uint8)
+            buf[128] = 1
+        except Exception:  # noqa: BLE001 -- reported through the flag
+            buf[128] = 0
+    dist.broadcast(buf, 0)
+    return bytes(buf[:128].tolist()) if int(buf[128]) else None
+
+
+def attach_fanout(ctx, dist, rank: int, world: int, min_level: int = 512, make_id=comm_unique_id):
+    """Attach `ctx` to a world-size RCCL communicator and enable level fan-out.
+    Returns (ok, error): ok is identical on all ranks."""
+    err = None
+    uid = share_id(dist, rank, make_id)
+    ok = uid is not None
+    if not ok:
+        err = "rank 0 could not create an RCCL id"
+    else:
+        try:
+            ctx.attach_comm(uid, world, rank)
+            ctx.set_fanout(min_level)
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, str(e)
+    if not all_ok(dist, ok):
+        try:
+            ctx.detach_comm()
+        except Exception:  # noqa: BLE001
+            pass
+        return False, err or "another rank failed to attach"
+    return True, None

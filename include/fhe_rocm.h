@@ -110,6 +110,20 @@ int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 640. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
 
+/* ------------------------------------------------------------------- multi-GPU fan-out */
+/* One process per GPU.  All ranks run the same radix program on identical inputs
+ * (same keys, same ciphertexts); a dependency level with at least `min_level` bootstraps is split
+ * over the ranks and its outputs all-gathered with RCCL on the engine stream.  Smaller levels are
+ * computed redundantly on every rank.  Rank 0 creates the id and shares it out of band. */
+#define FHE_COMM_ID_BYTES 128
+int fhe_comm_unique_id(uint8_t id[FHE_COMM_ID_BYTES]);
+int fhe_ctx_attach_comm(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank);
+int fhe_ctx_detach_comm(fhe_ctx* ctx);
+/* split threshold (default 512) and, for single-GPU tests, the number of emulated ranks (0 = off) */
+int fhe_ctx_set_fanout(fhe_ctx* ctx, uint32_t min_level, int emulate_ranks);
+/* rank, world (emulated ranks counted) and the number of levels split so far */
+int fhe_ctx_fanout_info(const fhe_ctx* ctx, int* rank, int* nranks, uint64_t* fanout_levels);
+
 /* ------------------------------------------------------------------- radix integers */
 /* FheUint<num_bits> (num_bits even, <= FHE_RADIX_MAX_BITS): num_bits/2 radix blocks, device-resident.
  * Replaces tfhe's FheUint8/32/64 as used at src/biguint.rs:26,135-143,221-248 and

@@ -49,3 +49,61 @@ def test_single_rank_needs_no_process_group():
     import bench
     assert bench.dist_setup(1) == (None, 0, 1, 0)
     assert bench.allmax(None, 2.5) == 2.5
+
+
+class _FakeCtx:
+    """Stands in for fhe_sign.Context: records what the fan-out control plane asks of it."""
+
+    def __init__(self, fail=False):
+        self.fail, self.calls = fail, []
+
+    def attach_comm(self, uid, world, rank):
+        if self.fail:
+            raise RuntimeError("attach refused")
+        self.calls.append(("attach", uid, world, rank))
+
+    def set_fanout(self, min_level):
+        self.calls.append(("fanout", min_level))
+
+    def detach_comm(self):
+        self.calls.append(("detach",))
+
+
+def _fanout_rank(rank, world, port, fail_rank, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
+    import torch.distributed as dist
+    from fhe_sign.dist import attach_fanout
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = _FakeCtx(fail=rank == fail_rank)
+    ok, err = attach_fanout(ctx, dist, rank, world, min_level=300, make_id=lambda: bytes(range(128)))
+    q.put((rank, ok, ctx.calls))
+    dist.destroy_process_group()
+
+
+def _run_fanout(fail_rank):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fanout_rank, args=(r, 2, port, fail_rank, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    return sorted(q.get() for _ in range(2))
+
+
+def test_fanout_attach_world2_shares_rank0_id():
+    """SURVEY 8e control plane: every rank attaches with rank 0's RCCL id and the split threshold."""
+    got = _run_fanout(fail_rank=-1)
+    for rank, ok, calls in got:
+        assert ok
+        assert calls == [("attach", bytes(range(128)), 2, rank), ("fanout", 300)]
+
+
+def test_fanout_attach_failure_is_agreed():
+    """one rank failing to attach makes every rank back out (no rank is left in a collective)"""
+    got = _run_fanout(fail_rank=1)
+    assert [ok for _, ok, _ in got] == [False, False]
+    assert got[0][2][-1] == ("detach",)

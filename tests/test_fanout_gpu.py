@@ -1,0 +1,81 @@
+"""Multi-GPU fan-out of the radix layer exercised on one GPU.
+
+A fanned-out level is split into contiguous rank slices that bootstrap into a gather buffer, are
+all-gathered (RCCL) and scattered into the block slots.  Here the split runs (a) over emulated
+ranks on one device -- every slice is computed locally, so the outputs must be byte-identical to
+the unsplit run, which pins the partition / gather / scatter indexing -- and (b) through a real
+RCCL communicator of world 1 (the all-gather path with the library).  Multi-rank RCCL on distinct
+GPUs is exercised by bench.py's fan-out leg at N > 1; the out-of-band id exchange is covered on
+CPU by tests/test_dist_cpu.py."""
+import random
+
+import numpy as np
+import pytest
+
+from fhe_sign import (COMPAT, FAST, BigUintFHE, Context, FheUint64, FheUint256, Schnorr, comm_unique_id, compute_nonce,
+                      generate_keys, set_server_key)
+
+pytestmark = pytest.mark.gpu
+
+
+def run_ops(ctx, ck):
+    set_server_key(ctx)
+    rng = random.Random(5)
+    a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(64)
+    ck.seed_encryption(77)  # identical ciphertext inputs for every configuration
+    A, B = FheUint256.try_encrypt(a, ck), FheUint64.try_encrypt(b, ck)
+    outs = {
+        "div": A / (rng.getrandbits(32) | 1),
+        "mul64": B * FheUint64.try_encrypt(rng.getrandbits(64), ck),
+        "sum": A + FheUint256.try_encrypt(rng.getrandbits(256), ck),
+    }
+    return {k: v.export() for k, v in outs.items()}, {k: v.decrypt(ck) for k, v in outs.items()}
+
+
+@pytest.fixture(scope="module")
+def keys():
+    ck, sk = generate_keys(seed=0xFA11)
+    return ck, sk
+
+
+def test_emulated_ranks_byte_identical(keys):
+    ck, sk = keys
+    ref_ctx = Context(0)
+    ref_ctx.set_server_key(sk)
+    ref_ct, ref_val = run_ops(ref_ctx, ck)
+    assert ref_ctx.fanout_info() == (0, 1, 0)
+    for ranks in (2, 3, 8):
+        ctx = Context(0)
+        ctx.set_server_key(sk)
+        ctx.set_fanout(min_level=1, emulate_ranks=ranks)
+        ct, val = run_ops(ctx, ck)
+        assert val == ref_val
+        for k in ref_ct:
+            assert np.array_equal(ct[k], ref_ct[k]), (ranks, k)
+        _, world, split = ctx.fanout_info()
+        assert world == ranks and split > 0
+        ctx.close()
+    set_server_key(None)
+    ref_ctx.close()
+
+
+def test_rccl_world1_all_gather(keys):
+    ck, sk = keys
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    ctx.attach_comm(comm_unique_id(), 1, 0)
+    ctx.set_fanout(min_level=1)
+    _, val = run_ops(ctx, ck)
+    ref_ctx = Context(0)
+    ref_ctx.set_server_key(sk)
+    _, ref_val = run_ops(ref_ctx, ck)
+    assert val == ref_val
+    set_server_key(ctx)
+    d, msg = 3, bytes(32)
+    k0 = compute_nonce(d, msg, bytes(32))
+    s = Schnorr()
+    assert s.sign_fhe_with_k0(msg, k0, d, BigUintFHE.new(d, ck), ck, FAST) == s.sign_with_k0(msg, k0, d)
+    ctx.detach_comm()
+    set_server_key(None)
+    ctx.close()
+    ref_ctx.close()

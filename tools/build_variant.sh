@@ -21,6 +21,6 @@ cp "$SRC" $VS
     -c -o $OUT/obj/pbs_kernels.o $VS
 rm -f $VS
 OBJS=$(ls $PKG/build/*.o | grep -v pbs_kernels.o)
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/lib/libfhe_rocm.so $OUT/obj/pbs_kernels.o $OBJS -lpthread
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/lib/libfhe_rocm.so $OUT/obj/pbs_kernels.o $OBJS -lpthread -L/opt/rocm/lib -lrccl
 rm -rf $OUT/fhe_sign && cp -r $PKG/fhe_sign $OUT/fhe_sign
 echo "built $OUT"
