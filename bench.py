@@ -265,6 +265,13 @@ def main():
     barrier(dist)
     dt = allmax(dist, dt)
 
+    # host-buffer boundary (fhe_pbs_batch: H2D + KS/BR + D2H), reported beside `value`, never as it
+    t0 = time.perf_counter()
+    host_reps = 2
+    for _ in range(host_reps):
+        ctx.pbs(cts, lid)
+    pcie_rate = host_reps * B / (time.perf_counter() - t0)
+
     # correctness spot check of the last step (decrypt a sample)
     out = np.zeros_like(cts)
     ctx.d2h(out, d_out)
@@ -334,6 +341,7 @@ def main():
                   "sign_fhe_with_k0_v0_compat": 4269.0}
         res["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
                                           "speedup": v / ops[k]["seconds"]} for k, v in readme.items() if k in ops}
+    res["pcie_inclusive_pbs_per_s"] = pcie_rate * world  # per-rank host-buffer rate x ranks
     if fan is not None:
         res["fanout"] = fan
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
