@@ -48,6 +48,15 @@ void lane_twiddles(const std::vector<double2>& W, std::vector<double2>* Wl) {
     }
 }
 
+void quad_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,
+                 std::vector<double2>* ps) {
+    // br_quad.hip: twiddles W[0..512) (copied into LDS per workgroup), twist psi[128 r + t] per thread
+    tw->assign(W.begin(), W.begin() + 512);
+    ps->assign(8 * 128, make_double2(0.0, 0.0));
+    for (int t = 0; t < 128; ++t)
+        for (int r = 0; r < 8; ++r) (*ps)[r * 128 + t] = psi[128 * r + t];
+}
+
 void wide_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,
                  std::vector<double2>* psiw) {
     tw->assign(12 * 256, make_double2(0.0, 0.0));
@@ -177,6 +186,9 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     if ((int)count <= wide_threshold)
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide, out,
                                         (int)count, (int)p.n, stream);
+    if (br_kernel == FHE_BR_QUAD)
+        return launch_blind_rotate_quad(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_quad, d_tw_quad, d_psi_quad, out,
+                                        (int)count, (int)p.n, stream);
     if (desc)
         return launch_blind_rotate_desc(d_ms, ms_stride, desc, d_luts, d_bsk, d_W, d_psi, (int)count, (int)p.n,
                                         stream);
@@ -282,10 +294,15 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
         return FHE_ERR_HIP;
     }
     for (auto& ev : c->ev) FHE_HIP_CHECK(hipEventCreate(&ev));
-    std::vector<double2> W0, W, psi, tww, psiw;
+    std::vector<double2> W0, W, psi, tww, psiw, twq, psq;
     fft_tables(&W0, &psi);
     lane_twiddles(W0, &W);
     wide_tables(W0, psi, &tww, &psiw);
+    quad_tables(W0, psi, &twq, &psq);
+    FHE_HIP_CHECK(hipMalloc(&c->d_tw_quad, twq.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMalloc(&c->d_psi_quad, psq.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMemcpy(c->d_tw_quad, twq.data(), twq.size() * sizeof(double2), hipMemcpyHostToDevice));
+    FHE_HIP_CHECK(hipMemcpy(c->d_psi_quad, psq.data(), psq.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMalloc(&c->d_tw_wide, tww.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMalloc(&c->d_psi_wide, psiw.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_tw_wide, tww.data(), tww.size() * sizeof(double2), hipMemcpyHostToDevice));
@@ -306,8 +323,8 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     delete c->engine;
     c->engine = nullptr;
     c->release_comm();
-    void* ptrs[] = {c->d_ksk, c->d_bsk, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out,
-                    c->d_stage_lut, c->d_gather};
+    void* ptrs[] = {c->d_ksk, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
+                    c->d_psi_quad, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)
@@ -324,8 +341,10 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
         FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
         FHE_HIP_CHECK(hipFree(c->d_ksk));
         FHE_HIP_CHECK(hipFree(c->d_bsk));
+        FHE_HIP_CHECK(hipFree(c->d_bsk_quad));
         c->d_ksk = nullptr;
         c->d_bsk = nullptr;
+        c->d_bsk_quad = nullptr;
         c->has_key = false;
     }
     FHE_HIP_CHECK(hipMalloc(&c->d_ksk, sk->ksk.size() * 8));
@@ -336,6 +355,8 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     FHE_HIP_CHECK(hipMalloc(&c->d_bsk, (size_t)npoly * 1024 * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpyAsync(d_std, sk->bsk.data(), sk->bsk.size() * 8, hipMemcpyHostToDevice, c->stream));
     FHE_HIP_CHECK(launch_bsk_to_fourier(d_std, npoly, c->d_W, c->d_psi, c->d_bsk, c->stream));
+    FHE_HIP_CHECK(hipMalloc(&c->d_bsk_quad, (size_t)npoly * 1024 * sizeof(double2)));
+    FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, c->d_bsk_quad, c->stream));
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
     FHE_HIP_CHECK(hipFree(d_std));
     if (!c->has_key || !(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
@@ -446,6 +467,12 @@ int fhe_memcpy_d2h(fhe_ctx* c, void* dst, const void* src, size_t bytes) {
     FHE_HIP_CHECK(hipSetDevice(c->device));
     FHE_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return FHE_OK;
+}
+
+int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
+    if (!c || (kind != FHE_BR_NARROW && kind != FHE_BR_QUAD)) return FHE_ERR_INVALID;
+    c->br_kernel = kind;
     return FHE_OK;
 }
 

@@ -28,6 +28,8 @@ void fft_tables(std::vector<double2>* W, std::vector<double2>* psi);
 // Per-lane twiddle table [slot][lane] (device_math.h:tw_slot) built from W.
 void lane_twiddles(const std::vector<double2>& W, std::vector<double2>* Wl);
 // Per-thread tables of the wide (latency) blind rotate: tw[12][256], psi[4][256] (br_wide.hip).
+void quad_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,
+                 std::vector<double2>* ps);
 void wide_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,
                  std::vector<double2>* psiw);
 // Accumulator polynomial of a univariate LUT (tfhe shortint box encoding, padding bit).
@@ -46,6 +48,10 @@ struct fhe_ctx {
     double2* d_psi = nullptr;
     double2* d_tw_wide = nullptr;   // [12][256]
     double2* d_psi_wide = nullptr;  // [4][256]
+    double2* d_bsk_quad = nullptr;  // Fourier BSK in the 4-wave kernel's layout (br_quad.hip)
+    double2* d_tw_quad = nullptr;   // W[0..512)
+    double2* d_psi_quad = nullptr;  // [8][128]
+    int br_kernel = FHE_BR_QUAD;    // throughput kernel for levels above wide_threshold
     // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU)
     int wide_threshold = 640;  // crossover measured in profiles/r1/latency_sweep_r1e.txt
     // LUT registry: table contents -> id, device array of accumulator polynomials

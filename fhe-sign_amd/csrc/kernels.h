@@ -34,6 +34,10 @@ hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const Pbs
                                     uint64_t* out, int count, int n, hipStream_t s);
 // dst_i = sum_t coef * src + cst, no bootstrap (linear radix ops)
 hipError_t launch_lincomb(const PbsDesc* desc, int count, hipStream_t s);
+hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
+                                    const uint64_t* luts, const double2* bsk_quad, const double2* tw, const double2* ps,
+                                    uint64_t* out, int count, int n, hipStream_t s);
+hipError_t launch_bsk_to_quad(const double2* bsk, int npoly, double2* out, hipStream_t s);
 // dst[i][0..2049) = src[i * 2049 ..] for i < count (all-gathered level outputs -> block slots)
 hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s);
 hipError_t launch_bsk_to_fourier(const uint64_t* bsk, int npoly, const double2* W,

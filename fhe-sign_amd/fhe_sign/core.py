@@ -156,6 +156,10 @@ class Context:
     def sync(self) -> None:
         check(load().fhe_ctx_sync(self._h))
 
+    def set_br_kernel(self, kind: int) -> None:
+        """0 = 2-wave throughput kernel, 1 = 4-wave (default); identical results"""
+        check(load().fhe_ctx_set_br_kernel(self._h, int(kind)))
+
     def set_wide_threshold(self, threshold: int) -> None:
         check(load().fhe_ctx_set_wide_threshold(self._h, int(threshold)))
 

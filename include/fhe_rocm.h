@@ -109,6 +109,11 @@ int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 640. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
+/* Throughput blind-rotate kernel for levels above the threshold: 2 waves per ciphertext
+ * (FHE_BR_NARROW) or 4 (FHE_BR_QUAD, default).  All kernels produce identical bits. */
+#define FHE_BR_NARROW 0
+#define FHE_BR_QUAD 1
+int fhe_ctx_set_br_kernel(fhe_ctx* ctx, int kind);
 
 /* ------------------------------------------------------------------- multi-GPU fan-out */
 /* One process per GPU.  All ranks run the same radix program on identical inputs
