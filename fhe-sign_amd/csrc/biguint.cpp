@@ -18,59 +18,43 @@ static Radix slice(const Radix& r, uint32_t from, uint32_t count) {
 }
 
 // impl Add for BigUintFHE (src/biguint.rs:120-192)
+// impl Add for BigUintFHE (src/biguint.rs:120-192).  The reference's limb loop never wraps (each
+// FheUint64 sum is < 2^34, the carry is its bit 32) and it always appends the final carry limb,
+// except that a zero (empty) operand returns the other one cloned (:163-165, :175-177).  So the
+// limbs it produces are exactly the true sum in max(la, lb) + 1 limbs: both modes compute that with
+// one wide carry propagation (a few levels instead of a limb-serial ripple).  `mode` is kept for the
+// ABI; tests/test_radix_gpu.py checks the limbs against oracle/ref_semantics.py:biguint_add.
 BigUint biguint_add(Engine& e, const BigUint& A, const BigUint& B, int mode) {
+    (void)mode;
     const size_t la = A.digits.size(), lb = B.digits.size(), max_len = std::max(la, lb);
     BigUint out;
-    if (mode == kFast) {
-        // identical results: the reference's add never wraps (each limb sum < 2^34)
-        if (la == 0) return B;
-        if (lb == 0) return A;
-        std::vector<const Radix*> pa, pb;
-        for (auto& d : A.digits) pa.push_back(&d);
-        for (auto& d : B.digits) pb.push_back(&d);
-        Radix wa = concat(pa), wb = concat(pb);
-        const uint32_t nb = (uint32_t)(max_len + 1) * kLimbBlocks;
-        Radix s = radix_sum(e, {&wa, &wb}, nb);
-        for (size_t i = 0; i <= max_len; ++i) out.digits.push_back(slice(s, (uint32_t)i * kLimbBlocks, kLimbBlocks));
-        return out;
-    }
-    bool have_carry = false;
-    Radix carry;
-    for (size_t i = 0; i < max_len; ++i) {
-        const Radix* a = i < la ? &A.digits[i] : nullptr;
-        const Radix* b = i < lb ? &B.digits[i] : nullptr;
-        if (!have_carry && a && !b) {  // (Some(a), None, None) => a.clone()
-            out.digits.push_back(*a);
-            continue;
-        }
-        if (!have_carry && !a && b) {  // (None, Some(b), None) => b.clone()
-            out.digits.push_back(*b);
-            continue;
-        }
-        // FheUint64::cast_from each present term, add (<= 3 terms, < 2^34: no wrap),
-        // carry = cast32(sum >> 32), digit = cast32(sum & 0xFFFFFFFF)
-        std::vector<Radix> terms;
-        if (a) terms.push_back(radix_resize(*a, 2 * kLimbBlocks));
-        if (b) terms.push_back(radix_resize(*b, 2 * kLimbBlocks));
-        if (have_carry) terms.push_back(radix_resize(carry, 2 * kLimbBlocks));
-        std::vector<const Radix*> tp;
-        for (auto& t : terms) tp.push_back(&t);
-        Radix sum = radix_sum(e, tp, 2 * kLimbBlocks);
-        carry = slice(sum, kLimbBlocks, kLimbBlocks);
-        have_carry = true;
-        out.digits.push_back(slice(sum, 0, kLimbBlocks));
-    }
-    if (have_carry) out.digits.push_back(carry);
+    if (la == 0) return B;
+    if (lb == 0) return A;
+    std::vector<const Radix*> pa, pb;
+    for (auto& d : A.digits) pa.push_back(&d);
+    for (auto& d : B.digits) pb.push_back(&d);
+    Radix wa = concat(pa), wb = concat(pb);
+    const uint32_t nb = (uint32_t)(max_len + 1) * kLimbBlocks;
+    Radix s = radix_sum(e, {&wa, &wb}, nb);
+    for (size_t i = 0; i <= max_len; ++i) out.digits.push_back(slice(s, (uint32_t)i * kLimbBlocks, kLimbBlocks));
     return out;
 }
 
-// impl Mul for BigUintFHE (src/biguint.rs:194-265)
+// impl Mul for BigUintFHE (src/biguint.rs:194-265).
+// kFast: the true product, one wide multiplication.
+// kCompat: the reference's limbs, including the carries its 96-bit windows drop (F7): step (i, j)
+// is R[idx..idx+3) += a_i * b_j mod 2^96 (mod 2^64 when idx + 2 = len).  Two exact shortcuts:
+//  * min(la, lb) = 1: before step k the limb above its window is still zero, so the window sum is
+//    < 2^65 and nothing is dropped (the last, 64-bit window holds the top of a product that fits
+//    la + lb limbs) -- the limbs are the true product;
+//  * otherwise steps whose windows do not overlap commute, so each step runs in the first
+//    dependency wave after every earlier overlapping step, and a wave's window adds share levels.
 BigUint biguint_mul(Engine& e, const BigUint& A, const BigUint& B, int mode) {
     const size_t la = A.digits.size(), lb = B.digits.size();
     BigUint out;
     if (la == 0 || lb == 0) return out;
     const size_t len = la + lb;
-    if (mode == kFast) {
+    if (mode == kFast || la == 1 || lb == 1) {
         std::vector<const Radix*> pa, pb;
         for (auto& d : A.digits) pa.push_back(&d);
         for (auto& d : B.digits) pb.push_back(&d);
@@ -90,18 +74,39 @@ BigUint biguint_mul(Engine& e, const BigUint& A, const BigUint& B, int mode) {
     for (size_t i = 0; i < la; ++i)
         for (size_t j = 0; j < lb; ++j) ops.push_back({&a64[i], &b64[j]});
     std::vector<Radix> prods = radix_mul_many(e, ops, 2 * kLimbBlocks);
-    // serial accumulation in the reference order (i outer, j inner), src/biguint.rs:214-254
+    // dependency waves of the accumulation steps (reference order: i outer, j inner)
+    struct Step {
+        size_t k, idx, wl;
+    };
+    std::vector<std::vector<Step>> waves;
+    std::vector<int> limb_wave(len, -1);  // last wave that wrote each limb
     for (size_t i = 0; i < la; ++i)
         for (size_t j = 0; j < lb; ++j) {
-            const size_t idx = i + j;
-            const size_t wl = (idx + 2 < len) ? 3 : 2;
-            std::vector<const Radix*> wlimbs;
-            for (size_t t = 0; t < wl; ++t) wlimbs.push_back(&R[idx + t]);
-            Radix W = concat(wlimbs);
-            const Radix& P = prods[i * lb + j];
-            Radix S = radix_sum(e, {&W, &P}, (uint32_t)wl * kLimbBlocks);
-            for (size_t t = 0; t < wl; ++t) R[idx + t] = slice(S, (uint32_t)t * kLimbBlocks, kLimbBlocks);
+            const size_t idx = i + j, wl = (idx + 2 < len) ? 3 : 2;
+            int wv = 0;
+            for (size_t t = 0; t < wl; ++t) wv = std::max(wv, limb_wave[idx + t] + 1);
+            for (size_t t = 0; t < wl; ++t) limb_wave[idx + t] = wv;
+            if ((size_t)wv >= waves.size()) waves.resize(wv + 1);
+            waves[wv].push_back({i * lb + j, idx, wl});
         }
+    for (auto& wave : waves) {
+        std::vector<Radix> W(wave.size());
+        std::vector<std::vector<const Radix*>> xs(wave.size());
+        std::vector<uint32_t> nbs(wave.size());
+        for (size_t s = 0; s < wave.size(); ++s) {
+            std::vector<const Radix*> wlimbs;
+            for (size_t t = 0; t < wave[s].wl; ++t) wlimbs.push_back(&R[wave[s].idx + t]);
+            W[s] = concat(wlimbs);
+        }
+        for (size_t s = 0; s < wave.size(); ++s) {
+            xs[s] = {&W[s], &prods[wave[s].k]};
+            nbs[s] = (uint32_t)wave[s].wl * kLimbBlocks;
+        }
+        std::vector<Radix> S = radix_sum_many(e, xs, nbs);
+        for (size_t s = 0; s < wave.size(); ++s)
+            for (size_t t = 0; t < wave[s].wl; ++t)
+                R[wave[s].idx + t] = slice(S[s], (uint32_t)t * kLimbBlocks, kLimbBlocks);
+    }
     out.digits = std::move(R);
     return out;
 }

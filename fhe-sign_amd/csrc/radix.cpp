@@ -544,6 +544,25 @@ Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblo
     return propagate_many(e, probs)[0];
 }
 
+std::vector<Radix> radix_sum_many(Engine& e, const std::vector<std::vector<const Radix*>>& xs,
+                                  const std::vector<uint32_t>& nblocks) {
+    std::vector<Radix> res(xs.size());
+    std::vector<ColProblem> probs;
+    std::vector<size_t> where;
+    for (size_t i = 0; i < xs.size(); ++i) {
+        ColProblem P;
+        P.nblocks = nblocks[i];
+        P.cols.resize(nblocks[i]);
+        for (const Radix* x : xs[i])
+            for (uint32_t k = 0; k < nblocks[i] && k < x->nblocks(); ++k) P.cols[k].push_back(x->blocks[k]);
+        probs.push_back(std::move(P));
+        where.push_back(i);
+    }
+    std::vector<Radix> outs = propagate_many(e, probs);
+    for (size_t i = 0; i < outs.size(); ++i) res[where[i]] = std::move(outs[i]);
+    return res;
+}
+
 Radix radix_sum(Engine& e, const std::vector<const Radix*>& xs, uint32_t nblocks) {
     std::vector<Blocks> cols(nblocks);
     for (const Radix* x : xs)

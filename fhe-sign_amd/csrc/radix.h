@@ -125,6 +125,9 @@ Radix radix_resize(const Radix& a, uint32_t nblocks);  // cast: truncate / zero-
 
 // Sum of several radix integers (wrapping at `nblocks`; carries propagated).  Used for every add.
 Radix radix_sum(Engine& e, const std::vector<const Radix*>& xs, uint32_t nblocks);
+// Independent sums advanced through shared levels (one launch pair per level for all of them).
+std::vector<Radix> radix_sum_many(Engine& e, const std::vector<std::vector<const Radix*>>& xs,
+                                  const std::vector<uint32_t>& nblocks);
 // Carry propagation of raw column blocks (each column may hold several blocks).
 Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks);
 // Wrapping product.
