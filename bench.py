@@ -28,7 +28,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds @1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6        # MI355X dense FP64 peak (matrix = vector on gfx950), spec
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "r1f_pmc_summary.json")  # tools/profile_round.sh
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "r1k_pmc_summary.json")  # tools/profile_round.sh
 FANOUT_MIN = 512  # levels with at least this many bootstraps are split over the GPUs (fan-out legs)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FLOPS_PER_CMUX = 4 * 51200 + 4 * 6144 + 32768   # 4 FFT-1024 (5 N log N), 4 twist/untwist, MAC
@@ -99,7 +99,7 @@ def pmc_traffic(batch):
     correction of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits included)"""
     try:
         d = json.load(open(PMC_SUMMARY))["pmc"][f"B={batch}"]
-        k = next(v for k, v in d.items() if "k_blind_rotate" in k and "wide" not in k)
+        k = next(v for k, v in d.items() if "k_blind_rotate" in k and "wide" not in k)  # quad / narrow
         return k["hbm_side_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
     except (OSError, KeyError, StopIteration, ValueError):
         return None, None
@@ -316,7 +316,7 @@ def main():
         "roofline": {
             "bound": "mfma",
             "compute_pipe": "fp64 VALU (FFT butterflies; no dense contraction on the path)",
-            "kernel": "k_blind_rotate",
+            "kernel": "k_blind_rotate_quad",
             "achieved": achieved,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",

@@ -53,7 +53,7 @@ struct fhe_ctx {
     double2* d_psi_quad = nullptr;  // [8][128]
     int br_kernel = FHE_BR_QUAD;    // throughput kernel for levels above wide_threshold
     // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU)
-    int wide_threshold = 640;  // crossover measured in profiles/r1/latency_sweep_r1e.txt
+    int wide_threshold = 256;  // wide up to one ciphertext per CU; quad above (profiles/r1/latency_sweep_r1j.txt)
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;

@@ -106,7 +106,7 @@ def test_wide_and_narrow_kernels_bit_identical(env):
         ctx.set_wide_threshold(1 << 30)
         wide = ctx.pbs(cts, lut_ids)
     finally:
-        ctx.set_wide_threshold(640)
+        ctx.set_wide_threshold(256)
         ctx.set_br_kernel(1)
     assert np.array_equal(narrow, wide)
     assert np.array_equal(quad, wide)
