@@ -170,7 +170,7 @@ int fhe_ctx::pbs_device(const uint64_t* d_in, size_t count, const uint32_t* d_lu
         return FHE_ERR_INVALID;
     }
     if (timing) FHE_HIP_CHECK(hipEventRecord(ev[0], stream));
-    FHE_HIP_CHECK(launch_keyswitch(d_in, (int)count, d_ksk, d_ms, ms_stride, (int)p.n, stream));
+    FHE_HIP_CHECK(keyswitch(d_in, nullptr, count));
     if (timing) FHE_HIP_CHECK(hipEventRecord(ev[1], stream));
     FHE_HIP_CHECK(blind_rotate(nullptr, d_lut, d_out, count));
     if (timing) {
@@ -180,6 +180,28 @@ int fhe_ctx::pbs_device(const uint64_t* d_in, size_t count, const uint32_t* d_lu
         FHE_HIP_CHECK(hipEventElapsedTime(&last_br_ms, ev[1], ev[2]));
     }
     return FHE_OK;
+}
+
+int fhe_ctx::ensure_ks(size_t count) {
+    if (count <= ks_cap) return FHE_OK;
+    FHE_HIP_CHECK(hipSetDevice(device));
+    FHE_HIP_CHECK(hipStreamSynchronize(stream));  // previous levels may still read them
+    if (d_ks_digits) FHE_HIP_CHECK(hipFree(d_ks_digits));
+    if (d_ks_body) FHE_HIP_CHECK(hipFree(d_ks_body));
+    ks_cap = std::max<size_t>(count, 1024);
+    FHE_HIP_CHECK(hipMalloc(&d_ks_digits, fhe::ks_digits_bytes((int)ks_cap)));
+    FHE_HIP_CHECK(hipMalloc(&d_ks_body, ks_cap * 8));
+    return FHE_OK;
+}
+
+hipError_t fhe_ctx::keyswitch(const uint64_t* in, const fhe::PbsDesc* desc, size_t count) {
+    if (ks_kernel == FHE_KS_MFMA) {
+        if (ensure_ks(count) != FHE_OK) return hipErrorOutOfMemory;
+        return launch_keyswitch_mfma(in, desc, (int)count, d_ksk_planes, d_ks_digits, d_ks_body, d_ms, ms_stride,
+                                     (int)p.n, stream);
+    }
+    if (desc) return launch_keyswitch_desc(desc, (int)count, d_ksk, d_ms, ms_stride, (int)p.n, stream);
+    return launch_keyswitch(in, (int)count, d_ksk, d_ms, ms_stride, (int)p.n, stream);
 }
 
 hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_idx, uint64_t* out, size_t count) {
@@ -323,7 +345,7 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     delete c->engine;
     c->engine = nullptr;
     c->release_comm();
-    void* ptrs[] = {c->d_ksk, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
+    void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
                     c->d_psi_quad, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -342,6 +364,8 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
         FHE_HIP_CHECK(hipFree(c->d_ksk));
         FHE_HIP_CHECK(hipFree(c->d_bsk));
         FHE_HIP_CHECK(hipFree(c->d_bsk_quad));
+        FHE_HIP_CHECK(hipFree(c->d_ksk_planes));
+        c->d_ksk_planes = nullptr;
         c->d_ksk = nullptr;
         c->d_bsk = nullptr;
         c->d_bsk_quad = nullptr;
@@ -349,6 +373,8 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     }
     FHE_HIP_CHECK(hipMalloc(&c->d_ksk, sk->ksk.size() * 8));
     FHE_HIP_CHECK(hipMemcpyAsync(c->d_ksk, sk->ksk.data(), sk->ksk.size() * 8, hipMemcpyHostToDevice, c->stream));
+    FHE_HIP_CHECK(hipMalloc(&c->d_ksk_planes, fhe::ks_planes_bytes((int)p.n)));
+    FHE_HIP_CHECK(launch_ksk_to_planes(c->d_ksk, (int)p.n, c->d_ksk_planes, c->stream));
     const int npoly = (int)(p.n * 4);
     uint64_t* d_std = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d_std, sk->bsk.size() * 8));
@@ -467,6 +493,12 @@ int fhe_memcpy_d2h(fhe_ctx* c, void* dst, const void* src, size_t bytes) {
     FHE_HIP_CHECK(hipSetDevice(c->device));
     FHE_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return FHE_OK;
+}
+
+int fhe_ctx_set_ks_kernel(fhe_ctx* c, int kind) {
+    if (!c || (kind != FHE_KS_VALU && kind != FHE_KS_MFMA)) return FHE_ERR_INVALID;
+    c->ks_kernel = kind;
     return FHE_OK;
 }
 

@@ -52,6 +52,11 @@ struct fhe_ctx {
     double2* d_tw_quad = nullptr;   // W[0..512)
     double2* d_psi_quad = nullptr;  // [8][128]
     int br_kernel = FHE_BR_QUAD;    // throughput kernel for levels above wide_threshold
+    int8_t* d_ksk_planes = nullptr; // KSK as balanced signed-byte planes (ks_mfma.hip)
+    int ks_kernel = FHE_KS_MFMA;
+    int8_t* d_ks_digits = nullptr;  // keyswitch digits workspace
+    uint64_t* d_ks_body = nullptr;
+    size_t ks_cap = 0;              // ciphertexts
     // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU)
     int wide_threshold = 256;  // wide up to one ciphertext per CU; quad above (profiles/r1/latency_sweep_r1j.txt)
     // LUT registry: table contents -> id, device array of accumulator polynomials
@@ -91,6 +96,9 @@ struct fhe_ctx {
     void release_comm();
 
     int ensure_ms(size_t count);
+    int ensure_ks(size_t count);
+    // keyswitch of `count` inputs (contiguous big LWE in `in`, or descriptors) into d_ms
+    hipError_t keyswitch(const uint64_t* in, const fhe::PbsDesc* desc, size_t count);
     int ensure_stage(size_t count);
     int sync_luts();
     int register_lut(const uint32_t* table, uint32_t* id);

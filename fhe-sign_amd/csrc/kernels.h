@@ -16,6 +16,27 @@ struct PbsDesc {
     uint64_t* dst;
 };
 
+// Keyswitch input coefficient j (2048 = body) of ciphertext ct: a contiguous batch of big LWE
+// or the linear combination a descriptor describes.
+template <bool DESC>
+__device__ __forceinline__ uint64_t ks_input(const uint64_t* __restrict__ in, const PbsDesc* __restrict__ desc, int ct,
+                                             int j) {
+    if (!DESC) return in[(size_t)ct * 2049 + j];
+    const PbsDesc& d = desc[ct];
+    uint64_t a = (j == 2048) ? d.cst : 0ull;
+    for (uint32_t t = 0; t < d.nterms; ++t) a += (uint64_t)(int64_t)d.coef[t] * d.src[t][j];
+    return a;
+}
+
+// ---- keyswitch on the matrix cores (ks_mfma.hip): exact int8 contraction against byte planes
+int ks_plane_tiles(int n);
+size_t ks_planes_bytes(int n);
+size_t ks_digits_bytes(int count);
+hipError_t launch_ksk_to_planes(const uint64_t* ksk, int n, int8_t* planes, hipStream_t s);
+// in (contiguous) or desc (linear combinations) -> small LWE (u64, stride) in `small`
+hipError_t launch_keyswitch_mfma(const uint64_t* in, const PbsDesc* desc, int count, const int8_t* planes,
+                                 int8_t* digits, uint64_t* body, uint64_t* small, int stride, int n, hipStream_t s);
+
 // ---- PBS pipeline (pbs_kernels.hip)
 hipError_t launch_keyswitch(const uint64_t* in, int count, const uint64_t* ksk, uint64_t* small,
                             int ks_stride, int n, hipStream_t s);

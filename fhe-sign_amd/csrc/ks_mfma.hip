@@ -1,0 +1,148 @@
+// ks_mfma.hip -- LWE keyswitch as an int8 matrix-core contraction.
+//
+// Keyswitch (oracle/tfhe_oracle.c:fho_keyswitch): out[t] = [t = n] body - sum_{j,l} d[j,l] KSK[j,l][t]
+// mod 2^64, with d the rounded base-2^3 x 5 balanced digits (|d| <= 4) of the 2048 mask words.
+// Writing every KSK word as balanced signed bytes, KSK = sum_b 256^b K_b (K_b in [-128, 128)),
+// turns it into 8 int8 GEMMs  S_b = D (count x 10240) . K_b (10240 x (n+1))  whose int32 sums are
+// exact (|S_b| <= 4 * 128 * 10240 < 2^23), recombined as sum_b S_b 256^b mod 2^64 -- bit-identical
+// to the u64 multiply-accumulate.  v_mfma_i32_16x16x64_i8: lane l holds row/column l & 15 and the
+// 16 bytes k = 16 (l >> 4) + j of the k-tile (tools/mfma_i8_probe.hip; any k map works if A and B
+// share it); C/D: column l & 15, row 4 (l >> 4) + r.
+//
+// Layouts (k = level * 2048 + j, level-major; 160 k-tiles of 64):
+//   planes  int8 [8 planes][TT col tiles][160][64 lanes][16]   (one 1 KiB fragment per (b, tile, kt))
+//   digits  int8 [ct tiles of 16][160][64 lanes][16]            (one 1 KiB fragment per (tile, kt))
+#include "device_math.h"
+#include "kernels.h"
+
+namespace fhe {
+
+namespace {
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int KS_K = 2048 * 5;  // contraction length
+constexpr int KS_KT = KS_K / 64;
+
+FHE_DEV size_t frag_off(size_t tile, int kt, int lane) { return ((tile * KS_KT + kt) * 64 + lane) * 16; }
+
+// element (row r of a 16-row tile, contraction index k) -> byte offset in the fragment layout
+FHE_DEV size_t elem_off(size_t tile, int r, int k) {
+    return frag_off(tile, k >> 6, (r & 15) + 16 * ((k & 63) >> 4)) + (k & 15);
+}
+}  // namespace
+
+// KSK u64 [2048][5][n+1] -> balanced byte planes (once, at set_server_key).  One thread per
+// (column tile, k-tile, lane): 16 consecutive k of one column, all 8 planes.
+__global__ __launch_bounds__(64) void k_ksk_to_planes(const uint64_t* __restrict__ ksk, int n, int tiles,
+                                                      int8_t* __restrict__ planes) {
+    const int tt = blockIdx.x / KS_KT, kt = blockIdx.x % KS_KT, lane = threadIdx.x;
+    const int t = 16 * tt + (lane & 15);
+    int8_t by[8][16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+        const int k = 64 * kt + 16 * (lane >> 4) + jj;
+        const int lvl = k >> 11, j = k & 2047;
+        uint64_t v = t <= n ? ksk[((size_t)j * 5 + lvl) * (n + 1) + t] : 0ull;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            int s = (int)(v & 255u);
+            if (s >= 128) s -= 256;
+            by[b][jj] = (int8_t)s;
+            v = (v - (uint64_t)(int64_t)s) >> 8;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        int8_t* o = planes + (size_t)b * tiles * KS_KT * 1024 + frag_off(tt, kt, lane);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) o[jj] = by[b][jj];
+    }
+}
+
+// Digits of one ciphertext per workgroup (input = a contiguous block or a PbsDesc linear
+// combination), staged in LDS and stored as 16-byte fragment rows; body word kept aside.
+template <bool DESC>
+__global__ __launch_bounds__(256) void k_ks_digits(const uint64_t* __restrict__ in, const PbsDesc* __restrict__ desc,
+                                                   int8_t* __restrict__ digits, uint64_t* __restrict__ body) {
+    __shared__ int8_t sd[KS_K];
+    const int ct = blockIdx.x;
+    for (int j = threadIdx.x; j < 2048; j += 256) {
+        const uint64_t a = ks_input<DESC>(in, desc, ct, j);
+        uint64_t v = (((a >> (63 - 15)) + 1) >> 1) & 0x7fffull;  // round to the top 15 bits
+#pragma unroll
+        for (int l = 4; l >= 0; --l) {
+            int d = (int)(v & 7u);
+            v >>= 3;
+            if (d >= 4) {
+                d -= 8;
+                v += 1;
+            }
+            sd[l * 2048 + j] = (int8_t)d;
+        }
+    }
+    if (threadIdx.x == 0) body[ct] = ks_input<DESC>(in, desc, ct, 2048);
+    __syncthreads();
+    // 640 chunks of 16 digits: (k-tile, lane group)
+    for (int c = threadIdx.x; c < KS_K / 16; c += 256) {
+        const int k0 = 16 * c;
+        const v4i v = *reinterpret_cast<const v4i*>(sd + k0);
+        *reinterpret_cast<v4i*>(digits + elem_off(ct >> 4, ct & 15, k0)) = v;
+    }
+}
+
+// out[ct][t] for a 64-ciphertext x 16-column tile: wave w owns ciphertext tile 4 blockIdx.x + w.
+__global__ __launch_bounds__(256) void k_ks_mfma(const int8_t* __restrict__ digits, const uint64_t* __restrict__ body,
+                                                 const int8_t* __restrict__ planes, int tiles, int count, int n,
+                                                 uint64_t* __restrict__ small, int stride) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const size_t ctile = (size_t)blockIdx.x * 4 + w;
+    const int tt = blockIdx.y;
+    if ((int)(ctile * 16) >= count) return;
+    const v4i* A = reinterpret_cast<const v4i*>(digits + frag_off(ctile, 0, lane));
+    const v4i* B = reinterpret_cast<const v4i*>(planes + frag_off(tt, 0, lane));
+    const size_t plane = (size_t)tiles * KS_KT * 64;  // v4i per plane
+    v4i acc[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[b] = v4i{0, 0, 0, 0};
+#pragma unroll 2
+    for (int kt = 0; kt < KS_KT; ++kt) {
+        const v4i a = A[kt * 64];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, B[b * plane + kt * 64], acc[b], 0, 0, 0);
+    }
+    const int t = 16 * tt + (lane & 15);
+    if (t > n) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int ct = (int)ctile * 16 + 4 * (lane >> 4) + r;
+        if (ct >= count) continue;
+        uint64_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) v += (uint64_t)(int64_t)acc[b][r] << (8 * b);
+        small[(size_t)ct * stride + t] = (t == n ? body[ct] : 0ull) - v;
+    }
+}
+
+int ks_plane_tiles(int n) { return (n + 1 + 15) / 16; }
+size_t ks_planes_bytes(int n) { return (size_t)8 * ks_plane_tiles(n) * KS_KT * 1024; }
+size_t ks_digits_bytes(int count) { return (size_t)((count + 63) / 64) * 4 * KS_KT * 1024; }
+
+hipError_t launch_ksk_to_planes(const uint64_t* ksk, int n, int8_t* planes, hipStream_t s) {
+    const int tiles = ks_plane_tiles(n);
+    hipLaunchKernelGGL(k_ksk_to_planes, dim3(tiles * KS_KT), dim3(64), 0, s, ksk, n, tiles, planes);
+    return hipGetLastError();
+}
+
+hipError_t launch_keyswitch_mfma(const uint64_t* in, const PbsDesc* desc, int count, const int8_t* planes,
+                                 int8_t* digits, uint64_t* body, uint64_t* small, int stride, int n, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    if (desc)
+        hipLaunchKernelGGL(k_ks_digits<true>, dim3(count), dim3(256), 0, s, nullptr, desc, digits, body);
+    else
+        hipLaunchKernelGGL(k_ks_digits<false>, dim3(count), dim3(256), 0, s, in, nullptr, digits, body);
+    const int tiles = ks_plane_tiles(n);
+    hipLaunchKernelGGL(k_ks_mfma, dim3((count + 63) / 64, tiles), dim3(256), 0, s, digits, body, planes, tiles, count, n,
+                       small, stride);
+    return hipGetLastError();
+}
+
+}  // namespace fhe

@@ -24,16 +24,6 @@ constexpr int KS_J = 16;   // input coefficients per LDS chunk
 constexpr int KS_LVL = 5;  // gadget levels (base 2^3)
 constexpr int KS_BL = 3;
 
-// Input coefficient j of ciphertext ct: either a contiguous batch or a linear combination.
-template <bool DESC>
-FHE_DEV uint64_t ks_input(const uint64_t* __restrict__ in, const PbsDesc* __restrict__ desc, int ct, int j) {
-    if (!DESC) return in[(size_t)ct * 2049 + j];
-    const PbsDesc& d = desc[ct];
-    uint64_t a = (j == 2048) ? d.cst : 0ull;
-    for (uint32_t t = 0; t < d.nterms; ++t) a += (uint64_t)(int64_t)d.coef[t] * d.src[t][j];
-    return a;
-}
-
 // The 2048 x 5 gadget rows can be split over gridDim.z workgroups (small batches: enough
 // workgroups to cover the chip); partial sums then meet through 64-bit atomic adds, which are
 // exact and order-independent mod 2^64, so results stay bit-identical.  Output: the small LWE

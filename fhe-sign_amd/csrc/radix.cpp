@@ -212,9 +212,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     hip_check(hipEventRecord(desc_ev_[desc_turn_], ctx_->stream), "desc event");
     auto pbs = [&](size_t lo, size_t hi) {
         if (hi <= lo) return;
-        hip_check(launch_keyswitch_desc(dev + lo, (int)(hi - lo), ctx_->d_ksk, ctx_->d_ms, ctx_->ms_stride, (int)p.n,
-                                        ctx_->stream),
-                  "keyswitch");
+        hip_check(ctx_->keyswitch(nullptr, dev + lo, hi - lo), "keyswitch");
         hip_check(ctx_->blind_rotate(dev + lo, nullptr, nullptr, hi - lo), "blind rotate");
     };
     if (!split) {

@@ -160,6 +160,10 @@ class Context:
         """0 = 2-wave throughput kernel, 1 = 4-wave (default); identical results"""
         check(load().fhe_ctx_set_br_kernel(self._h, int(kind)))
 
+    def set_ks_kernel(self, kind: int) -> None:
+        """0 = 64-bit VALU keyswitch, 1 = int8 matrix-core keyswitch (default); identical results"""
+        check(load().fhe_ctx_set_ks_kernel(self._h, int(kind)))
+
     def set_wide_threshold(self, threshold: int) -> None:
         check(load().fhe_ctx_set_wide_threshold(self._h, int(threshold)))
 

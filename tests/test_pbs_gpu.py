@@ -112,3 +112,26 @@ def test_wide_and_narrow_kernels_bit_identical(env):
     assert np.array_equal(quad, wide)
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(wide[:6], ref)
+
+
+def test_keyswitch_kernels_identical(env):
+    """The int8 matrix-core keyswitch (ks_mfma.hip: byte-plane contraction) and the 64-bit VALU
+    keyswitch are both exact: the bootstraps they feed give identical words, equal to the oracle.
+    Batches of 1, 16, 37 (ragged tiles) and 130."""
+    _, _, ok, ctx = env
+    tables = _luts()
+    ids = [ctx.lut(t) for t in tables]
+    r = ok.rng(4242)
+    for count in (1, 16, 37, 130):
+        cts = np.stack([ok.encrypt(r, i % 16) for i in range(count)])
+        lut_ids = np.array([ids[i % len(ids)] for i in range(count)], np.uint32)
+        try:
+            ctx.set_ks_kernel(0)
+            valu = ctx.pbs(cts, lut_ids)
+            ctx.set_ks_kernel(1)
+            mfma = ctx.pbs(cts, lut_ids)
+        finally:
+            ctx.set_ks_kernel(1)
+        assert np.array_equal(valu, mfma), count
+    ref = ok.pbs_batch(cts[:4], np.stack([ok.make_lut(t) for t in tables]), np.arange(4, dtype=np.uint32) % len(tables))
+    assert np.array_equal(mfma[:4], ref)
