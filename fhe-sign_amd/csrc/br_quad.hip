@@ -86,7 +86,8 @@ FHE_DEV void q_stage9(cplx (&x)[8], uint32_t signbit) {
 }
 }  // namespace
 
-// One workgroup (4 waves) per ciphertext.  W = twiddles W[0..512), ps = [8][128] twist factors.
+// One workgroup (4 waves) per ciphertext.  W = twiddles W[0..512), ps = [2][8][128]: twist factors
+// psi, then the untwist factors (psi.x 2^-10, -psi.y 2^-10) -- exact scalings, as the oracle's.
 __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
                                                               const uint32_t* __restrict__ lut_idx,
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         for (int r = 0; r < 8; ++r) x[r] = reg[bA + fq(128 * r)];
         __syncthreads();  // every B->A read done before the next rotation overwrites the region
 #pragma unroll
-        for (int r = 0; r < 8; ++r) pst[r] = P[128 * r];
+        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];  // untwist factors conj(psi) 2^-10
         q_dit<0>(x, s_w, tpos(4 * t));
         q_dit<1>(x, s_w, tpos(2 * t));
         q_dit<2>(x, s_w, tpos(t));
@@ -244,8 +245,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         // ---- untwist, round, accumulate (point j = 128 r + t -> coefficients j, j + 1024)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const cplx u = make_double2(pst[r].x * 0.0009765625, -pst[r].y * 0.0009765625);
-            const cplx y = cmul(x[r], u);
+            const cplx y = cmul(x[r], pst[r]);
             acc[r] += f64_to_torus(y.x);
             acc[r + 8] += f64_to_torus(y.y);
         }

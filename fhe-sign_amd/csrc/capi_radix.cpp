@@ -230,6 +230,27 @@ int fhe_radix_lt(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix**
     if (rc == FHE_OK) (*out)->bits = 2;
     return rc;
 }
+int fhe_radix_divrem(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** q, fhe_radix** r) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !b || (!q && !r)) return FHE_ERR_INVALID;
+    if (a->bits != b->bits) {
+        set_error("operands must have the same bit width");
+        return FHE_ERR_INVALID;
+    }
+    return guarded([&] {
+        auto qr = radix_divrem(*c->engine, a->r, b->r);
+        if (q) *q = wrap(std::move(qr.first), a->bits);
+        if (r) *r = wrap(std::move(qr.second), a->bits);
+        return FHE_OK;
+    });
+}
+int fhe_radix_div(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    return fhe_radix_divrem(c, a, b, out, nullptr);
+}
+int fhe_radix_rem(fhe_ctx* c, const fhe_radix* a, const fhe_radix* b, fhe_radix** out) {
+    return fhe_radix_divrem(c, a, b, nullptr, out);
+}
 int fhe_radix_shr(fhe_ctx* c, const fhe_radix* a, const fhe_radix* amount, fhe_radix** out) {
     int rc = need_engine(c);
     if (rc) return rc;

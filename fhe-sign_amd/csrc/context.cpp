@@ -52,9 +52,13 @@ void quad_tables(const std::vector<double2>& W, const std::vector<double2>& psi,
                  std::vector<double2>* ps) {
     // br_quad.hip: twiddles W[0..512) (copied into LDS per workgroup), twist psi[128 r + t] per thread
     tw->assign(W.begin(), W.begin() + 512);
-    ps->assign(8 * 128, make_double2(0.0, 0.0));
+    ps->assign(2 * 8 * 128, make_double2(0.0, 0.0));
     for (int t = 0; t < 128; ++t)
-        for (int r = 0; r < 8; ++r) (*ps)[r * 128 + t] = psi[128 * r + t];
+        for (int r = 0; r < 8; ++r) {
+            const double2 q = psi[128 * r + t];
+            (*ps)[r * 128 + t] = q;
+            (*ps)[1024 + r * 128 + t] = make_double2(q.x * 0.0009765625, -q.y * 0.0009765625);
+        }
 }
 
 void wide_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,

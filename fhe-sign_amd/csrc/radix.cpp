@@ -463,8 +463,9 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
     }
 }
 
-// Carry-propagate compressed columns (each column sum v_k <= 6, <= 7 at k = 0).
-static std::vector<Radix> propagate_many(Engine& e, std::vector<ColProblem>& probs) {
+// Carries of compressed columns (each column sum v_k <= 6, <= 7 at k = 0): cur[p][k] = carry out of
+// position k, k < nblocks - 1.  A problem with one extra empty top column yields its carry out.
+static std::vector<Blocks> propagate_carries(Engine& e, std::vector<ColProblem>& probs) {
     std::vector<ColProblem*> ptrs;
     for (auto& p : probs) {
         p.cols.resize(p.nblocks);
@@ -513,18 +514,25 @@ static std::vector<Radix> propagate_many(Engine& e, std::vector<ColProblem>& pro
         Blocks outs = e.run(items);
         for (size_t i = 0; i < outs.size(); ++i) cur[refs[i].pi][refs[i].k] = outs[i];
     }
+    return cur;
+}
+
+// out_k = (v_k + c_{k-1}) mod 4 for k < upto (the final level of a carry propagation)
+static void final_items(const ColProblem& P, const Blocks& carries, uint32_t upto, std::vector<PbsItem>& items) {
+    for (uint32_t k = 0; k < upto; ++k) {
+        PbsItem it;
+        for (auto& b : P.cols[k]) it.terms.push_back({b, 1});
+        if (k > 0) it.terms.push_back({carries[k - 1], 1});
+        it.table = LUT_MOD4();
+        items.push_back(it);
+    }
+}
+
+static std::vector<Radix> propagate_many(Engine& e, std::vector<ColProblem>& probs) {
+    std::vector<Blocks> cur = propagate_carries(e, probs);
     // final: out_k = (v_k + c_{k-1}) mod 4
     std::vector<PbsItem> items;
-    for (size_t pi = 0; pi < probs.size(); ++pi) {
-        ColProblem& P = probs[pi];
-        for (uint32_t k = 0; k < P.nblocks; ++k) {
-            PbsItem it;
-            for (auto& b : P.cols[k]) it.terms.push_back({b, 1});
-            if (k > 0) it.terms.push_back({cur[pi][k - 1], 1});
-            it.table = LUT_MOD4();
-            items.push_back(it);
-        }
-    }
+    for (size_t pi = 0; pi < probs.size(); ++pi) final_items(probs[pi], cur[pi], probs[pi].nblocks, items);
     Blocks outs = e.run(items);
     std::vector<Radix> res(probs.size());
     size_t o = 0;
@@ -991,6 +999,87 @@ Radix radix_clean(Engine& e, const Radix& a) {
     Radix r;
     r.blocks = e.run(items);
     return r;
+}
+
+// Encrypted / encrypted: radix-4 restoring division, one quotient block (2 bits) per step from the
+// top.  With r < d kept exact in n + 1 blocks:  r4 = 4 r + a_i,  three subtractions r4 - c d
+// (c = 1..3, complements of d, 2d, 3d prepared once) share their levels and give the borrow bits
+// ge_c = [r4 >= c d];  q_i = ge_1 + ge_2 + ge_3 (one bootstrap, in the subtractions' final level),
+// r = the candidate picked by q_i (half-selects f(4 q_i + cand), noise 16 + 1) and cleaned.
+// d = 0 gives q = 2^bits - 1 and r = a (every ge_c = 1), tfhe's convention.  ~12 levels per block.
+std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) {
+    const uint32_t n = a.nblocks(), W = n + 1;
+    Radix d1 = radix_resize(d, W);
+    Radix d2 = radix_sum(e, {&d1, &d1}, W);
+    Radix d3 = radix_sum(e, {&d2, &d1}, W);
+    std::vector<Blocks> nd(3);
+    {
+        std::vector<PbsItem> items;
+        for (const Radix* dc : {&d1, &d2, &d3})
+            for (uint32_t k = 0; k < W; ++k) {
+                PbsItem it;
+                it.terms = {{dc->blocks[k], -1}};
+                it.cst = 3;
+                it.table = lut1([](uint32_t v) { return v & 3; });
+                items.push_back(it);
+            }
+        Blocks o = e.run(items);
+        for (int c = 0; c < 3; ++c) nd[c].assign(o.begin() + c * W, o.begin() + (c + 1) * W);
+    }
+    static const auto LUT_ID = lut1([](uint32_t v) { return v & 3; });
+    std::vector<std::vector<uint32_t>> sel(4);
+    for (uint32_t c = 0; c < 4; ++c) sel[c] = lut1([c](uint32_t v) { return (v >> 2) == c ? v & 3 : 0u; });
+    Blocks r(W, Block::make_trivial(0));
+    Radix q;
+    q.blocks.resize(n);
+    for (int i = (int)n - 1; i >= 0; --i) {
+        Blocks r4(W);
+        r4[0] = a.blocks[i];
+        for (uint32_t k = 1; k < W; ++k) r4[k] = r[k - 1];  // r < d < 4^n: its top block is 0
+        std::vector<ColProblem> probs(3);
+        for (int c = 0; c < 3; ++c) {
+            probs[c].nblocks = W + 1;  // empty top column: the carry out of position W - 1 is ge_c
+            probs[c].cols.assign(W + 1, {});
+            for (uint32_t k = 0; k < W; ++k) probs[c].cols[k] = {r4[k], nd[c][k]};
+            probs[c].cols[0].push_back(Block::make_trivial(1));
+        }
+        std::vector<Blocks> cur = propagate_carries(e, probs);
+        std::vector<PbsItem> items;
+        for (int c = 0; c < 3; ++c) final_items(probs[c], cur[c], W, items);
+        {
+            PbsItem qi;
+            qi.terms = {{cur[0][W - 1], 1}, {cur[1][W - 1], 1}, {cur[2][W - 1], 1}};
+            qi.table = LUT_ID;
+            items.push_back(qi);
+        }
+        Blocks o = e.run(items);
+        const Block qb = o[3 * W];
+        q.blocks[i] = qb;
+        // r_k = sum over c of [q == c] cand_c[k], exactly one term nonzero
+        std::vector<PbsItem> hs;
+        for (uint32_t k = 0; k < W - 1; ++k)
+            for (uint32_t c = 0; c < 4; ++c) {
+                PbsItem it;
+                it.terms = {{qb, 4}, {c == 0 ? r4[k] : o[(c - 1) * W + k], 1}};
+                it.table = sel[c];
+                hs.push_back(it);
+            }
+        Blocks h = e.run(hs);
+        std::vector<PbsItem> fin;
+        for (uint32_t k = 0; k < W - 1; ++k) {
+            PbsItem it;
+            for (uint32_t c = 0; c < 4; ++c) it.terms.push_back({h[4 * k + c], 1});
+            it.table = LUT_MOD4();
+            fin.push_back(it);
+        }
+        Blocks rn = e.run(fin);
+        for (uint32_t k = 0; k < W - 1; ++k) {
+            r[k] = rn[k];
+            r[k].degree = std::min<uint32_t>(r[k].degree, 3);
+        }
+        r[W - 1] = Block::make_trivial(0);
+    }
+    return {q, radix_resize(Radix{r}, n)};
 }
 
 Radix radix_scalar_rem(Engine& e, const Radix& a, const BigConst& d) {

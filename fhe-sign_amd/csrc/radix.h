@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <functional>
 #include <memory>
+#include <utility>
 #include <vector>
 
 #include "context.h"
@@ -149,6 +150,8 @@ inline Radix radix_scalar_mul(Engine& e, const Radix& a, uint64_t s) { return ra
 inline Radix radix_scalar_div(Engine& e, const Radix& a, uint64_t d) { return radix_scalar_div(e, a, BigConst{d}); }
 inline Radix radix_scalar_rem(Engine& e, const Radix& a, uint64_t d) { return radix_scalar_rem(e, a, BigConst{d}); }
 Radix radix_sub(Engine& e, const Radix& a, const Radix& b);
+// floor(a / d), a mod d for an encrypted divisor (d = 0: quotient all ones, remainder a)
+std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d);
 // encrypted boolean (one block, value 0/1)
 Block radix_lt(Engine& e, const Radix& a, const Radix& b);
 Radix radix_select(Engine& e, const Block& cond, const Radix& if_true, const Radix& if_false);

@@ -76,6 +76,9 @@ _SIGNATURES = [
     ("fhe_radix_scalar_mul", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_div", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_rem", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_div", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_rem", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_divrem", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_and_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_add_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_mul_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),

@@ -147,13 +147,23 @@ class FheUint:
             return self._bin("fhe_radix_shl", o)
         return self._scalar("fhe_radix_scalar_shl", int(o) % 2**32)
 
-    def __floordiv__(self, d: int):
+    def __floordiv__(self, d):
+        if isinstance(d, FheUint):
+            return self._bin("fhe_radix_div", d)
         return self._scalar_any("fhe_radix_scalar_div", d, wrap=False)
 
     __truediv__ = __floordiv__  # tfhe's `&a / 5` on FheUint is integer division (src/perf_test.rs:54)
 
-    def __mod__(self, d: int):
+    def __mod__(self, d):
+        if isinstance(d, FheUint):
+            return self._bin("fhe_radix_rem", d)
         return self._scalar_any("fhe_radix_scalar_rem", d, wrap=False)
+
+    def div_rem(self, d):
+        """(self // d, self % d) for an encrypted divisor, one pass"""
+        q, r = C.c_void_p(), C.c_void_p()
+        check(load().fhe_radix_divrem(_ctx().handle, self._h, d._h, C.byref(q), C.byref(r)))
+        return self._wrap(q, self.bits), self._wrap(r, self.bits)
 
     def min(self, o):
         return self._bin("fhe_radix_min", o)

@@ -177,6 +177,12 @@ int fhe_radix_scalar_add_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t*
 int fhe_radix_scalar_mul_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out);
 int fhe_radix_scalar_div_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* d, size_t nwords, fhe_radix** out);
 int fhe_radix_scalar_rem_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* d, size_t nwords, fhe_radix** out);
+/* FheUint / FheUint, FheUint % FheUint (encrypted divisor; SURVEY 8d config 3 stretch, 8f rank 1).
+ * Division by an encrypted zero yields quotient 2^num_bits - 1 and remainder a (tfhe's convention).
+ * fhe_radix_divrem returns both (either output may be NULL). */
+int fhe_radix_div(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+int fhe_radix_rem(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
+int fhe_radix_divrem(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** q, fhe_radix** r);
 /* FheUint::cast_from / cast_into (src/biguint.rs:110,116,221; src/perf_test.rs:40) */
 int fhe_radix_cast(fhe_ctx* ctx, const fhe_radix* a, uint32_t num_bits, fhe_radix** out);
 /* FheUint::min (src/perf_test.rs:44), max, lt (encrypted bool returned as a 2-bit radix) */

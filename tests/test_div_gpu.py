@@ -4,12 +4,14 @@
 Parity bar: decrypted quotient / remainder equal floor division of the plaintexts (tfhe scalar div
 semantics, 1344 / 5 = 268 at src/perf_test.rs:75), on seeded random 256-bit dividends with the
 divisors SURVEY.md 8d names (5, a random u32, a random 128-bit value) and the edge cases (1, powers
-of two, divisor wider than the dividend)."""
+of two, divisor wider than the dividend).  Encrypted divisors (FheUint / FheUint, SURVEY.md 8f
+rank 1): same floor-division bar, and tfhe's division-by-zero convention (quotient all ones,
+remainder = dividend)."""
 import random
 
 import pytest
 
-from fhe_sign import Context, FheUint32, FheUint128, FheUint256, generate_keys, set_server_key
+from fhe_sign import Context, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, generate_keys, set_server_key
 
 pytestmark = pytest.mark.gpu
 M256 = (1 << 256) - 1
@@ -67,3 +69,39 @@ def test_wide_scalar_ops(keys):
     assert (A & s).decrypt(ck) == a & s
     assert (A + s).decrypt(ck) == (a + s) & m
     assert (A * s).decrypt(ck) == (a * s) & m
+
+
+@pytest.mark.parametrize("bits,cls", [(8, FheUint8), (32, FheUint32)])
+def test_div_by_encrypted_random(keys, bits, cls):
+    ck, _ = keys
+    rng = random.Random(0xD1F + bits)
+    m = (1 << bits) - 1
+    cases = [(rng.getrandbits(bits), rng.getrandbits(rng.randint(1, bits)) or 1) for _ in range(3)]
+    cases += [(rng.getrandbits(bits) >> 3, m), (m, 1), (m, m), (0, 7), (5, 9)]  # b > a, a = b, a = 0
+    for a, b in cases:
+        q, r = cls.try_encrypt(a, ck).div_rem(cls.try_encrypt(b, ck))
+        assert (q.decrypt(ck), r.decrypt(ck)) == (a // b, a % b), (a, b)
+
+
+def test_div_by_encrypted_zero(keys):
+    ck, _ = keys
+    A, Z = FheUint32.try_encrypt(123456789, ck), FheUint32.try_encrypt(0, ck)
+    assert (A / Z).decrypt(ck) == (1 << 32) - 1
+    assert (A % Z).decrypt(ck) == 123456789
+
+
+def test_div_by_encrypted_operators(keys):
+    ck, _ = keys
+    rng = random.Random(64)
+    a, b = rng.getrandbits(64), rng.getrandbits(40) | 1 << 39
+    A, B = FheUint64.try_encrypt(a, ck), FheUint64.try_encrypt(b, ck)
+    assert (A // B).decrypt(ck) == a // b
+    assert (A % B).decrypt(ck) == a % b
+
+
+def test_div256_by_encrypted(keys):
+    ck, _ = keys
+    rng = random.Random(256)
+    a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(128) | 1 << 127
+    q, r = FheUint256.try_encrypt(a, ck).div_rem(FheUint256.try_encrypt(b, ck))
+    assert (q.decrypt(ck), r.decrypt(ck)) == (a // b, a % b)

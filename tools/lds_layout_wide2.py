@@ -1,0 +1,44 @@
+"""LDS map for the latency kernel's merged exchange (br_wide.hip): phase D (wave (p, q), lane L, reg r:
+idx = 16 L + 4 r + q, region p) <-> phase E'' (wave w = 0..7, lane L, reg (pp, b0): idx = 128 w + 2 L + b0,
+region pp).  One linear map over the 10 index bits, per-instruction conflict degree under the gfx950
+b128 lane groups (lds_layout_quad3.py)."""
+import numpy as np
+from lds_layout_quad3 import RG, WG
+
+def cost(addr, write):
+    groups, ns = (WG, 8) if write else (RG, 16)
+    tot = 0.0
+    for g in groups:
+        a = addr[..., g]
+        s = a % ns
+        m = np.zeros(a.shape[:-1], np.int64)
+        for sl in range(ns):
+            m = np.maximum(m, (s == sl).sum(-1))
+        tot += m.sum()
+    return tot / addr[..., 0].size / len(groups) * (1)
+
+Lr = np.arange(64)
+D = np.array([[[16 * L + 4 * r + q for L in range(64)] for r in range(4)] for q in range(4)])     # [q][r][L]
+E = np.array([[[128 * w + 2 * L + b for L in range(64)] for b in range(2)] for w in range(8)])    # [w][b0][L]
+def bits(i):
+    return np.stack([(i >> k) & 1 for k in range(10)], -1)
+bD, bE = bits(D), bits(E)
+allb = bits(np.arange(1024))
+def score(w):
+    fD, fE = bD @ w, bE @ w
+    return cost(fD, 1) + cost(fD, 0) + cost(fE, 1) + cost(fE, 0), (cost(fD, 1), cost(fD, 0), cost(fE, 1), cost(fE, 0))
+if __name__ == "__main__":
+    base = np.array([1, 2, 4, 8, 16, 32, 66, 131, 264, 528])
+    print("current WX", score(base))
+    print("plain", score(1 << np.arange(10)))
+    rng = np.random.default_rng(3)
+    best = None
+    for trial in range(30000):
+        w = (1 << np.arange(10)) + rng.integers(0, 20, 10) * (rng.random(10) < 0.5)
+        ad = allb @ w
+        if ad.max() >= 1100 or len(np.unique(ad)) != 1024:
+            continue
+        s = score(w)
+        if best is None or s[0] < best[0][0]:
+            best = (s, w.tolist(), int(ad.max()))
+    print(best)
