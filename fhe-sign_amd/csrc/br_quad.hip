@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
     const int p = w >> 1, h = w & 1, t = threadIdx.x & 127;
     cplx* reg = s_x[p];
     const cplx* other = s_x[p ^ 1];
-    uint64_t* rot = reinterpret_cast<uint64_t*>(reg);
+    double* rot = reinterpret_cast<double*>(reg);
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
     const uint32_t sign9 = (uint32_t)(L & 1) << 31;
 
@@ -114,18 +114,17 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
     const int bB = fq(512 * h + 256 * ((L >> 5) & 1) + 128 * ((L >> 4) & 1) + (L & 15));
     const int bC = fq(512 * h + 16 * (L >> 1) + (L & 1));
 
-    uint64_t acc[16];  // coefficients 128 r + t
+    double acc[16];  // coefficients 128 r + t (f64 torus representatives)
     {
         const uint32_t bt = modswitch_2n(a_ct[n]);
         const int rotb = (int)((4096u - bt) & 4095u);  // X^{-b}
         const uint64_t* lut = luts + (size_t)(desc ? desc[ct].lut : lut_idx[ct]) * 2048;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            uint64_t v = 0;
+            double v = 0.0;
             if (p == 1) {
                 const uint32_t u = (uint32_t)(128 * r + t - rotb) & 4095u;
-                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
-                v = (lut[u & 2047u] ^ neg) - neg;
+                v = neg_if((double)(int64_t)lut[u & 2047u], (u >> 11) << 31);
             }
             acc[r] = v;
         }
@@ -149,17 +148,16 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) rot[128 * r + t] = acc[r];
         __syncthreads();
-        int32_t dg[16];  // digits of X^a acc - acc, decomposed as the rotated words arrive
+        double dg[16];  // digits of X^a acc - acc, decomposed as the rotated words arrive
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t u = (uint32_t)(128 * r + t - (int)a) & 4095u;
-            const uint64_t neg = 0ull - (uint64_t)(u >> 11);
-            dg[r] = decomp1<23>(((rot[u & 2047u] ^ neg) - neg) - acc[r]);
+            dg[r] = tor_digit<23>(neg_if(rot[u & 2047u], (u >> 11) << 31) - acc[r]);
         }
         __syncthreads();  // every rotation read done before the region is reused
         cplx x[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = cmul(make_double2((double)dg[r], (double)dg[r + 8]), pst[r]);
+        for (int r = 0; r < 8; ++r) x[r] = cmul(make_double2(dg[r], dg[r + 8]), pst[r]);
 
         // ---- forward FFT
         q_dif<2>(x, s_w, tpos(t));
@@ -242,12 +240,12 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         q_dit<1>(x, s_w, tpos(2 * t));
         q_dit<2>(x, s_w, tpos(t));
 
-        // ---- untwist, round, accumulate (point j = 128 r + t -> coefficients j, j + 1024)
+        // ---- untwist, accumulate (point j = 128 r + t -> coefficients j, j + 1024)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const cplx y = cmul(x[r], pst[r]);
-            acc[r] += f64_to_torus(y.x);
-            acc[r + 8] += f64_to_torus(y.y);
+            acc[r] = tor_red(acc[r] + y.x);
+            acc[r + 8] = tor_red(acc[r + 8] + y.y);
         }
     }
 
@@ -257,11 +255,12 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int j = 128 * r + t;
-            if (j == 0) o[0] = acc[r];
-            else o[2048 - j] = 0ull - acc[r];
+            const uint64_t v = f64_to_torus(acc[r]);
+            if (j == 0) o[0] = v;
+            else o[2048 - j] = 0ull - v;
         }
     } else if (t == 0) {
-        o[2048] = acc[0];
+        o[2048] = f64_to_torus(acc[0]);
     }
 }
 

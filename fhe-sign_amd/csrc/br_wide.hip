@@ -136,7 +136,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                                                               const cplx* __restrict__ tw,   // [12][256]
                                                               const cplx* __restrict__ psiw, // [4][256]
                                                               uint64_t* __restrict__ out, int n) {
-    __shared__ __attribute__((aligned(16))) uint64_t s_rot[2][ROT_SZ];
+    __shared__ __attribute__((aligned(16))) double s_rot[2][ROT_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_dx[2][1024];
 
@@ -153,23 +153,22 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     for (int r = 0; r < 4; ++r) PS[r] = psiw[r * 256 + t];
 
     // accumulator: coefficient c = 256 r' + 4 L + q, r' = 0..7
-    uint64_t acc[8];
+    double acc[8];  // f64 torus representatives
     {
         const uint32_t bt = modswitch_2n(a_ct[n]);
         const int rot = (int)((4096u - bt) & 4095u);
         const uint64_t* lut = luts + (size_t)(desc ? desc[ct].lut : lut_idx[ct]) * 2048;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            uint64_t v = 0;
+            double v = 0.0;
             if (p == 1) {
                 const uint32_t u = (uint32_t)(256 * r + 4 * L + q - rot) & 4095u;
-                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
-                v = (lut[u & 2047u] ^ neg) - neg;
+                v = neg_if((double)(int64_t)lut[u & 2047u], (u >> 11) << 31);
             }
             acc[r] = v;
         }
     }
-    uint64_t* rot_me = s_rot[p];
+    double* rot_me = s_rot[p];
     cplx* cross = s_cross[p];
     // lane parts of the linear LDS maps
     const int xD = fx(16 * L + q), xE = fx(256 * q + 4 * L);
@@ -202,17 +201,15 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         cplx x[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            int32_t d2[2];
+            double d2[2];
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
                 const int rr = r + 4 * hh;
                 const uint32_t u = (uint32_t)(256 * rr + 4 * L + q - (int)a) & 4095u;
-                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
                 const uint32_t c = u & 2047u;
-                const uint64_t v = (rot_me[c + (c >> 2)] ^ neg) - neg;
-                d2[hh] = decomp1<23>(v - acc[rr]);
+                d2[hh] = tor_digit<23>(neg_if(rot_me[c + (c >> 2)], (u >> 11) << 31) - acc[rr]);
             }
-            x[r] = cmul(make_double2((double)d2[0], (double)d2[1]), PS[r]);
+            x[r] = cmul(make_double2(d2[0], d2[1]), PS[r]);
         }
 
         // ---- forward FFT: A (stages 0,1) -> B -> C -> D (wave-private) -> E (cross-wave)
@@ -275,13 +272,13 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         xpose_AB(x);                 // B -> A
         dit2(x, T[0], T[1], T[2]);
 
-        // ---- untwist, round, accumulate (x[r] = idx 256 r + 4 L + q -> coefs idx, idx + 1024)
+        // ---- untwist, accumulate (x[r] = idx 256 r + 4 L + q -> coefs idx, idx + 1024)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const cplx u = make_double2(PS[r].x * 0.0009765625, -PS[r].y * 0.0009765625);
             const cplx y = cmul(x[r], u);
-            acc[r] += f64_to_torus(y.x);
-            acc[r + 4] += f64_to_torus(y.y);
+            acc[r] = tor_red(acc[r] + y.x);
+            acc[r + 4] = tor_red(acc[r + 4] + y.y);
         }
     }
 
@@ -291,11 +288,12 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int j = 256 * r + 4 * L + q;
-            if (j == 0) o[0] = acc[r];
-            else o[2048 - j] = 0ull - acc[r];
+            const uint64_t v = f64_to_torus(acc[r]);
+            if (j == 0) o[0] = v;
+            else o[2048 - j] = 0ull - v;
         }
     } else if (t == 0) {
-        o[2048] = acc[0];
+        o[2048] = f64_to_torus(acc[0]);
     }
 }
 

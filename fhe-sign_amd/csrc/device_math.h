@@ -7,6 +7,9 @@
 //   * multiplications by exactly 1 / +-i are done as moves (identical results up to the sign of
 //     zero, which cannot change any nonzero value and converts to torus 0 either way)
 //   * f64 -> torus: rint (v_rndne_f64), then exact mantissa/exponent reconstruction mod 2^64
+//   * blind-rotation accumulator: f64 torus representatives in [-2^63, 2^63] (oracle
+//     fho_blind_rotate): digit = tor_digit(X^a acc - acc), acc = tor_red(acc + y), u64 only at
+//     sample extraction
 // The whole translation unit is compiled with -ffp-contract=off.
 //
 // FFT register layout (one wave64 owns one 1024-point complex FFT, 16 points per lane):
@@ -53,6 +56,21 @@ FHE_DEV uint64_t f64_to_torus(double x) {
     v = ((unsigned)(e + 52) <= 115u) ? v : 0ull;  // keep e in [-52, 63]
     const uint64_t neg = 0ull - (b >> 63);
     return (v ^ neg) - neg;
+}
+
+// f64 torus representatives (oracle fho_tor_red / fho_tor_digit): v mod 2^64 into [-2^63, 2^63]
+// (the fma is exact), and the balanced one-level digit of v, base 2^BL, as an integer-valued double
+FHE_DEV double tor_red(double v) { return __fma_rn(-0x1p64, __builtin_rint(v * 0x1p-64), v); }
+template <int BL>
+FHE_DEV double tor_digit(double v) {
+    constexpr double down = 1.0 / (double)(1ull << (64 - BL)), base = (double)(1ull << BL), ibase = 1.0 / base;
+    const double g = __builtin_rint(v * down);
+    return __fma_rn(-base, __builtin_rint(g * ibase), g);
+}
+// v or -v by a lane bit (negbit = 0 or 1 << 31 applied to the high word): exact, one VALU op
+FHE_DEV double neg_if(double v, uint32_t negbit) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v) ^ ((uint64_t)negbit << 32);
+    return __longlong_as_double((long long)b);
 }
 
 // gadget decomposition, one level, base 2^BL, balanced digit in [-2^(BL-1), 2^(BL-1))

@@ -149,21 +149,20 @@ __global__ __launch_bounds__(128 * G, 2) void k_blind_rotate(const uint64_t* __r
     const int w = (threadIdx.x >> 6) & 1, L = threadIdx.x & 63;
     cplx* sc = lds[2 * g + w];
     cplx* sc_other = lds[2 * g + (w ^ 1)];
-    uint64_t* scu = reinterpret_cast<uint64_t*>(sc);
+    double* scu = reinterpret_cast<double*>(sc);
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
 
-    uint64_t acc[32];
+    double acc[32];  // f64 torus representatives (oracle fho_blind_rotate)
     {
         const uint32_t bt = modswitch_2n(a_ct[n]);
         const int rot = (int)((4096u - bt) & 4095u);  // X^{-b}
         const uint64_t* lut = luts + (size_t)(desc ? desc[ct].lut : lut_idx[ct]) * 2048;
 #pragma unroll
         for (int t = 0; t < 32; ++t) {
-            uint64_t v = 0;
+            double v = 0.0;
             if (w == 1) {
                 const uint32_t u = (uint32_t)(L + 64 * t - rot) & 4095u;
-                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
-                v = (lut[u & 2047u] ^ neg) - neg;
+                v = neg_if((double)(int64_t)lut[u & 2047u], (u >> 11) << 31);
             }
             acc[t] = v;
         }
@@ -198,17 +197,15 @@ __global__ __launch_bounds__(128 * G, 2) void k_blind_rotate(const uint64_t* __r
         cplx x[16];
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-            int32_t d2[2];
+            double d2[2];
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
                 const int tt = t + 16 * hh;
                 // (X^a acc)[j]: u = (j - a) mod 2N -> acc[u mod N], negated iff u >= N
                 const uint32_t u = (uint32_t)(L + 64 * tt - (int)a) & 4095u;
-                const uint64_t neg = 0ull - (uint64_t)(u >> 11);
-                const uint64_t v = (scu[u & 2047u] ^ neg) - neg;
-                d2[hh] = decomp1<BR_PBS_BL>(v - acc[tt]);
+                d2[hh] = tor_digit<BR_PBS_BL>(neg_if(scu[u & 2047u], (u >> 11) << 31) - acc[tt]);
             }
-            x[t] = cmul(make_double2((double)d2[0], (double)d2[1]), ps[t]);
+            x[t] = cmul(make_double2(d2[0], d2[1]), ps[t]);
             if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         wave_sync();
@@ -254,14 +251,14 @@ __global__ __launch_bounds__(128 * G, 2) void k_blind_rotate(const uint64_t* __r
         __builtin_amdgcn_sched_barrier(0);
         dit_stage<0>(x, Wl);
 
-        // ---- untwist, round, accumulate
+        // ---- untwist, accumulate
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const cplx p = ps[t];
             const cplx u = make_double2(p.x * 0.0009765625, -p.y * 0.0009765625);
             const cplx y = cmul(x[t], u);
-            acc[t] += f64_to_torus(y.x);
-            acc[t + 16] += f64_to_torus(y.y);
+            acc[t] = tor_red(acc[t] + y.x);
+            acc[t + 16] = tor_red(acc[t + 16] + y.y);
             if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -273,11 +270,12 @@ __global__ __launch_bounds__(128 * G, 2) void k_blind_rotate(const uint64_t* __r
 #pragma unroll
         for (int t = 0; t < 32; ++t) {
             const int j = L + 64 * t;
-            if (j == 0) o[0] = acc[t];
-            else o[2048 - j] = 0ull - acc[t];
+            const uint64_t v = f64_to_torus(acc[t]);
+            if (j == 0) o[0] = v;
+            else o[2048 - j] = 0ull - v;
         }
     } else if (L == 0) {
-        o[2048] = acc[0];
+        o[2048] = f64_to_torus(acc[0]);
     }
 }
 

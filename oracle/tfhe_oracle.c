@@ -175,13 +175,11 @@ void fho_poly_to_fourier(const uint64_t* poly, double* out) {
     fho_fft_forward(out);
 }
 
-void fho_ipoly_to_fourier(const int64_t* poly, double* out) {
+/* digit polynomial (integer-valued doubles) -> Fourier */
+void fho_dpoly_to_fourier(const double* poly, double* out) {
     fho_tables_init();
-    for (int j = 0; j < 1024; ++j) {
-        double re = (double)poly[j];
-        double im = (double)poly[j + 1024];
-        cmul(re, im, g_psi[2 * j], g_psi[2 * j + 1], &out[2 * j], &out[2 * j + 1]);
-    }
+    for (int j = 0; j < 1024; ++j)
+        cmul(poly[j], poly[j + 1024], g_psi[2 * j], g_psi[2 * j + 1], &out[2 * j], &out[2 * j + 1]);
     fho_fft_forward(out);
 }
 
@@ -200,7 +198,19 @@ uint64_t fho_f64_to_torus(double x) {
     return (b >> 63) ? (uint64_t)0 - v : v;
 }
 
-void fho_fourier_add_to_poly(double* f, uint64_t* acc) {
+/* Torus elements in the blind-rotation accumulator are held as f64 representatives (see
+ * fho_blind_rotate).  tor_red: v mod 2^64 into [-2^63, 2^63]; the fma is exact (the result is a
+ * multiple of ulp(v) no larger than |v|), so only v itself carries rounding. */
+double fho_tor_red(double v) { return fma(-0x1p64, rint(v * 0x1p-64), v); }
+
+/* one-level gadget digit of v (base 2^base_log, balanced into [-2^(bl-1), 2^(bl-1)]) as a double:
+ * g = round(v / 2^(64-bl)) in [-2^bl, 2^bl], then g mod 2^bl */
+double fho_tor_digit(double v, uint32_t base_log) {
+    const double g = rint(v * ldexp(1.0, -(int)(64 - base_log)));
+    return fma(-ldexp(1.0, (int)base_log), rint(g * ldexp(1.0, -(int)base_log)), g);
+}
+
+void fho_fourier_add_to_poly(double* f, double* acc) {
     fho_tables_init();
     fho_fft_inverse(f);
     const double inv = 0.0009765625; /* 2^-10, exact */
@@ -208,8 +218,8 @@ void fho_fourier_add_to_poly(double* f, uint64_t* acc) {
         double ur = g_psi[2 * j] * inv, ui = -g_psi[2 * j + 1] * inv; /* exact scalings */
         double yr, yi;
         cmul(f[2 * j], f[2 * j + 1], ur, ui, &yr, &yi);
-        acc[j] += fho_f64_to_torus(yr);
-        acc[j + 1024] += fho_f64_to_torus(yi);
+        acc[j] = fho_tor_red(acc[j] + yr);
+        acc[j + 1024] = fho_tor_red(acc[j + 1024] + yi);
     }
 }
 
@@ -336,47 +346,50 @@ uint32_t fho_modswitch(uint64_t x) {
     return (uint32_t)((((x >> 51) + 1) >> 1) & (2 * FHO_N - 1));
 }
 
-/* out = X^r * v (negacyclic), r in [0, 2N) */
-static void poly_rotate(const uint64_t* v, uint32_t r, uint64_t* out) {
+/* out = X^r * v (negacyclic), r in [0, 2N); negation of a double is exact */
+static void poly_rotate_d(const double* v, uint32_t r, double* out) {
     for (int j = 0; j < FHO_N; ++j) {
         int t = j - (int)r;
         if (t >= 0) out[j] = v[t];
-        else if (t >= -FHO_N) out[j] = (uint64_t)0 - v[t + FHO_N];
+        else if (t >= -FHO_N) out[j] = -v[t + FHO_N];
         else out[j] = v[t + 2 * FHO_N];
     }
 }
 
-static inline int64_t decomp_pbs(uint64_t x, uint32_t base_log) {
-    const uint32_t sh = 64 - base_log;                 /* 41 */
-    uint64_t v = (((x >> (sh - 1)) + 1) >> 1) & ((1ull << base_log) - 1);
-    int64_t d = (int64_t)v;
-    if (d >= (1ll << (base_log - 1))) d -= (1ll << base_log);
-    return d;
-}
-
+/* Blind rotation ACC = X^{-b} LUT, then n CMUX.  The accumulator's torus coefficients are kept as
+ * f64 representatives in [-2^63, 2^63] instead of u64: X^a acc - acc is one f64 subtraction, its
+ * gadget digit two rint's (fho_tor_digit, exact integers, no int->f64 conversion), and the external
+ * product is added without rounding to an integer first (acc = tor_red(acc + y)).  The extra error
+ * is the rounding of acc + y at the magnitude of y (~2^90 typical, <= 2^97), i.e. the same order as
+ * the f64 transform's own error -- 2^-25 of the torus per CMUX against a blind-rotation noise of
+ * ~2^-15 (bootstrapping-key noise x digits); decryption is unaffected.  The GLWE is returned as u64
+ * (fho_f64_to_torus, round half even) for sample extraction. */
 void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_t* lut,
                       uint64_t* glwe) {
     const uint32_t n = k->p.n;
-    uint64_t* acc0 = glwe;            /* mask */
-    uint64_t* acc1 = glwe + FHO_N;    /* body */
-    uint64_t* rot = (uint64_t*)malloc(FHO_N * 8);
-    int64_t* dig = (int64_t*)malloc(FHO_N * 8);
+    double* acc0 = (double*)malloc(FHO_N * 8);  /* mask */
+    double* acc1 = (double*)malloc(FHO_N * 8);  /* body */
+    double* rot = (double*)malloc(FHO_N * 8);
+    double* dig = (double*)malloc(FHO_N * 8);
     double* D0 = (double*)malloc(FHO_HALF * 16);
     double* D1 = (double*)malloc(FHO_HALF * 16);
     double* O = (double*)malloc(FHO_HALF * 16);
 
     uint32_t bt = fho_modswitch(ct_small[n]);
-    memset(acc0, 0, FHO_N * 8);
-    poly_rotate(lut, (2 * FHO_N - bt) & (2 * FHO_N - 1), acc1);
+    for (int j = 0; j < FHO_N; ++j) {
+        acc0[j] = 0.0;
+        rot[j] = (double)(int64_t)lut[j];
+    }
+    poly_rotate_d(rot, (2 * FHO_N - bt) & (2 * FHO_N - 1), acc1);
 
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t a = fho_modswitch(ct_small[i]);
         if (a == 0) continue;
         for (int m = 0; m < 2; ++m) {
-            uint64_t* acc = m ? acc1 : acc0;
-            poly_rotate(acc, a, rot);
-            for (int j = 0; j < FHO_N; ++j) dig[j] = decomp_pbs(rot[j] - acc[j], k->p.pbs_base_log);
-            fho_ipoly_to_fourier(dig, m ? D1 : D0);
+            double* acc = m ? acc1 : acc0;
+            poly_rotate_d(acc, a, rot);
+            for (int j = 0; j < FHO_N; ++j) dig[j] = fho_tor_digit(rot[j] - acc[j], k->p.pbs_base_log);
+            fho_dpoly_to_fourier(dig, m ? D1 : D0);
         }
         const double* bi = k->bsk_f + (size_t)i * 4 * FHO_HALF * 2;
         for (int w = 0; w < 2; ++w) {
@@ -391,7 +404,11 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
             fho_fourier_add_to_poly(O, w ? acc1 : acc0);
         }
     }
-    free(rot); free(dig); free(D0); free(D1); free(O);
+    for (int j = 0; j < FHO_N; ++j) {
+        glwe[j] = fho_f64_to_torus(acc0[j]);
+        glwe[FHO_N + j] = fho_f64_to_torus(acc1[j]);
+    }
+    free(acc0); free(acc1); free(rot); free(dig); free(D0); free(D1); free(O);
 }
 
 void fho_sample_extract(const uint64_t* glwe, uint64_t* ct) {

@@ -93,9 +93,12 @@ void fho_fft_inverse(double* x /* HALF complex, output unscaled */);
 /* standard-domain torus polynomial (N u64) -> Fourier (HALF complex, bit-reversed) */
 void fho_poly_to_fourier(const uint64_t* poly, double* out);
 /* small signed integer polynomial -> Fourier */
-void fho_ipoly_to_fourier(const int64_t* poly, double* out);
-/* Fourier (bit-reversed) -> torus polynomial, ADDED into acc (acc += round(result)) */
-void fho_fourier_add_to_poly(double* f /* clobbered */, uint64_t* acc);
+void fho_dpoly_to_fourier(const double* poly, double* out);
+/* Fourier (bit-reversed) -> torus polynomial ADDED into an f64 accumulator: acc = red(acc + y) */
+void fho_fourier_add_to_poly(double* f /* clobbered */, double* acc);
+/* f64 torus representatives: v mod 2^64 into [-2^63, 2^63]; one-level gadget digit */
+double fho_tor_red(double v);
+double fho_tor_digit(double v, uint32_t base_log);
 uint64_t fho_f64_to_torus(double x);
 
 /* --- encryption (big key, dimension N) --- */
