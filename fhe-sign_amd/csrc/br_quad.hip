@@ -59,10 +59,7 @@ FHE_DEV void q_dit(cplx (&x)[8], const cplx* __restrict__ sw, int lb) {
     for (int r = 0; r < 8; ++r) {
         if (r >> K & 1) continue;
         const int c = r | (1 << K);
-        const cplx w = conj_(sw[lb + step * (r & ((1 << K) - 1))]);
-        const cplx a = x[r], t = cmul(x[c], w);
-        x[r] = cadd(a, t);
-        x[c] = csub(a, t);
+        dit_bfly(x[r], x[c], conj_(sw[lb + step * (r & ((1 << K) - 1))]));
     }
 }
 
@@ -138,8 +135,9 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         const cplx* Pg = ps;
         asm volatile("" : "+s"(Pg));
         const gcptr P = as_global(Pg) + t;
-        const gcptr b0 = as_global(bsk) + ((size_t)((i * 2 + 0) * 2 + p) * 16 + 8 * h) * 64 + L;
-        const gcptr b1 = as_global(bsk) + ((size_t)((i * 2 + 1) * 2 + p) * 16 + 8 * h) * 64 + L;
+        // BSK rows for this wave's own digit (row p) and the other polynomial's digit (row 1 - p)
+        const gcptr bm = as_global(bsk) + ((size_t)((i * 2 + p) * 2 + p) * 16 + 8 * h) * 64 + L;
+        const gcptr bo = as_global(bsk) + ((size_t)((i * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 64 + L;
 
         // ---- rotate (X^a acc - acc) through the polynomial's region, decompose, twist
         cplx pst[8];
@@ -182,8 +180,8 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         cplx Bq0[QR], Bq1[QR];
 #pragma unroll
         for (int r = 0; r < QR; ++r) {
-            Bq0[r] = b0[r * 64];
-            Bq1[r] = b1[r * 64];
+            Bq0[r] = bm[r * 64];
+            Bq1[r] = bo[r * 64];
         }
         q_dif<2>(x, s_w, tpos(64 * (L & 1)));
         q_dif<1>(x, s_w, tpos(128 * (L & 1)));
@@ -195,22 +193,15 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bC + fq(2 * r)] = x[r];
         __syncthreads();
-        const bool own_mask = __builtin_amdgcn_readfirstlane(p) == 0;
+        // mac2 is symmetric in its two rows: own digit x BSK row p, other digit x row 1 - p
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const cplx B0 = Bq0[r % QR], B1 = Bq1[r % QR];
+            const cplx Bm = Bq0[r % QR], Bo = Bq1[r % QR];
             if (r + QR < 8) {
-                Bq0[r % QR] = b0[(r + QR) * 64];
-                Bq1[r % QR] = b1[(r + QR) * 64];
+                Bq0[r % QR] = bm[(r + QR) * 64];
+                Bq1[r % QR] = bo[(r + QR) * 64];
             }
-            const cplx mine = x[r];
-            const cplx oth = other[bC + fq(2 * r)];
-            const cplx d0 = own_mask ? mine : oth;
-            const cplx d1 = own_mask ? oth : mine;
-            cplx o;
-            o.x = __fma_rn(d0.x, B0.x, __fma_rn(-d0.y, B0.y, __fma_rn(d1.x, B1.x, -(d1.y * B1.y))));
-            o.y = __fma_rn(d0.x, B0.y, __fma_rn(d0.y, B0.x, __fma_rn(d1.x, B1.y, d1.y * B1.x)));
-            x[r] = o;
+            x[r] = mac2(x[r], Bm, other[bC + fq(2 * r)], Bo);
         }
 
         // ---- inverse FFT: stage 9 and phase C in registers, then the region again

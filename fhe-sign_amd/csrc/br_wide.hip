@@ -41,12 +41,7 @@ FHE_DEV void dif(cplx& a, cplx& c, cplx w) {
     a = s;
     c = cmul(d, w);
 }
-FHE_DEV void dit(cplx& a, cplx& c, cplx wconj) {
-    cplx t = cmul(c, wconj);
-    cplx s = cadd(a, t), d = csub(a, t);
-    a = s;
-    c = d;
-}
+FHE_DEV void dit(cplx& a, cplx& c, cplx wconj) { dit_bfly(a, c, wconj); }
 
 // ---- in-register 2x2 transposes between a register bit and a lane bit (wave-private exchanges)
 // X holds register bit 0, Y register bit 1; afterwards the register bit and lane bit k are swapped.
@@ -182,8 +177,8 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         // BSK slice for this iteration (issued early; consumed after the forward FFT)
         cplx B0[4], B1[4];
         {
-            const cplx* b0 = bsk + ((size_t)((i * 2 + 0) * 2 + p) * 16 + 4 * q) * 64 + L;
-            const cplx* b1 = bsk + ((size_t)((i * 2 + 1) * 2 + p) * 16 + 4 * q) * 64 + L;
+            const cplx* b0 = bsk + ((size_t)((i * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;        // own digit's row
+            const cplx* b1 = bsk + ((size_t)((i * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;  // other digit's row
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 B0[r] = b0[r * 64];
@@ -242,13 +237,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const cplx oth = dx_other[r * 64];
-            const cplx d0 = (p == 0) ? x[r] : oth;
-            const cplx d1 = (p == 0) ? oth : x[r];
-            cplx o;
-            o.x = __fma_rn(d0.x, B0[r].x, __fma_rn(-d0.y, B0[r].y, __fma_rn(d1.x, B1[r].x, -(d1.y * B1[r].y))));
-            o.y = __fma_rn(d0.x, B0[r].y, __fma_rn(d0.y, B0[r].x, __fma_rn(d1.x, B1[r].y, d1.y * B1[r].x)));
-            x[r] = o;
+            x[r] = mac2(x[r], B0[r], dx_other[r * 64], B1[r]);  // symmetric: own row p, other row 1 - p
         }
 
         // ---- inverse FFT: E -> D (cross-wave) -> C -> B -> A (wave-private)
@@ -256,8 +245,8 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             cplx a0 = x[0], c0 = x[1], a1 = x[2], c1 = x[3];
             x[0] = cadd(a0, c0); x[1] = csub(a0, c0);
             x[2] = cadd(a1, c1); x[3] = csub(a1, c1);
-            a0 = x[0]; c0 = x[2]; x[0] = cadd(a0, c0); x[2] = csub(a0, c0);
-            a1 = x[1]; c1 = mul_negi(x[3]); x[1] = cadd(a1, c1); x[3] = csub(a1, c1);
+            dit_bfly_unit(x[0], x[2], x[2]);
+            dit_bfly_unit(x[1], x[3], mul_negi(x[3]));
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) cross[xE + fx(r)] = x[r];

@@ -3,7 +3,10 @@
 // Arithmetic contract (identical, operation for operation, to oracle/tfhe_oracle.c so that GPU
 // outputs are bit-exact against the CPU restatement):
 //   * complex multiply  y = x*w : y.re = fma(x.re, w.re, -(x.im*w.im)); y.im = fma(x.re, w.im, x.im*w.re)
-//   * forward FFT: radix-2 DIF, natural -> bit-reversed; inverse: radix-2 DIT with conj twiddles
+//   * forward FFT: radix-2 DIF, natural -> bit-reversed; inverse: radix-2 DIT with conj twiddles,
+//     butterfly p = a + w c (two fmas per component), m = 2a - p (dit_bfly); its first stage
+//     (span 1, twiddle 1) is the plain a +- c
+//   * pointwise product: D0 B0 + D1 B1 = cmul(D0, B0) + cmul(D1, B1) (mac2: symmetric in the rows)
 //   * multiplications by exactly 1 / +-i are done as moves (identical results up to the sign of
 //     zero, which cannot change any nonzero value and converts to torus 0 either way)
 //   * f64 -> torus: rint (v_rndne_f64), then exact mantissa/exponent reconstruction mod 2^64
@@ -35,6 +38,28 @@ FHE_DEV cplx cmul(cplx x, cplx w) {
     y.x = __fma_rn(x.x, w.x, -(x.y * w.y));
     y.y = __fma_rn(x.x, w.y, x.y * w.x);
     return y;
+}
+// DIT butterfly with twiddle w (already conjugated): (a, c) <- (a + w c, a - w c) as
+// p = a + w c (two fmas per component) and m = 2a - p (one fma) -- 6 ops instead of 8
+FHE_DEV void dit_bfly(cplx& a, cplx& c, cplx w) {
+    cplx p;
+    p.x = __fma_rn(w.x, c.x, __fma_rn(-w.y, c.y, a.x));
+    p.y = __fma_rn(w.x, c.y, __fma_rn(w.y, c.x, a.y));
+    c = make_double2(__fma_rn(2.0, a.x, -p.x), __fma_rn(2.0, a.y, -p.y));
+    a = p;
+}
+// the same butterfly when w c is exact (w = 1 or -i, t = c or mul_negi(c)): p = a + t, m = 2a - p
+FHE_DEV void dit_bfly_unit(cplx& a, cplx& c, cplx t) {
+    const cplx p = make_double2(a.x + t.x, a.y + t.y);
+    c = make_double2(__fma_rn(2.0, a.x, -p.x), __fma_rn(2.0, a.y, -p.y));
+    a = p;
+}
+// pointwise MAC of the external product for one Fourier point: d0 B0 + d1 B1 (oracle order)
+FHE_DEV cplx mac2(cplx d0, cplx b0, cplx d1, cplx b1) {
+    cplx o;
+    o.x = __fma_rn(d0.x, b0.x, -(d0.y * b0.y)) + __fma_rn(d1.x, b1.x, -(d1.y * b1.y));
+    o.y = __fma_rn(d0.x, b0.y, d0.y * b0.x) + __fma_rn(d1.x, b1.y, d1.y * b1.x);
+    return o;
 }
 FHE_DEV cplx cadd(cplx a, cplx b) { return make_double2(a.x + b.x, a.y + b.y); }
 FHE_DEV cplx csub(cplx a, cplx b) { return make_double2(a.x - b.x, a.y - b.y); }
@@ -142,11 +167,7 @@ FHE_DEV void dit_stage(cplx (&x)[16], gcptr Wl) {
     for (int g = 0; g < hd; ++g) {
         const cplx tw = conj_(Wl[tw_slot(hd, g) * 64]);
 #pragma unroll
-        for (int t = g; t < 16; t += 2 * hd) {
-            cplx a = x[t], c = cmul(x[t + hd], tw);
-            x[t] = cadd(a, c);
-            x[t + hd] = csub(a, c);
-        }
+        for (int t = g; t < 16; t += 2 * hd) dit_bfly(x[t], x[t + hd], tw);
     }
 }
 
@@ -188,9 +209,9 @@ FHE_DEV void dit_phase_c(cplx (&x)[16]) {
         cplx a0 = y[0], c0 = y[1], a1 = y[2], c1 = y[3];
         y[0] = cadd(a0, c0); y[1] = csub(a0, c0);
         y[2] = cadd(a1, c1); y[3] = csub(a1, c1);
-        // stage 8 (h = 2): q=1 twiddle conj(i) = -i
-        a0 = y[0]; c0 = y[2]; y[0] = cadd(a0, c0); y[2] = csub(a0, c0);
-        a1 = y[1]; c1 = mul_negi(y[3]); y[1] = cadd(a1, c1); y[3] = csub(a1, c1);
+        // stage 8 (h = 2): twiddles 1 and conj(i) = -i, exact products, fused butterfly
+        dit_bfly_unit(y[0], y[2], y[2]);
+        dit_bfly_unit(y[1], y[3], mul_negi(y[3]));
     }
 }
 

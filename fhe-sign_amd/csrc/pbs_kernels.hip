@@ -102,11 +102,10 @@ constexpr int BR_PBS_BL = 23;
 constexpr int kRing = 2;
 constexpr int kBrGroup = 1;  // ciphertexts per workgroup; measured per 8192: G=1 101 ms, G=2 157, G=4 108
 
-// out[R] = D0[R] * B0[R] + D1[R] * B1[R] (fused chain identical to the oracle), in place in x.
+// out[R] = own digit x BSK row w + partner digit x row 1 - w (mac2, symmetric like the oracle), in place.
 // The BSK rows stream through a register ring of depth kRing (Bq0/Bq1 hold R < kRing on entry): each
 // step consumes slot R % kRing and refills it with R + kRing.  kRing = 2 is what fits beside the
 // accumulator and FFT state in 256 VGPRs (deeper rings spill: measured 146 ms vs 102 ms per 8192).
-template <bool OWN_IS_MASK>
 FHE_DEV void pointwise_mac(cplx (&x)[16], const cplx* __restrict__ other, cplx (&Bq0)[kRing], cplx (&Bq1)[kRing],
                            gcptr b0, gcptr b1) {
 #pragma unroll
@@ -116,14 +115,7 @@ FHE_DEV void pointwise_mac(cplx (&x)[16], const cplx* __restrict__ other, cplx (
             Bq0[R % kRing] = b0[(R + kRing) * 64];
             Bq1[R % kRing] = b1[(R + kRing) * 64];
         }
-        const cplx mine = x[R];
-        const cplx oth = other[R * 64];
-        const cplx d0 = OWN_IS_MASK ? mine : oth;
-        const cplx d1 = OWN_IS_MASK ? oth : mine;
-        cplx o;
-        o.x = __fma_rn(d0.x, B0.x, __fma_rn(-d0.y, B0.y, __fma_rn(d1.x, B1.x, -(d1.y * B1.y))));
-        o.y = __fma_rn(d0.x, B0.y, __fma_rn(d0.y, B0.x, __fma_rn(d1.x, B1.y, d1.y * B1.x)));
-        x[R] = o;
+        x[R] = mac2(x[R], B0, other[R * 64], B1);  // symmetric: own digit x row w, other x row 1 - w
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -181,8 +173,9 @@ __global__ __launch_bounds__(128 * G, 2) void k_blind_rotate(const uint64_t* __r
         const cplx* Pg = psi;
         asm volatile("" : "+s"(Wg), "+s"(Pg));
         const gcptr Wl = as_global(Wg) + L, Pl = as_global(Pg) + L;
-        const gcptr b0 = as_global(bsk) + ((size_t)((i * 2 + 0) * 2 + w) * 16) * 64 + L;
-        const gcptr b1 = as_global(bsk) + ((size_t)((i * 2 + 1) * 2 + w) * 16) * 64 + L;
+        // row w multiplies this wave's own digit polynomial, row 1 - w the partner's (mac2 is symmetric)
+        const gcptr b0 = as_global(bsk) + ((size_t)((i * 2 + w) * 2 + w) * 16) * 64 + L;
+        const gcptr b1 = as_global(bsk) + ((size_t)((i * 2 + (w ^ 1)) * 2 + w) * 16) * 64 + L;
 
         // ---- twist factors in flight while the accumulator goes through LDS
         cplx ps[16];
@@ -229,12 +222,7 @@ __global__ __launch_bounds__(128 * G, 2) void k_blind_rotate(const uint64_t* __r
 #pragma unroll
         for (int R = 0; R < 16; ++R) sc[R * 64 + L] = x[R];
         __syncthreads();
-        // row 0 multiplies the mask digits D0, row 1 the body digits D1 (oracle order); the branch
-        // is wave-uniform so both waves evaluate the identical expression tree.
-        if (__builtin_amdgcn_readfirstlane(w) == 0)
-            pointwise_mac<true>(x, sc_other + L, Bq0, Bq1, b0, b1);
-        else
-            pointwise_mac<false>(x, sc_other + L, Bq0, Bq1, b0, b1);
+        pointwise_mac(x, sc_other + L, Bq0, Bq1, b0, b1);
         __syncthreads();
 
         // ---- inverse FFT (untwist factors issued before its last stage)

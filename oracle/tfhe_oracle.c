@@ -145,7 +145,8 @@ void fho_fft_forward(double* x) {
 }
 
 /* Inverse: radix-2 decimation in time with conjugate twiddles, bit-reversed in, natural out,
- * unscaled (x 1024). */
+ * unscaled (x 1024).  Butterfly (a, c) -> (p, m): p = a + conj(w) c with two fmas per component,
+ * m = 2a - p (one fma); the first stage (span 1, twiddle 1) is the plain (a + c, a - c). */
 void fho_fft_inverse(double* x) {
     fho_tables_init();
     for (int s = 9; s >= 0; --s) {
@@ -155,11 +156,16 @@ void fho_fft_inverse(double* x) {
                 double* p = x + 2 * (b + j);
                 double* q = x + 2 * (b + j + h);
                 const double* w = g_tw + 2 * (j << s);
-                double tr, ti;
-                cmul(q[0], q[1], w[0], -w[1], &tr, &ti);
-                double ar = p[0], ai = p[1];
-                p[0] = ar + tr; p[1] = ai + ti;
-                q[0] = ar - tr; q[1] = ai - ti;
+                const double ar = p[0], ai = p[1], cr = q[0], ci = q[1];
+                if (s == 9) {
+                    p[0] = ar + cr; p[1] = ai + ci;
+                    q[0] = ar - cr; q[1] = ai - ci;
+                    continue;
+                }
+                const double pr = fma(w[0], cr, fma(w[1], ci, ar));   /* conj(w) = (w0, -w1) */
+                const double pi = fma(w[0], ci, fma(-w[1], cr, ai));
+                p[0] = pr; p[1] = pi;
+                q[0] = fma(2.0, ar, -pr); q[1] = fma(2.0, ai, -pi);
             }
         }
     }
@@ -398,8 +404,10 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
             for (int q = 0; q < FHO_HALF; ++q) {
                 double d0r = D0[2 * q], d0i = D0[2 * q + 1], d1r = D1[2 * q], d1i = D1[2 * q + 1];
                 double b0r = B0[2 * q], b0i = B0[2 * q + 1], b1r = B1[2 * q], b1i = B1[2 * q + 1];
-                O[2 * q] = fma(d0r, b0r, fma(-d0i, b0i, fma(d1r, b1r, -(d1i * b1i))));
-                O[2 * q + 1] = fma(d0r, b0i, fma(d0i, b0r, fma(d1r, b1i, d1i * b1r)));
+                /* D0 B0 + D1 B1 as a sum of two products: symmetric in the two rows, so a GPU wave
+                 * may hold either digit as its own */
+                O[2 * q] = fma(d0r, b0r, -(d0i * b0i)) + fma(d1r, b1r, -(d1i * b1i));
+                O[2 * q + 1] = fma(d0r, b0i, d0i * b0r) + fma(d1r, b1i, d1i * b1r);
             }
             fho_fourier_add_to_poly(O, w ? acc1 : acc0);
         }
