@@ -38,28 +38,45 @@ FHE_DEV constexpr int fq(int i) {
 constexpr int QTW_SZ = 512 + 16;
 FHE_DEV constexpr int tpos(int k) { return k + (k >> 5); }
 
-// DIF stage on register bit K (pairs r, r | 2^K); lb = tpos(lane part of the twiddle index)
+// DIF stage on register bit K (pairs r, r | 2^K); lb = tpos(lane part of the twiddle index).
+// The twiddle index is lane part + step * (r mod 2^K), step 128 (K = 2) or 256 (K = 1), with lane
+// part < step; the table's W[k + 256] = i W[k] (oracle fho_tables_init), so the upper entries of
+// those stages are moves of the lower ones (K = 0 loads its single twiddle, index < 512).
+template <int K>
+FHE_DEV void q_twiddles(cplx (&w)[4], const cplx* __restrict__ sw, int lb) {
+    if constexpr (K == 2) {
+        w[0] = sw[lb];
+        w[1] = sw[lb + 132];
+        w[2] = mul_i(w[0]);
+        w[3] = mul_i(w[1]);
+    } else if constexpr (K == 1) {
+        w[0] = sw[lb];
+        w[1] = mul_i(w[0]);
+    } else {
+        w[0] = sw[lb];
+    }
+}
 template <int K>
 FHE_DEV void q_dif(cplx (&x)[8], const cplx* __restrict__ sw, int lb) {
-    constexpr int step = K == 2 ? 132 : 264;
+    cplx w[4];
+    q_twiddles<K>(w, sw, lb);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         if (r >> K & 1) continue;
         const int c = r | (1 << K);
-        const cplx w = sw[lb + step * (r & ((1 << K) - 1))];
         const cplx a = x[r], b = x[c];
         x[r] = cadd(a, b);
-        x[c] = cmul(csub(a, b), w);
+        x[c] = cmul(csub(a, b), w[r & ((1 << K) - 1)]);
     }
 }
 template <int K>
 FHE_DEV void q_dit(cplx (&x)[8], const cplx* __restrict__ sw, int lb) {
-    constexpr int step = K == 2 ? 132 : 264;
+    cplx w[4];
+    q_twiddles<K>(w, sw, lb);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         if (r >> K & 1) continue;
-        const int c = r | (1 << K);
-        dit_bfly(x[r], x[c], conj_(sw[lb + step * (r & ((1 << K) - 1))]));
+        dit_bfly(x[r], x[r | (1 << K)], conj_(w[r & ((1 << K) - 1)]));
     }
 }
 

@@ -24,7 +24,7 @@ void fft_tables(std::vector<double2>* W, std::vector<double2>* psi) {
         (*W)[k] = make_double2(std::cos(a), std::sin(a));
     }
     (*W)[0] = make_double2(1.0, 0.0);
-    (*W)[256] = make_double2(0.0, 1.0);
+    for (int k = 256; k < 512; ++k) (*W)[k] = make_double2(-(*W)[k - 256].y, (*W)[k - 256].x);  // i W[k - 256], exact
     for (int j = 0; j < 1024; ++j) {
         double a = pi * (double)j / 2048.0;
         (*psi)[j] = make_double2(std::cos(a), std::sin(a));

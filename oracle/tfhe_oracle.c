@@ -103,9 +103,14 @@ void fho_tables_init(void) {
         g_tw[2 * k] = cos(a);
         g_tw[2 * k + 1] = sin(a);
     }
-    /* exact values where the angle is a multiple of pi/2 */
+    /* exact values where the angle is a multiple of pi/2; the upper quarter turn is defined as
+     * i times the lower one, exactly (W[k + 256] = (-W[k].im, W[k].re)), so a kernel may derive
+     * it from W[k] with a move instead of loading it */
     g_tw[0] = 1.0; g_tw[1] = 0.0;
-    g_tw[2 * 256] = 0.0; g_tw[2 * 256 + 1] = 1.0;
+    for (int k = 256; k < 512; ++k) {
+        g_tw[2 * k] = -g_tw[2 * (k - 256) + 1];
+        g_tw[2 * k + 1] = g_tw[2 * (k - 256)];
+    }
     for (int j = 0; j < 1024; ++j) {
         double a = pi * (double)j / 2048.0;
         g_psi[2 * j] = cos(a);
