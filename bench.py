@@ -141,6 +141,10 @@ def ops_legs(ck, ctx, seed):
     leg("div256_by_5", lambda: A256 / 5, lambda r: r.decrypt(ck) == a // 5)
     leg("div256_by_u32", lambda: A256 / du32, lambda r: r.decrypt(ck) == a // du32)
     leg("div256_by_u128", lambda: A256 / du128, lambda r: r.decrypt(ck) == a // du128)
+    # the stretch case of config 3: 256-bit by an ENCRYPTED 128-bit-valued divisor, quotient + remainder
+    D256 = FheUint256.try_encrypt(du128, ck)
+    leg("div256_by_encrypted", lambda: A256.div_rem(D256),
+        lambda r: (r[0].decrypt(ck), r[1].decrypt(ck)) == (a // du128, a % du128))
     X32 = FheUint32.try_encrypt(1344, ck)  # src/perf_test.rs:14-15,54 (README.md:114: 1121 s on CPU)
     leg("fheuint32_div5", lambda: X32 / 5, lambda r: r.decrypt(ck) == 268)
     leg("fheuint32_add", lambda: X32 + FheUint32.try_encrypt(5, ck), lambda r: r.decrypt(ck) == 1349)

@@ -1002,17 +1002,22 @@ Radix radix_clean(Engine& e, const Radix& a) {
 }
 
 // Encrypted / encrypted: radix-4 restoring division, one quotient block (2 bits) per step from the
-// top.  With r < d kept exact in n + 1 blocks:  r4 = 4 r + a_i,  three subtractions r4 - c d
-// (c = 1..3, complements of d, 2d, 3d prepared once) share their levels and give the borrow bits
-// ge_c = [r4 >= c d];  q_i = ge_1 + ge_2 + ge_3 (one bootstrap, in the subtractions' final level),
-// r = the candidate picked by q_i (half-selects f(4 q_i + cand), noise 16 + 1) and cleaned.
-// d = 0 gives q = 2^bits - 1 and r = a (every ge_c = 1), tfhe's convention.  ~12 levels per block.
+// top.  Step i (w = n - i) keeps r < d exact: r4 = 4 r + a_i < 4^w, so only w blocks take part.
+// Three subtractions r4 - c d (c = 1..3, complements of d, 2d, 3d prepared once) share their levels;
+// the blocks of c d at positions >= w enter as ONE column holding P_c[w] = 3 if all of them are zero
+// (else 0), so the carry out of that column is ge_c = [r4 >= c d] (the high blocks of r4 are zero:
+// the carry passes them only where c d's block is zero).  q_i = ge_1 + ge_2 + ge_3 (one bootstrap,
+// in the subtractions' final level), the remainder is the candidate picked by q_i (half-selects
+// f(4 q_i + cand), noise 16 + 1), cleaned.  d = 0 gives q = 2^bits - 1 and r = a (every ge_c = 1),
+// tfhe's convention.  Levels per step: 4 + log2(w + 2).
 std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) {
     const uint32_t n = a.nblocks(), W = n + 1;
     Radix d1 = radix_resize(d, W);
     Radix d2 = radix_sum(e, {&d1, &d1}, W);
     Radix d3 = radix_sum(e, {&d2, &d1}, W);
-    std::vector<Blocks> nd(3);
+    static const auto LUT_ID = lut1([](uint32_t v) { return v & 3; });
+    static const auto LUT_ZERO = lut1([](uint32_t v) { return v == 0 ? 1u : 0u; });
+    std::vector<Blocks> nd(3), zf(3);  // complements 3 - (c d)_k, zero flags [(c d)_k == 0]
     {
         std::vector<PbsItem> items;
         for (const Radix* dc : {&d1, &d2, &d3})
@@ -1020,66 +1025,95 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
                 PbsItem it;
                 it.terms = {{dc->blocks[k], -1}};
                 it.cst = 3;
-                it.table = lut1([](uint32_t v) { return v & 3; });
+                it.table = LUT_ID;
+                items.push_back(it);
+                PbsItem z;
+                z.terms = {{dc->blocks[k], 1}};
+                z.table = LUT_ZERO;
+                items.push_back(z);
+            }
+        Blocks o = e.run(items);
+        for (int c = 0; c < 3; ++c)
+            for (uint32_t k = 0; k < W; ++k) {
+                nd[c].push_back(o[2 * (c * W + k)]);
+                zf[c].push_back(o[2 * (c * W + k) + 1]);
+            }
+    }
+    // P_c[w] = 3 [blocks w..W-1 of c d all zero], w = 1..n: suffix AND of the zero flags, kMaxTerms
+    // at a time (one PBS input sums at most kMaxTerms blocks): ceil(log6 W) levels, 3 for 256 bits.
+    std::vector<Blocks> P(3);
+    for (int c = 0; c < 3; ++c) P[c] = zf[c];
+    uint32_t span = 1;  // P[c][k] = AND of flags k .. k + span - 1 (clipped at W)
+    bool scaled = false;
+    while (!scaled) {
+        const bool last = span * kMaxTerms >= W;
+        std::vector<PbsItem> items;
+        for (int c = 0; c < 3; ++c)
+            for (uint32_t k = 0; k < W; ++k) {
+                PbsItem it;
+                uint32_t cnt = 0;
+                for (uint32_t j = 0; j < (uint32_t)kMaxTerms && k + j * span < W; ++j, ++cnt)
+                    it.terms.push_back({P[c][k + j * span], 1});
+                const uint32_t full = cnt, mul = last ? 3u : 1u;
+                it.table = lut1([full, mul](uint32_t v) { return v == full ? mul : 0u; });
                 items.push_back(it);
             }
         Blocks o = e.run(items);
-        for (int c = 0; c < 3; ++c) nd[c].assign(o.begin() + c * W, o.begin() + (c + 1) * W);
+        for (int c = 0; c < 3; ++c) P[c].assign(o.begin() + c * W, o.begin() + (c + 1) * W);
+        span *= kMaxTerms;
+        scaled = last;
     }
-    static const auto LUT_ID = lut1([](uint32_t v) { return v & 3; });
     std::vector<std::vector<uint32_t>> sel(4);
     for (uint32_t c = 0; c < 4; ++c) sel[c] = lut1([c](uint32_t v) { return (v >> 2) == c ? v & 3 : 0u; });
-    Blocks r(W, Block::make_trivial(0));
+    Blocks r;  // remainder, w - 1 blocks before step i
     Radix q;
     q.blocks.resize(n);
     for (int i = (int)n - 1; i >= 0; --i) {
-        Blocks r4(W);
+        const uint32_t w = n - (uint32_t)i;
+        Blocks r4(w);
         r4[0] = a.blocks[i];
-        for (uint32_t k = 1; k < W; ++k) r4[k] = r[k - 1];  // r < d < 4^n: its top block is 0
+        for (uint32_t k = 1; k < w; ++k) r4[k] = r[k - 1];
         std::vector<ColProblem> probs(3);
         for (int c = 0; c < 3; ++c) {
-            probs[c].nblocks = W + 1;  // empty top column: the carry out of position W - 1 is ge_c
-            probs[c].cols.assign(W + 1, {});
-            for (uint32_t k = 0; k < W; ++k) probs[c].cols[k] = {r4[k], nd[c][k]};
+            probs[c].nblocks = w + 2;  // column w: the high part of c d; empty top column: carry out = ge_c
+            probs[c].cols.assign(w + 2, {});
+            for (uint32_t k = 0; k < w; ++k) probs[c].cols[k] = {r4[k], nd[c][k]};
             probs[c].cols[0].push_back(Block::make_trivial(1));
+            probs[c].cols[w] = {P[c][w]};
         }
         std::vector<Blocks> cur = propagate_carries(e, probs);
         std::vector<PbsItem> items;
-        for (int c = 0; c < 3; ++c) final_items(probs[c], cur[c], W, items);
+        for (int c = 0; c < 3; ++c) final_items(probs[c], cur[c], w, items);
         {
             PbsItem qi;
-            qi.terms = {{cur[0][W - 1], 1}, {cur[1][W - 1], 1}, {cur[2][W - 1], 1}};
+            qi.terms = {{cur[0][w], 1}, {cur[1][w], 1}, {cur[2][w], 1}};
             qi.table = LUT_ID;
             items.push_back(qi);
         }
         Blocks o = e.run(items);
-        const Block qb = o[3 * W];
+        const Block qb = o[3 * w];
         q.blocks[i] = qb;
         // r_k = sum over c of [q == c] cand_c[k], exactly one term nonzero
         std::vector<PbsItem> hs;
-        for (uint32_t k = 0; k < W - 1; ++k)
+        for (uint32_t k = 0; k < w; ++k)
             for (uint32_t c = 0; c < 4; ++c) {
                 PbsItem it;
-                it.terms = {{qb, 4}, {c == 0 ? r4[k] : o[(c - 1) * W + k], 1}};
+                it.terms = {{qb, 4}, {c == 0 ? r4[k] : o[(c - 1) * w + k], 1}};
                 it.table = sel[c];
                 hs.push_back(it);
             }
         Blocks h = e.run(hs);
         std::vector<PbsItem> fin;
-        for (uint32_t k = 0; k < W - 1; ++k) {
+        for (uint32_t k = 0; k < w; ++k) {
             PbsItem it;
             for (uint32_t c = 0; c < 4; ++c) it.terms.push_back({h[4 * k + c], 1});
             it.table = LUT_MOD4();
             fin.push_back(it);
         }
-        Blocks rn = e.run(fin);
-        for (uint32_t k = 0; k < W - 1; ++k) {
-            r[k] = rn[k];
-            r[k].degree = std::min<uint32_t>(r[k].degree, 3);
-        }
-        r[W - 1] = Block::make_trivial(0);
+        r = e.run(fin);
+        for (Block& b : r) b.degree = std::min<uint32_t>(b.degree, 3);
     }
-    return {q, radix_resize(Radix{r}, n)};
+    return {q, Radix{r}};
 }
 
 Radix radix_scalar_rem(Engine& e, const Radix& a, const BigConst& d) {

@@ -37,6 +37,10 @@ timed("fheuint32_shr_enc", lambda: X >> FheUint32.try_encrypt(13, ck), lambda r:
 y = rng.getrandbits(256)
 Y = FheUint64.try_encrypt(y % 2**64, ck)
 timed("fheuint64_div_random", lambda: Y / 0xDEADBEEF, lambda r: r.decrypt(ck) == (y % 2**64) // 0xDEADBEEF)
+Z = FheUint64.try_encrypt(0xDEADBEEF12345, ck)
+timed("fheuint64_div_encrypted", lambda: Y.div_rem(Z), lambda r: (r[0].decrypt(ck), r[1].decrypt(ck)) == divmod(y % 2**64, 0xDEADBEEF12345))
+A256, D256 = FheUint256.try_encrypt(a, ck), FheUint256.try_encrypt(b >> 128, ck)
+timed("div256_by_encrypted", lambda: A256.div_rem(D256), lambda r: (r[0].decrypt(ck), r[1].decrypt(ck)) == divmod(a, b >> 128))
 d = 3; msg = bytes(32); k0 = compute_nonce(d, msg, bytes(32)); dF = BigUintFHE.new(d, ck)
 s = Schnorr()
 timed("sign_fhe_with_k0_v0_compat", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT), lambda r: r == s.sign_with_k0(msg, k0, d))
