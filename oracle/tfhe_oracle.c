@@ -215,10 +215,13 @@ uint64_t fho_f64_to_torus(double x) {
 double fho_tor_red(double v) { return fma(-0x1p64, rint(v * 0x1p-64), v); }
 
 /* one-level gadget digit of v (base 2^base_log, balanced into [-2^(bl-1), 2^(bl-1)]) as a double:
- * g = round(v / 2^(64-bl)) in [-2^bl, 2^bl], then g mod 2^bl */
+ * g = round(v / 2^(64-bl)) in [-2^bl, 2^bl], then g mod 2^bl.  The scalings are exact powers of 2. */
+static inline double tor_digit(double v, double down, double base, double ibase) {
+    const double g = rint(v * down);
+    return fma(-base, rint(g * ibase), g);
+}
 double fho_tor_digit(double v, uint32_t base_log) {
-    const double g = rint(v * ldexp(1.0, -(int)(64 - base_log)));
-    return fma(-ldexp(1.0, (int)base_log), rint(g * ldexp(1.0, -(int)base_log)), g);
+    return tor_digit(v, ldexp(1.0, -(int)(64 - base_log)), ldexp(1.0, (int)base_log), ldexp(1.0, -(int)base_log));
 }
 
 void fho_fourier_add_to_poly(double* f, double* acc) {
@@ -386,6 +389,8 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
     double* D1 = (double*)malloc(FHO_HALF * 16);
     double* O = (double*)malloc(FHO_HALF * 16);
 
+    const uint32_t bl = k->p.pbs_base_log;
+    const double down = ldexp(1.0, -(int)(64 - bl)), base = ldexp(1.0, (int)bl), ibase = ldexp(1.0, -(int)bl);
     uint32_t bt = fho_modswitch(ct_small[n]);
     for (int j = 0; j < FHO_N; ++j) {
         acc0[j] = 0.0;
@@ -399,7 +404,7 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
         for (int m = 0; m < 2; ++m) {
             double* acc = m ? acc1 : acc0;
             poly_rotate_d(acc, a, rot);
-            for (int j = 0; j < FHO_N; ++j) dig[j] = fho_tor_digit(rot[j] - acc[j], k->p.pbs_base_log);
+            for (int j = 0; j < FHO_N; ++j) dig[j] = tor_digit(rot[j] - acc[j], down, base, ibase);
             fho_dpoly_to_fourier(dig, m ? D1 : D0);
         }
         const double* bi = k->bsk_f + (size_t)i * 4 * FHO_HALF * 2;
