@@ -99,7 +99,7 @@ def pmc_traffic(batch):
     correction of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits included)"""
     try:
         d = json.load(open(PMC_SUMMARY))["pmc"][f"B={batch}"]
-        k = next(v for k, v in d.items() if "k_blind_rotate" in k and "wide" not in k)  # quad / narrow
+        k = next(v for k, v in d.items() if "k_blind_rotate_quad" in k)
         return k["hbm_side_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
     except (OSError, KeyError, StopIteration, ValueError):
         return None, None

@@ -36,9 +36,15 @@ FHE_DEV constexpr int fq(int i) {
 // stage's lane pattern; tools/lds_layout_quad*.py).  Stage s of the transform uses W[lane part +
 // step * (r mod 2^K)] with step 128 (K = 2) or 256 (K = 1): tpos of that is lane base + 132 / 264.
 constexpr int QTW_SZ = 512 + 16;
+// Zetas of the twisted forward transform that vary across lanes, in the order of
+// context.cpp:quad_zetas: stage 3 [B3], 4 [8 + B3], 5 [16 + 8j + B3], 6 [32 + B6], 7 [96 + B6],
+// 8 [160 + 64j + B6], 9 [288 + 64 r2 + 32 h + u] (B3 = 4h + (L >> 4), B6 = 32h + u, u = L >> 1, even
+// blocks only: odd ones are i times them), then 1 and -i (stage 9, lanes L0 = 0) and the uniform
+// zetas of stages 0-2 (read from global memory: Z[1], Z[2], Z[4], Z[6]).
+constexpr int QZ_LDS = 546, QZ_ONE = 544, QZ_MINUS_I = 545, QZ_UNIFORM = 546;
 FHE_DEV constexpr int tpos(int k) { return k + (k >> 5); }
 
-// DIF stage on register bit K (pairs r, r | 2^K); lb = tpos(lane part of the twiddle index).
+// Inverse (DIT) stage on register bit K (pairs r, r | 2^K); lb = tpos(lane part of the twiddle index).
 // The twiddle index is lane part + step * (r mod 2^K), step 128 (K = 2) or 256 (K = 1), with lane
 // part < step; the table's W[k + 256] = i W[k] (oracle fho_tables_init), so the upper entries of
 // those stages are moves of the lower ones (K = 0 loads its single twiddle, index < 512).
@@ -57,19 +63,6 @@ FHE_DEV void q_twiddles(cplx (&w)[4], const cplx* __restrict__ sw, int lb) {
     }
 }
 template <int K>
-FHE_DEV void q_dif(cplx (&x)[8], const cplx* __restrict__ sw, int lb) {
-    cplx w[4];
-    q_twiddles<K>(w, sw, lb);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        if (r >> K & 1) continue;
-        const int c = r | (1 << K);
-        const cplx a = x[r], b = x[c];
-        x[r] = cadd(a, b);
-        x[c] = cmul(csub(a, b), w[r & ((1 << K) - 1)]);
-    }
-}
-template <int K>
 FHE_DEV void q_dit(cplx (&x)[8], const cplx* __restrict__ sw, int lb) {
     cplx w[4];
     q_twiddles<K>(w, sw, lb);
@@ -77,6 +70,25 @@ FHE_DEV void q_dit(cplx (&x)[8], const cplx* __restrict__ sw, int lb) {
     for (int r = 0; r < 8; ++r) {
         if (r >> K & 1) continue;
         dit_bfly(x[r], x[r | (1 << K)], conj_(w[r & ((1 << K) - 1)]));
+    }
+}
+
+// Twisted forward (oracle fho_fft_forward_twisted): Cooley-Tukey stage on register bit K with the
+// block twiddles of this lane.  Block index = lane part * 2^(2-K) + (r >> (K+1)); sibling blocks
+// differ by exactly i, so K = 1 needs one zeta (za) and K = 0 two (za, zb: blocks 0 and 2 of 4).
+template <int K>
+FHE_DEV void q_ct(cplx (&x)[8], cplx za, cplx zb) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        if (r >> K & 1) continue;
+        cplx w = za;
+        if constexpr (K == 1) w = (r >> 2) ? mul_i(za) : za;
+        if constexpr (K == 0) {
+            const int b = r >> 1;
+            const cplx base = (b >> 1) ? zb : za;
+            w = (b & 1) ? mul_i(base) : base;
+        }
+        dit_bfly(x[r], x[r | (1 << K)], w);
     }
 }
 
@@ -109,10 +121,13 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
                                                               const cplx* __restrict__ bsk,  // quad layout
                                                               const cplx* __restrict__ W,
                                                               const cplx* __restrict__ ps,
+                                                              const cplx* __restrict__ zq,  // quad_zetas
                                                               uint64_t* __restrict__ out, int n) {
     __shared__ __attribute__((aligned(16))) cplx s_x[2][QX_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_w[QTW_SZ];
+    __shared__ __attribute__((aligned(16))) cplx s_z[QZ_LDS];
     for (int k = threadIdx.x; k < 512; k += 256) s_w[tpos(k)] = W[k];
+    for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[k] = zq[k];
     __syncthreads();
     const int ct = blockIdx.x;
     const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
@@ -122,6 +137,8 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
     double* rot = reinterpret_cast<double*>(reg);
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
     const uint32_t sign9 = (uint32_t)(L & 1) << 31;
+    const int B3 = 4 * h + (L >> 4), B6 = 32 * h + (L >> 1);  // twisted-transform block bases of phases B, C
+    const int z9 = 288 + 32 * h + (L >> 1);                   // stage-9 zeta of this lane (r2 = 0)
 
     // lane parts of the exchange addresses (register parts are compile-time constants)
     const int bA = fq(t);
@@ -156,10 +173,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         const gcptr bm = as_global(bsk) + ((size_t)((i * 2 + p) * 2 + p) * 16 + 8 * h) * 64 + L;
         const gcptr bo = as_global(bsk) + ((size_t)((i * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 64 + L;
 
-        // ---- rotate (X^a acc - acc) through the polynomial's region, decompose, twist
-        cplx pst[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) pst[r] = P[128 * r];
+        // ---- rotate (X^a acc - acc) through the polynomial's region, decompose
 #pragma unroll
         for (int r = 0; r < 16; ++r) rot[128 * r + t] = acc[r];
         __syncthreads();
@@ -172,20 +186,23 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         __syncthreads();  // every rotation read done before the region is reused
         cplx x[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = cmul(make_double2(dg[r], dg[r + 8]), pst[r]);
+        for (int r = 0; r < 8; ++r) x[r] = make_double2(dg[r], dg[r + 8]);
 
-        // ---- forward FFT
-        q_dif<2>(x, s_w, tpos(t));
-        q_dif<1>(x, s_w, tpos(2 * t));
-        q_dif<0>(x, s_w, tpos(4 * t));
+        // ---- forward transform: twisted Cooley-Tukey (the negacyclic twist is in the zetas)
+        {
+            const cplx* Zu = zq + QZ_UNIFORM;  // uniform: stage 0 Z[1], stage 1 Z[2], stage 2 Z[4], Z[6]
+            q_ct<2>(x, Zu[0], Zu[0]);
+            q_ct<1>(x, Zu[1], Zu[1]);
+            q_ct<0>(x, Zu[2], Zu[3]);
+        }
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bA + fq(128 * r)] = x[r];
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bB + fq(16 * r)];
-        q_dif<2>(x, s_w, tpos(8 * (L & 15)));
-        q_dif<1>(x, s_w, tpos(16 * (L & 15)));
-        q_dif<0>(x, s_w, tpos(32 * (L & 15)));
+        q_ct<2>(x, s_z[B3], s_z[B3]);
+        q_ct<1>(x, s_z[8 + B3], s_z[8 + B3]);
+        q_ct<0>(x, s_z[16 + B3], s_z[24 + B3]);
         wave_sync();  // own half: A->B reads of this wave precede its B->C writes
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bB + fq(16 * r)] = x[r];
@@ -200,9 +217,18 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
             Bq0[r] = bm[r * 64];
             Bq1[r] = bo[r * 64];
         }
-        q_dif<2>(x, s_w, tpos(64 * (L & 1)));
-        q_dif<1>(x, s_w, tpos(128 * (L & 1)));
-        q_dif<0>(x, s_w, tpos(256 * (L & 1)));
+        q_ct<2>(x, s_z[32 + B6], s_z[32 + B6]);
+        q_ct<1>(x, s_z[96 + B6], s_z[96 + B6]);
+        q_ct<0>(x, s_z[160 + B6], s_z[224 + B6]);
+        // stage 9 across lane pairs: t = zeta c on the odd lane, the even lane keeps a (x 1, exact),
+        // then (a + t, a - t) by the shared DPP step; odd registers use i zeta (1 on even lanes)
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2) {
+            const int ia = (L & 1) ? z9 + 64 * r2 : QZ_ONE;
+            const int ib = (L & 1) ? ia : QZ_MINUS_I;
+            x[2 * r2] = cmul(x[2 * r2], s_z[ia]);
+            x[2 * r2 + 1] = cmul(x[2 * r2 + 1], mul_i(s_z[ib]));
+        }
         q_stage9(x, sign9);
 
         // ---- swap Fourier digits with the other polynomial's wave of the same half, MAC with BSK
@@ -242,8 +268,9 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bA + fq(128 * r)];
         __syncthreads();  // every B->A read done before the next rotation overwrites the region
+        cplx pst[8];  // untwist factors conj(psi) 2^-10
 #pragma unroll
-        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];  // untwist factors conj(psi) 2^-10
+        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
         q_dit<0>(x, s_w, tpos(4 * t));
         q_dit<1>(x, s_w, tpos(2 * t));
         q_dit<2>(x, s_w, tpos(t));
@@ -287,10 +314,10 @@ __global__ __launch_bounds__(256) void k_bsk_to_quad(const cplx* __restrict__ sr
 
 hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const cplx* bsk_quad, const cplx* tw, const cplx* ps,
-                                    uint64_t* out, int count, int n, hipStream_t s) {
+                                    const cplx* zq, uint64_t* out, int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_blind_rotate_quad, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk_quad,
-                       tw, ps, out, n);
+                       tw, ps, zq, out, n);
     return hipGetLastError();
 }
 

@@ -107,6 +107,26 @@ FHE_DEV void xpose_dpp2(cplx (&x)[4], int L) {
     xpose_dpp<KL>(x[2], x[3], l);
 }
 
+// two stages of the twisted forward (oracle fho_fft_forward_twisted) on register bits 1 then 0: the
+// first shares one block zeta z0, the second's blocks are siblings (z1, i z1)
+FHE_DEV void ct2(cplx (&x)[4], cplx z0, cplx z1) {
+    dit_bfly(x[0], x[2], z0);
+    dit_bfly(x[1], x[3], z0);
+    dit_bfly(x[0], x[1], z1);
+    dit_bfly(x[2], x[3], mul_i(z1));
+}
+// the last two stages (phase E): stage 8 fused, stage 9 as t = z c, (a + t, a - t)
+FHE_DEV void ct2_last(cplx (&x)[4], cplx z0, cplx z1) {
+    dit_bfly(x[0], x[2], z0);
+    dit_bfly(x[1], x[3], z0);
+    const cplx t0 = cmul(x[1], z1), t1 = cmul(x[3], mul_i(z1));
+    const cplx a0 = x[0], a1 = x[2];
+    x[0] = cadd(a0, t0);
+    x[1] = csub(a0, t0);
+    x[2] = cadd(a1, t1);
+    x[3] = csub(a1, t1);
+}
+
 // two DIF stages on regs (r,r+2) then (r,r+1) with twiddles tw0 (r=0), tw1 (r=1), tw2
 FHE_DEV void dif2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
     dif(x[0], x[2], tw0);
@@ -130,6 +150,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                                                               const cplx* __restrict__ bsk,
                                                               const cplx* __restrict__ tw,   // [12][256]
                                                               const cplx* __restrict__ psiw, // [4][256]
+                                                              const cplx* __restrict__ zw,   // [10][256]
                                                               uint64_t* __restrict__ out, int n) {
     __shared__ __attribute__((aligned(16))) double s_rot[2][ROT_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
@@ -141,9 +162,11 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
 
     // loop-invariant per-thread twiddles and twist factors (held in registers)
-    cplx T[12], PS[4];
+    cplx T[12], PS[4], ZT[10];
 #pragma unroll
     for (int s = 0; s < 12; ++s) T[s] = tw[s * 256 + t];
+#pragma unroll
+    for (int s = 0; s < 10; ++s) ZT[s] = zw[s * 256 + t];
 #pragma unroll
     for (int r = 0; r < 4; ++r) PS[r] = psiw[r * 256 + t];
 
@@ -204,30 +227,24 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 const uint32_t c = u & 2047u;
                 d2[hh] = tor_digit<23>(neg_if(rot_me[c + (c >> 2)], (u >> 11) << 31) - acc[rr]);
             }
-            x[r] = cmul(make_double2(d2[0], d2[1]), PS[r]);
+            x[r] = make_double2(d2[0], d2[1]);
         }
 
-        // ---- forward FFT: A (stages 0,1) -> B -> C -> D (wave-private) -> E (cross-wave)
-        dif2(x, T[0], T[1], T[2]);
+        // ---- forward transform (twisted: no twist multiply): A (stages 0,1) -> B -> C -> D
+        // (wave-private) -> E (cross-wave)
+        ct2(x, ZT[0], ZT[1]);
         xpose_AB(x);                 // A -> B: regs <-> lane bits 5,4
-        dif2(x, T[3], T[4], T[5]);
+        ct2(x, ZT[2], ZT[3]);
         xpose_dpp2<3, 2>(x, L);      // B -> C: regs <-> lane bits 3,2
-        dif2(x, T[6], T[7], T[8]);
+        ct2(x, ZT[4], ZT[5]);
         xpose_dpp2<1, 0>(x, L);      // C -> D: regs <-> lane bits 1,0
-        dif2(x, T[9], T[10], T[11]);
+        ct2(x, ZT[6], ZT[7]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) cross[xD + fx(4 * r)] = x[r];
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = cross[xE + fx(r)];
-        // phase E: stage 8 (r=1 twiddle i), stage 9 (twiddle 1)
-        {
-            cplx a0 = x[0], c0 = x[2], a1 = x[1], c1 = x[3];
-            x[0] = cadd(a0, c0); x[2] = csub(a0, c0);
-            x[1] = cadd(a1, c1); x[3] = mul_i(csub(a1, c1));
-            a0 = x[0]; c0 = x[1]; x[0] = cadd(a0, c0); x[1] = csub(a0, c0);
-            a1 = x[2]; c1 = x[3]; x[2] = cadd(a1, c1); x[3] = csub(a1, c1);
-        }
+        ct2_last(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
 
         // ---- swap Fourier digits between the two polynomials, pointwise MAC
         cplx* dx_me = s_dx[p] + 4 * q * 64 + L;
@@ -288,10 +305,10 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 
 hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const double2* bsk, const double2* tw, const double2* psiw,
-                                    uint64_t* out, int count, int n, hipStream_t s) {
+                                    const double2* zw, uint64_t* out, int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_blind_rotate_wide, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk, tw,
-                       psiw, out, n);
+                       psiw, zw, out, n);
     return hipGetLastError();
 }
 

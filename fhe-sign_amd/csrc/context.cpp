@@ -32,6 +32,57 @@ void fft_tables(std::vector<double2>* W, std::vector<double2>* psi) {
     (*psi)[0] = make_double2(1.0, 0.0);
 }
 
+// zeta(s, b) at [2^s + b] of the twisted forward transform: same expressions and order as
+// oracle/tfhe_oracle.c:fho_tables_init (exp(i pi (4 bitrev_s(b) + 1) / 2^(s+2)), odd b = i * even)
+void zeta_table(std::vector<double2>* Z) {
+    const double pi = 3.14159265358979323846264338327950288;
+    Z->assign(1024, make_double2(0.0, 0.0));
+    for (int st = 0; st < 10; ++st)
+        for (uint32_t b = 0; b < (1u << st); b += 2) {
+            uint32_t br = 0;
+            for (int i = 0; i < st; ++i) br |= ((b >> i) & 1u) << (st - 1 - i);
+            const double a = pi * (double)(4 * br + 1) / (double)(1u << (st + 2));
+            const double2 z = make_double2(std::cos(a), std::sin(a));
+            (*Z)[(1u << st) + b] = z;
+            if (st > 0) (*Z)[(1u << st) + b + 1] = make_double2(-z.y, z.x);
+        }
+}
+
+// br_quad.hip zeta layout (QZ_*): lane-varying zetas of stages 3-9 (even blocks), 1, -i, uniform ones
+void quad_zetas(const std::vector<double2>& Z, std::vector<double2>* q) {
+    q->assign(550, make_double2(0.0, 0.0));
+    for (int B3 = 0; B3 < 8; ++B3) {
+        (*q)[B3] = Z[8 + B3];
+        (*q)[8 + B3] = Z[16 + 2 * B3];
+        for (int j = 0; j < 2; ++j) (*q)[16 + 8 * j + B3] = Z[32 + 4 * B3 + 2 * j];
+    }
+    for (int B6 = 0; B6 < 64; ++B6) {
+        (*q)[32 + B6] = Z[64 + B6];
+        (*q)[96 + B6] = Z[128 + 2 * B6];
+        for (int j = 0; j < 2; ++j) (*q)[160 + 64 * j + B6] = Z[256 + 4 * B6 + 2 * j];
+    }
+    for (int r2 = 0; r2 < 4; ++r2)
+        for (int h = 0; h < 2; ++h)
+            for (int u = 0; u < 32; ++u) (*q)[288 + 64 * r2 + 32 * h + u] = Z[512 + 256 * h + 8 * u + 2 * r2];
+    (*q)[544] = make_double2(1.0, 0.0);
+    (*q)[545] = make_double2(0.0, -1.0);
+    (*q)[546] = Z[1];
+    (*q)[547] = Z[2];
+    (*q)[548] = Z[4];
+    (*q)[549] = Z[6];
+}
+
+// br_wide.hip: per-thread zetas of the twisted forward, [10][256] (t = 64 q + L): phases A..E, two each
+void wide_zetas(const std::vector<double2>& Z, std::vector<double2>* zw) {
+    zw->assign(10 * 256, make_double2(0.0, 0.0));
+    for (int t = 0; t < 256; ++t) {
+        const int q = t >> 6, L = t & 63;
+        const int idx[10] = {1, 2, 4 + (L >> 4), 8 + 2 * (L >> 4), 16 + (L >> 2), 32 + 2 * (L >> 2),
+                             64 + L, 128 + 2 * L, 256 + 64 * q + L, 512 + 128 * q + 2 * L};
+        for (int s = 0; s < 10; ++s) (*zw)[s * 256 + t] = Z[idx[s]];
+    }
+}
+
 void lane_twiddles(const std::vector<double2>& W, std::vector<double2>* Wl) {
     // [slot][lane] copies of W entries, slot layout of device_math.h:tw_slot
     Wl->assign(30 * 64, make_double2(0.0, 0.0));
@@ -210,15 +261,10 @@ hipError_t fhe_ctx::keyswitch(const uint64_t* in, const fhe::PbsDesc* desc, size
 
 hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_idx, uint64_t* out, size_t count) {
     if ((int)count <= wide_threshold)
-        return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide, out,
+        return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide, d_zeta_wide, out,
                                         (int)count, (int)p.n, stream);
-    if (br_kernel == FHE_BR_QUAD)
-        return launch_blind_rotate_quad(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_quad, d_tw_quad, d_psi_quad, out,
-                                        (int)count, (int)p.n, stream);
-    if (desc)
-        return launch_blind_rotate_desc(d_ms, ms_stride, desc, d_luts, d_bsk, d_W, d_psi, (int)count, (int)p.n,
-                                        stream);
-    return launch_blind_rotate(d_ms, ms_stride, lut_idx, d_luts, d_bsk, d_W, d_psi, out, (int)count, (int)p.n, stream);
+    return launch_blind_rotate_quad(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_quad, d_tw_quad, d_psi_quad,
+                                    d_zeta_quad, out, (int)count, (int)p.n, stream);
 }
 
 // =========================================================================== C ABI (core)
@@ -320,8 +366,16 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
         return FHE_ERR_HIP;
     }
     for (auto& ev : c->ev) FHE_HIP_CHECK(hipEventCreate(&ev));
-    std::vector<double2> W0, W, psi, tww, psiw, twq, psq;
+    std::vector<double2> W0, W, psi, tww, psiw, twq, psq, Z, zq;
     fft_tables(&W0, &psi);
+    zeta_table(&Z);
+    quad_zetas(Z, &zq);
+    std::vector<double2> zw;
+    wide_zetas(Z, &zw);
+    FHE_HIP_CHECK(hipMalloc(&c->d_zeta_wide, zw.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMemcpy(c->d_zeta_wide, zw.data(), zw.size() * sizeof(double2), hipMemcpyHostToDevice));
+    FHE_HIP_CHECK(hipMalloc(&c->d_zeta_quad, zq.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMemcpy(c->d_zeta_quad, zq.data(), zq.size() * sizeof(double2), hipMemcpyHostToDevice));
     lane_twiddles(W0, &W);
     wide_tables(W0, psi, &tww, &psiw);
     quad_tables(W0, psi, &twq, &psq);
@@ -350,7 +404,7 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     c->engine = nullptr;
     c->release_comm();
     void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
-                    c->d_psi_quad, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
+                    c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)
@@ -507,7 +561,12 @@ int fhe_ctx_set_ks_kernel(fhe_ctx* c, int kind) {
 }
 
 int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
-    if (!c || (kind != FHE_BR_NARROW && kind != FHE_BR_QUAD)) return FHE_ERR_INVALID;
+    if (!c) return FHE_ERR_INVALID;
+    if (kind == FHE_BR_NARROW) {
+        set_error("the 2-wave blind-rotate kernel (FHE_BR_NARROW) is retired; FHE_BR_QUAD is the throughput kernel");
+        return FHE_ERR_INVALID;
+    }
+    if (kind != FHE_BR_QUAD) return FHE_ERR_INVALID;
     c->br_kernel = kind;
     return FHE_OK;
 }

@@ -93,179 +93,8 @@ __global__ __launch_bounds__(256) void k_keyswitch(const uint64_t* __restrict__ 
     }
 }
 
-// ============================================================================ blind rotate
-// One workgroup (2 waves) per ciphertext.  Wave w owns GLWE polynomial w (0 = mask, 1 = body):
-// its accumulator lives in registers (lane L holds coefficients L + 64 t, t < 32), its FFT runs
-// in registers with two swizzled LDS exchanges, and the two waves swap their Fourier-domain
-// digit polynomials through LDS once per CMUX.
-constexpr int BR_PBS_BL = 23;
-constexpr int kRing = 2;
-constexpr int kBrGroup = 1;  // ciphertexts per workgroup; measured per 8192: G=1 101 ms, G=2 157, G=4 108
-
-// out[R] = own digit x BSK row w + partner digit x row 1 - w (mac2, symmetric like the oracle), in place.
-// The BSK rows stream through a register ring of depth kRing (Bq0/Bq1 hold R < kRing on entry): each
-// step consumes slot R % kRing and refills it with R + kRing.  kRing = 2 is what fits beside the
-// accumulator and FFT state in 256 VGPRs (deeper rings spill: measured 146 ms vs 102 ms per 8192).
-FHE_DEV void pointwise_mac(cplx (&x)[16], const cplx* __restrict__ other, cplx (&Bq0)[kRing], cplx (&Bq1)[kRing],
-                           gcptr b0, gcptr b1) {
-#pragma unroll
-    for (int R = 0; R < 16; ++R) {
-        const cplx B0 = Bq0[R % kRing], B1 = Bq1[R % kRing];
-        if (R + kRing < 16) {
-            Bq0[R % kRing] = b0[(R + kRing) * 64];
-            Bq1[R % kRing] = b1[(R + kRing) * 64];
-        }
-        x[R] = mac2(x[R], B0, other[R * 64], B1);  // symmetric: own digit x row w, other x row 1 - w
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// G ciphertexts per workgroup run in lockstep (their per-iteration barriers are shared), so the
-// G reads of each BSK slice land together and are served once from L1/L2 instead of G times.
-// Direct (lut_idx/out) or descriptor-driven (desc) launches share one instantiation: desc is a
-// uniform runtime choice read only before and after the CMUX loop.  (Two template copies of the
-// loop were scheduled differently enough that the descriptor copy ran 35% slower.)
-template <int G>
-__global__ __launch_bounds__(128 * G, 2) void k_blind_rotate(const uint64_t* __restrict__ ms, int ms_stride,
-                                                         const uint32_t* __restrict__ lut_idx,
-                                                         const PbsDesc* __restrict__ desc,
-                                                         const uint64_t* __restrict__ luts,
-                                                         const cplx* __restrict__ bsk,
-                                                         const cplx* __restrict__ W,
-                                                         const cplx* __restrict__ psi,
-                                                         uint64_t* __restrict__ out, int n, int count) {
-    __shared__ __attribute__((aligned(16))) cplx lds[2 * G][FFT_SCRATCH];
-    const int g = threadIdx.x >> 7;
-    const bool live = G == 1 || (int)blockIdx.x * G + g < count;
-    const int ct = live ? (int)blockIdx.x * G + g : count - 1;  // tail slots recompute the last one
-    const int w = (threadIdx.x >> 6) & 1, L = threadIdx.x & 63;
-    cplx* sc = lds[2 * g + w];
-    cplx* sc_other = lds[2 * g + (w ^ 1)];
-    double* scu = reinterpret_cast<double*>(sc);
-    const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
-
-    double acc[32];  // f64 torus representatives (oracle fho_blind_rotate)
-    {
-        const uint32_t bt = modswitch_2n(a_ct[n]);
-        const int rot = (int)((4096u - bt) & 4095u);  // X^{-b}
-        const uint64_t* lut = luts + (size_t)(desc ? desc[ct].lut : lut_idx[ct]) * 2048;
-#pragma unroll
-        for (int t = 0; t < 32; ++t) {
-            double v = 0.0;
-            if (w == 1) {
-                const uint32_t u = (uint32_t)(L + 64 * t - rot) & 4095u;
-                v = neg_if((double)(int64_t)lut[u & 2047u], (u >> 11) << 31);
-            }
-            acc[t] = v;
-        }
-    }
-
-    uint32_t a_next = modswitch_2n(a_ct[0]);
-    for (int i = 0; i < n; ++i) {
-        const uint32_t a = a_next;
-        a_next = modswitch_2n(a_ct[i + 1]);
-        // X^0 - 1 = 0: the external product is exactly zero (skipping it is bit-identical); only a
-        // lone ciphertext may skip, a lockstep group shares its barriers
-        if (G == 1 && a == 0) continue;
-        // Tables are re-derived every iteration (kept out of the register file across iterations)
-        // and every batch of loads is issued well ahead of its use; sched_barriers pin the order.
-        const cplx* Wg = W;
-        const cplx* Pg = psi;
-        asm volatile("" : "+s"(Wg), "+s"(Pg));
-        const gcptr Wl = as_global(Wg) + L, Pl = as_global(Pg) + L;
-        // row w multiplies this wave's own digit polynomial, row 1 - w the partner's (mac2 is symmetric)
-        const gcptr b0 = as_global(bsk) + ((size_t)((i * 2 + w) * 2 + w) * 16) * 64 + L;
-        const gcptr b1 = as_global(bsk) + ((size_t)((i * 2 + (w ^ 1)) * 2 + w) * 16) * 64 + L;
-
-        // ---- twist factors in flight while the accumulator goes through LDS
-        cplx ps[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) ps[t] = Pl[64 * t];
-        __builtin_amdgcn_sched_barrier(0);
-
-        // ---- rotate, subtract, decompose, twist
-#pragma unroll
-        for (int t = 0; t < 32; ++t) scu[L + 64 * t] = acc[t];
-        wave_sync();
-        cplx x[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            double d2[2];
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int tt = t + 16 * hh;
-                // (X^a acc)[j]: u = (j - a) mod 2N -> acc[u mod N], negated iff u >= N
-                const uint32_t u = (uint32_t)(L + 64 * tt - (int)a) & 4095u;
-                d2[hh] = tor_digit<BR_PBS_BL>(neg_if(scu[u & 2047u], (u >> 11) << 31) - acc[tt]);
-            }
-            x[t] = cmul(make_double2(d2[0], d2[1]), ps[t]);
-            if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-        }
-        wave_sync();
-
-        // ---- forward FFT of this wave's digit polynomial
-        dif_phase_a(x, Wl);
-        xchg_a_to_b(x, sc, L);
-        dif_phase_b(x, Wl);
-        // head of the BSK ring, in flight across the B->C exchange, phase C and the barrier
-        cplx Bq0[kRing], Bq1[kRing];
-#pragma unroll
-        for (int R = 0; R < kRing; ++R) {
-            Bq0[R] = b0[R * 64];
-            Bq1[R] = b1[R * 64];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        xchg_b_to_c(x, sc, L);
-        dif_phase_c(x);
-
-        // ---- swap Fourier digits with the partner wave, pointwise MAC with the BSK
-#pragma unroll
-        for (int R = 0; R < 16; ++R) sc[R * 64 + L] = x[R];
-        __syncthreads();
-        pointwise_mac(x, sc_other + L, Bq0, Bq1, b0, b1);
-        __syncthreads();
-
-        // ---- inverse FFT (untwist factors issued before its last stage)
-        dit_phase_c(x);
-        xchg_c_to_b(x, sc, L);
-        dit_phase_b(x, Wl);
-        xchg_b_to_a(x, sc, L);
-        dit_stage<3>(x, Wl);
-        dit_stage<2>(x, Wl);
-        dit_stage<1>(x, Wl);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) ps[t] = Pl[64 * t];
-        __builtin_amdgcn_sched_barrier(0);
-        dit_stage<0>(x, Wl);
-
-        // ---- untwist, accumulate
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const cplx p = ps[t];
-            const cplx u = make_double2(p.x * 0.0009765625, -p.y * 0.0009765625);
-            const cplx y = cmul(x[t], u);
-            acc[t] = tor_red(acc[t] + y.x);
-            acc[t + 16] = tor_red(acc[t + 16] + y.y);
-            if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-
-    // ---- sample extract (coefficient 0)
-    if (!live) return;
-    uint64_t* o = desc ? desc[ct].dst : out + (size_t)ct * 2049;
-    if (w == 0) {
-#pragma unroll
-        for (int t = 0; t < 32; ++t) {
-            const int j = L + 64 * t;
-            const uint64_t v = f64_to_torus(acc[t]);
-            if (j == 0) o[0] = v;
-            else o[2048 - j] = 0ull - v;
-        }
-    } else if (L == 0) {
-        o[2048] = f64_to_torus(acc[0]);
-    }
-}
+// (The 2-wave blind-rotate kernel that lived here was retired when the digit transform became the
+// twisted forward; br_quad.hip / br_wide.hip are the blind-rotate kernels.)
 
 // ============================================================================ BSK -> Fourier
 // One wave per polynomial: [n][row][poly][2048] u64 -> [n][row][poly][R][L] complex (phase C).
@@ -322,26 +151,6 @@ hipError_t launch_keyswitch_desc(const PbsDesc* desc, int count, const uint64_t*
     }
     dim3 grid((count + KS_C - 1) / KS_C, (n + 1 + 255) / 256, z);
     hipLaunchKernelGGL(k_keyswitch<true>, grid, dim3(256), 0, s, nullptr, desc, count, ksk, small, ks_stride, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_blind_rotate(const uint64_t* ms, int ms_stride, const uint32_t* lut_idx,
-                               const uint64_t* luts, const cplx* bsk, const cplx* W,
-                               const cplx* psi, uint64_t* out, int count, int n, hipStream_t s) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL((k_blind_rotate<kBrGroup>), dim3((count + kBrGroup - 1) / kBrGroup),
-                       dim3(128 * kBrGroup), 0, s, ms, ms_stride, lut_idx, nullptr, luts, bsk, W, psi, out, n,
-                       count);
-    return hipGetLastError();
-}
-
-hipError_t launch_blind_rotate_desc(const uint64_t* ms, int ms_stride, const PbsDesc* desc,
-                                    const uint64_t* luts, const cplx* bsk, const cplx* W,
-                                    const cplx* psi, int count, int n, hipStream_t s) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL((k_blind_rotate<kBrGroup>), dim3((count + kBrGroup - 1) / kBrGroup),
-                       dim3(128 * kBrGroup), 0, s, ms, ms_stride, nullptr, desc, luts, bsk, W, psi, nullptr, n,
-                       count);
     return hipGetLastError();
 }
 

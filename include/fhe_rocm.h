@@ -109,8 +109,9 @@ int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
-/* Throughput blind-rotate kernel for levels above the threshold: 2 waves per ciphertext
- * (FHE_BR_NARROW) or 4 (FHE_BR_QUAD, default).  All kernels produce identical bits. */
+/* Throughput blind-rotate kernel for levels above the threshold: 4 waves per ciphertext
+ * (FHE_BR_QUAD, the default and only one; FHE_BR_NARROW, the retired 2-wave kernel, is refused with
+ * FHE_ERR_INVALID).  The throughput and latency kernels produce identical bits. */
 #define FHE_BR_NARROW 0
 #define FHE_BR_QUAD 1
 int fhe_ctx_set_br_kernel(fhe_ctx* ctx, int kind);

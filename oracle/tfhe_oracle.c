@@ -93,7 +93,14 @@ int64_t fho_rng_tuniform(fho_rng* r, uint32_t b) {
 /* ------------------------------------------------------------------ FFT tables */
 static double g_tw[512 * 2];
 static double g_psi[1024 * 2];
+static double g_zeta[1024 * 2];
 static int g_tables_ready = 0;
+
+static uint32_t bitrev(uint32_t b, int bits) {
+    uint32_t r = 0;
+    for (int i = 0; i < bits; ++i) r |= ((b >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
 
 void fho_tables_init(void) {
     if (g_tables_ready) return;
@@ -117,11 +124,27 @@ void fho_tables_init(void) {
         g_psi[2 * j + 1] = sin(a);
     }
     g_psi[0] = 1.0; g_psi[1] = 0.0;
+    /* zeta(s, b) at [2^s + b]: the twiddle of block b in stage s of the twisted (negacyclic) forward
+     * transform, exp(i pi (4 bitrev_s(b) + 1) / 2^(s+2)); the odd block of a sibling pair is i times
+     * the even one, defined exactly (zeta[2^s + b + 1] = (-zeta.im, zeta.re)) */
+    for (int st = 0; st < 10; ++st) {
+        for (uint32_t b = 0; b < (1u << st); b += 2) {
+            const double a = pi * (double)(4 * bitrev(b, st) + 1) / (double)(1u << (st + 2));
+            double* z = g_zeta + 2 * ((1u << st) + b);
+            z[0] = cos(a);
+            z[1] = sin(a);
+            if (st > 0) {
+                z[2] = -z[1];
+                z[3] = z[0];
+            }
+        }
+    }
     g_tables_ready = 1;
 }
 
 const double* fho_twiddles(void) { fho_tables_init(); return g_tw; }
 const double* fho_twist(void) { fho_tables_init(); return g_psi; }
+const double* fho_zetas(void) { fho_tables_init(); return g_zeta; }
 
 /* (x) * (w): the single complex-multiply formula used everywhere (GPU identical) */
 static inline void cmul(double xr, double xi, double wr, double wi, double* yr, double* yi) {
@@ -144,6 +167,38 @@ void fho_fft_forward(double* x) {
                 const double* w = g_tw + 2 * (j << s);
                 p[0] = sr; p[1] = si;
                 cmul(dr, di, w[0], w[1], &q[0], &q[1]);
+            }
+        }
+    }
+}
+
+/* Twisted forward transform of the blind rotation's digit polynomials (no separate twist): the
+ * negacyclic split X^1024 - i -> (X^512 - z)(X^512 + z) -> ..., i.e. radix-2 Cooley-Tukey stages
+ * s = 0..9 on natural-order input, block b of stage s using zeta(s, b); output in the same
+ * bit-reversed order and the same mathematical values as twist + fho_fft_forward.  Butterfly
+ * (a, c) -> (p, m), p = a + z c with two fmas per component, m = 2a - p; the last stage (span 1)
+ * is t = z c (cmul), (a + t, a - t). */
+void fho_fft_forward_twisted(double* x) {
+    fho_tables_init();
+    for (int st = 0; st < 10; ++st) {
+        const int h = 512 >> st;
+        for (int b = 0; b < (1 << st); ++b) {
+            const double* z = g_zeta + 2 * ((1 << st) + b);
+            for (int j = 0; j < h; ++j) {
+                double* p = x + 2 * (2 * h * b + j);
+                double* q = p + 2 * h;
+                const double ar = p[0], ai = p[1], cr = q[0], ci = q[1];
+                if (st == 9) {
+                    double tr, ti;
+                    cmul(cr, ci, z[0], z[1], &tr, &ti);
+                    p[0] = ar + tr; p[1] = ai + ti;
+                    q[0] = ar - tr; q[1] = ai - ti;
+                    continue;
+                }
+                const double pr = fma(z[0], cr, fma(-z[1], ci, ar));
+                const double pi = fma(z[0], ci, fma(z[1], cr, ai));
+                p[0] = pr; p[1] = pi;
+                q[0] = fma(2.0, ar, -pr); q[1] = fma(2.0, ai, -pi);
             }
         }
     }
@@ -186,12 +241,13 @@ void fho_poly_to_fourier(const uint64_t* poly, double* out) {
     fho_fft_forward(out);
 }
 
-/* digit polynomial (integer-valued doubles) -> Fourier */
+/* digit polynomial (integer-valued doubles) -> Fourier, twisted forward transform */
 void fho_dpoly_to_fourier(const double* poly, double* out) {
-    fho_tables_init();
-    for (int j = 0; j < 1024; ++j)
-        cmul(poly[j], poly[j + 1024], g_psi[2 * j], g_psi[2 * j + 1], &out[2 * j], &out[2 * j + 1]);
-    fho_fft_forward(out);
+    for (int j = 0; j < 1024; ++j) {
+        out[2 * j] = poly[j];
+        out[2 * j + 1] = poly[j + 1024];
+    }
+    fho_fft_forward_twisted(out);
 }
 
 /* round(x) mod 2^64, x finite.  rint = IEEE round-half-even (GPU: v_rndne_f64). */

@@ -93,6 +93,8 @@ void fho_fft_inverse(double* x /* HALF complex, output unscaled */);
 /* standard-domain torus polynomial (N u64) -> Fourier (HALF complex, bit-reversed) */
 void fho_poly_to_fourier(const uint64_t* poly, double* out);
 /* small signed integer polynomial -> Fourier */
+void fho_fft_forward_twisted(double* x);
+const double* fho_zetas(void);
 void fho_dpoly_to_fourier(const double* poly, double* out);
 /* Fourier (bit-reversed) -> torus polynomial ADDED into an f64 accumulator: acc = red(acc + y) */
 void fho_fourier_add_to_poly(double* f /* clobbered */, double* acc);

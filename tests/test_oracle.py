@@ -42,6 +42,17 @@ def test_fft_matches_numpy_dft():
     assert np.max(np.abs(f[rev] - ref)) < 1e-9
 
 
+def test_twisted_forward_equals_twist_then_dif():
+    """The blind rotation's digit transform (negacyclic split with zeta twiddles, no separate twist)
+    computes the same values, in the same bit-reversed order, as twist by psi^j + the DIF transform
+    the bootstrapping key is converted with (different rounding, same mathematics)."""
+    x = rng.integers(-2**22, 2**22, 1024) + 1j * rng.integers(-2**22, 2**22, 1024)
+    psi = np.exp(1j * np.pi * np.arange(1024) / 2048)
+    a = oracle.fft_forward_twisted(x)
+    b = oracle.fft_forward(x * psi)
+    assert np.max(np.abs(a - b)) < 1e-9 * np.max(np.abs(b))
+
+
 def test_f64_to_torus():
     assert oracle.f64_to_torus(0.0) == 0
     assert oracle.f64_to_torus(-0.0) == 0

@@ -87,28 +87,25 @@ def test_pbs_empty_batch(env):
     assert out.shape == (0, 2049)
 
 
-def test_wide_and_narrow_kernels_bit_identical(env):
-    """The latency kernel (br_wide.hip, 8 waves per ciphertext) and both throughput kernels (2 waves,
-    pbs_kernels.hip; 4 waves, br_quad.hip) implement the same arithmetic: identical output words,
-    equal to the oracle.  37 ciphertexts: a ragged batch with every LUT."""
+def test_wide_and_quad_kernels_bit_identical(env):
+    """The latency kernel (br_wide.hip, 8 waves per ciphertext) and the throughput kernel (4 waves,
+    br_quad.hip) implement the same arithmetic: identical output words, equal to the oracle.  37
+    ciphertexts: a ragged batch with every LUT.  The retired 2-wave kernel is refused loudly."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = [ctx.lut(t) for t in tables]
     r = ok.rng(777)
     cts = np.stack([ok.encrypt(r, i % 16) for i in range(37)])
     lut_ids = np.array([ids[i % len(ids)] for i in range(37)], np.uint32)
+    with pytest.raises(Exception, match="retired"):
+        ctx.set_br_kernel(0)
     try:
         ctx.set_wide_threshold(0)
-        ctx.set_br_kernel(0)
-        narrow = ctx.pbs(cts, lut_ids)
-        ctx.set_br_kernel(1)
         quad = ctx.pbs(cts, lut_ids)
         ctx.set_wide_threshold(1 << 30)
         wide = ctx.pbs(cts, lut_ids)
     finally:
         ctx.set_wide_threshold(256)
-        ctx.set_br_kernel(1)
-    assert np.array_equal(narrow, wide)
     assert np.array_equal(quad, wide)
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(wide[:6], ref)

@@ -1,5 +1,5 @@
 """Blind-rotate kernel choice: batch-size sweep of the latency kernel (wide, 8 waves/ciphertext) vs
-the throughput kernels (narrow: 2 waves, quad: 4 waves)."""
+the throughput kernel (quad: 4 waves)."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
@@ -16,9 +16,8 @@ ctx.h2d(d_in, cts); ctx.h2d(d_lut, np.full(Bmax, lid, np.uint32))
 ctx.enable_timing(True)
 for B in [1, 16, 64, 128, 256, 320, 384, 512, 640, 768, 1024, 2048, 4096, 8192]:
     res = {}
-    for name, thr, kern in (("wide", 1 << 30, 1), ("narrow", 0, 0), ("quad", 0, 1)):
+    for name, thr in (("wide", 1 << 30), ("quad", 0)):
         ctx.set_wide_threshold(thr)
-        ctx.set_br_kernel(kern)
         ctx.pbs_device(d_in, B, d_lut, d_out); ctx.sync()
         best = 1e9
         for _ in range(2 if B >= 2048 else 3):
@@ -28,5 +27,5 @@ for B in [1, 16, 64, 128, 256, 320, 384, 512, 640, 768, 1024, 2048, 4096, 8192]:
         res[name] = (ks, best)
         out = np.zeros((B, 2049), np.uint64); ctx.d2h(out, d_out)
         assert all(ck.decrypt_block(out[i]) == ((i % 64) % 16 + 1) % 16 for i in range(0, B, max(1, B // 16)))
-    print("B=%5d  ks %.3f ms | br wide %.3f  narrow %.3f  quad %.3f ms" %
-          (B, res["quad"][0], res["wide"][1], res["narrow"][1], res["quad"][1]), flush=True)
+    print("B=%5d  ks %.3f ms | br wide %.3f  quad %.3f ms" % (B, res["quad"][0], res["wide"][1], res["quad"][1]),
+          flush=True)
