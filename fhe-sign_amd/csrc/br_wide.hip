@@ -154,7 +154,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                                                               uint64_t* __restrict__ out, int n) {
     __shared__ __attribute__((aligned(16))) double s_rot[2][ROT_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
-    __shared__ __attribute__((aligned(16))) cplx s_dx[2][1024];
+    __shared__ __attribute__((aligned(16))) cplx s_inv[2][CROSS_SZ];  // inverse E -> D exchange
 
     const int ct = blockIdx.x;
     const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
@@ -242,20 +242,24 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 4; ++r) cross[xD + fx(4 * r)] = x[r];
         __syncthreads();
+        // phase E reads both polynomials' regions: stages 8, 9 of the other polynomial's digits are
+        // recomputed here (identical operations to its own waves') instead of swapping the results
+        // through LDS -- one barrier and one exchange less per CMUX
+        cplx y[4];
+        {
+            const cplx* cross_other = s_cross[p ^ 1];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = cross[xE + fx(r)];
-        ct2_last(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
-
-        // ---- swap Fourier digits between the two polynomials, pointwise MAC
-        cplx* dx_me = s_dx[p] + 4 * q * 64 + L;
-        const cplx* dx_other = s_dx[p ^ 1] + 4 * q * 64 + L;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dx_me[r * 64] = x[r];
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            x[r] = mac2(x[r], B0[r], dx_other[r * 64], B1[r]);  // symmetric: own row p, other row 1 - p
+            for (int r = 0; r < 4; ++r) {
+                x[r] = cross[xE + fx(r)];
+                y[r] = cross_other[xE + fx(r)];
+            }
         }
+        ct2_last(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
+        ct2_last(y, ZT[8], ZT[9]);
+
+        // ---- pointwise MAC (symmetric: own digit x row p, other digit x row 1 - p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], B0[r], y[r], B1[r]);
 
         // ---- inverse FFT: E -> D (cross-wave) -> C -> B -> A (wave-private)
         {
@@ -265,11 +269,13 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             dit_bfly_unit(x[0], x[2], x[2]);
             dit_bfly_unit(x[1], x[3], mul_negi(x[3]));
         }
+        // through a region of its own: the other polynomial's waves may still be reading `cross`
+        cplx* inv = s_inv[p];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cross[xE + fx(r)] = x[r];
+        for (int r = 0; r < 4; ++r) inv[xE + fx(r)] = x[r];
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = cross[xD + fx(4 * r)];
+        for (int r = 0; r < 4; ++r) x[r] = inv[xD + fx(4 * r)];
         dit2(x, T[9], T[10], T[11]);
         xpose_dpp2<1, 0>(x, L);      // D -> C
         dit2(x, T[6], T[7], T[8]);
