@@ -24,15 +24,17 @@
 namespace fhe {
 
 namespace {
-// cross-wave region per polynomial (1024 entries + pad): weights of idx-bits 0..9
-constexpr int WX[10] = {1, 2, 4, 8, 16, 32, 66, 131, 264, 528};
-constexpr int CROSS_SZ = 1056;
-constexpr int ROT_SZ = 2560;  // u64 accumulator staging: pos(c) = c + (c >> 2)
+// cross-wave regions: an XOR swizzle pos = A idx over GF(2) (bijective, no padding) under which the
+// D-side stores/loads and E-side loads/stores are all conflict-free by the gfx950 lane-group rules
+// (tools/lds_layout_wide3.py; the additive map of earlier rounds was 4-way on three of the four)
+constexpr int XA[10] = {0x038, 0x190, 0x144, 0x184, 0x001, 0x002, 0x004, 0x008, 0x040, 0x200};
+constexpr int CROSS_SZ = 1024;
+constexpr int ROT_SZ = 2560;  // accumulator staging (f64): pos(c) = c + (c >> 2)
 
 FHE_DEV constexpr int fx(int x) {
-    return ((x & 1) ? WX[0] : 0) + ((x & 2) ? WX[1] : 0) + ((x & 4) ? WX[2] : 0) + ((x & 8) ? WX[3] : 0) +
-           ((x & 16) ? WX[4] : 0) + ((x & 32) ? WX[5] : 0) + ((x & 64) ? WX[6] : 0) + ((x & 128) ? WX[7] : 0) +
-           ((x & 256) ? WX[8] : 0) + ((x & 512) ? WX[9] : 0);
+    int p = 0;
+    for (int k = 0; k < 10; ++k) p |= (__builtin_popcount(x & XA[k]) & 1) << k;
+    return p;
 }
 
 // radix-2 DIF pair (a, c) -> (a + c, (a - c) w) ; DIT pair (a, c) -> (a + c w~, a - c w~)
@@ -91,6 +93,35 @@ FHE_DEV void xpose_dpp(cplx& X, cplx& Y, bool hi) {
     X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
     Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
 }
+// K in 2..3: the lanes with lane bit K set are whole 4-lane DPP banks, so each half of the
+// transpose is ONE bank-masked DPP move (disabled lanes keep the old value): 2 ops per dword, no select
+template <int K>
+FHE_DEV void xpose_dpp_banked(cplx& X, cplx& Y) {
+    static_assert(K == 2 || K == 3, "bank-aligned lane bits only");
+    constexpr int SH = 1 << K;
+    constexpr int HI = K == 3 ? 0xC : 0xA, LO = K == 3 ? 0x3 : 0x5;  // banks with lane bit K = 1 / 0
+    uint32_t x[4], y[4];
+    u64_split(X.x, x[0], x[1]);
+    u64_split(X.y, x[2], x[3]);
+    u64_split(Y.x, y[0], y[1]);
+    u64_split(Y.y, y[2], y[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)x[d], (int)y[d], 0x110 + SH, 0xF, HI, false);
+        const uint32_t ny = (uint32_t)__builtin_amdgcn_update_dpp((int)y[d], (int)x[d], 0x100 + SH, 0xF, LO, false);
+        x[d] = nx;
+        y[d] = ny;
+    }
+    X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
+    Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
+}
+FHE_DEV void xpose_dpp32(cplx (&x)[4]) {  // register bits (1, 0) <-> lane bits (3, 2)
+    xpose_dpp_banked<3>(x[0], x[2]);
+    xpose_dpp_banked<3>(x[1], x[3]);
+    xpose_dpp_banked<2>(x[0], x[1]);
+    xpose_dpp_banked<2>(x[2], x[3]);
+}
+
 // register bits (1, 0) <-> lane bits (KH, KL): pairs (x0,x2),(x1,x3) for bit 1; (x0,x1),(x2,x3) for bit 0
 FHE_DEV void xpose_AB(cplx (&x)[4]) {
     xpose_permlane<5>(x[0], x[2]);
@@ -235,12 +266,12 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         ct2(x, ZT[0], ZT[1]);
         xpose_AB(x);                 // A -> B: regs <-> lane bits 5,4
         ct2(x, ZT[2], ZT[3]);
-        xpose_dpp2<3, 2>(x, L);      // B -> C: regs <-> lane bits 3,2
+        xpose_dpp32(x);              // B -> C: regs <-> lane bits 3,2
         ct2(x, ZT[4], ZT[5]);
         xpose_dpp2<1, 0>(x, L);      // C -> D: regs <-> lane bits 1,0
         ct2(x, ZT[6], ZT[7]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cross[xD + fx(4 * r)] = x[r];
+        for (int r = 0; r < 4; ++r) cross[xD ^ fx(4 * r)] = x[r];
         __syncthreads();
         // phase E reads both polynomials' regions: stages 8, 9 of the other polynomial's digits are
         // recomputed here (identical operations to its own waves') instead of swapping the results
@@ -250,8 +281,8 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             const cplx* cross_other = s_cross[p ^ 1];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                x[r] = cross[xE + fx(r)];
-                y[r] = cross_other[xE + fx(r)];
+                x[r] = cross[xE ^ fx(r)];
+                y[r] = cross_other[xE ^ fx(r)];
             }
         }
         ct2_last(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
@@ -272,14 +303,14 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         // through a region of its own: the other polynomial's waves may still be reading `cross`
         cplx* inv = s_inv[p];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) inv[xE + fx(r)] = x[r];
+        for (int r = 0; r < 4; ++r) inv[xE ^ fx(r)] = x[r];
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = inv[xD + fx(4 * r)];
+        for (int r = 0; r < 4; ++r) x[r] = inv[xD ^ fx(4 * r)];
         dit2(x, T[9], T[10], T[11]);
         xpose_dpp2<1, 0>(x, L);      // D -> C
         dit2(x, T[6], T[7], T[8]);
-        xpose_dpp2<3, 2>(x, L);      // C -> B
+        xpose_dpp32(x);              // C -> B
         dit2(x, T[3], T[4], T[5]);
         xpose_AB(x);                 // B -> A
         dit2(x, T[0], T[1], T[2]);

@@ -60,7 +60,7 @@ struct fhe_ctx {
     uint64_t* d_ks_body = nullptr;
     size_t ks_cap = 0;              // ciphertexts
     // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU)
-    int wide_threshold = 256;  // wide up to one ciphertext per CU; quad above (profiles/r1/latency_sweep_r1j.txt)
+    int wide_threshold = 512;  // wide up to two ciphertexts per CU; quad above (profiles/r1/latency_sweep_r1p.txt)
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;
@@ -88,7 +88,7 @@ struct fhe_ctx {
     void* comm = nullptr;       // ncclComm_t
     int rank = 0, nranks = 1;
     int fanout_emulate = 0;     // test hook: split levels over this many virtual ranks on one GPU
-    size_t fanout_min = 512;
+    size_t fanout_min = 257;  // above one ciphertext per CU (256 CUs) a level costs 2x the floor
     uint64_t* d_gather = nullptr;        // [nranks * chunk][2049]
     size_t gather_cap = 0;               // ciphertexts
     int fanout_world() const { return comm ? nranks : (fanout_emulate > 1 ? fanout_emulate : 1); }

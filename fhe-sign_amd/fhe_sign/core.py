@@ -175,7 +175,7 @@ class Context:
     def detach_comm(self) -> None:
         check(load().fhe_ctx_detach_comm(self._h))
 
-    def set_fanout(self, min_level: int = 512, emulate_ranks: int = 0) -> None:
+    def set_fanout(self, min_level: int = 257, emulate_ranks: int = 0) -> None:
         check(load().fhe_ctx_set_fanout(self._h, int(min_level), int(emulate_ranks)))
 
     def fanout_info(self):

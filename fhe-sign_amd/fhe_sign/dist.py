@@ -34,7 +34,7 @@ def share_id(dist, rank: int, make_id=comm_unique_id) -> bytes | None:
     return bytes(buf[:128].tolist()) if int(buf[128]) else None
 
 
-def attach_fanout(ctx, dist, rank: int, world: int, min_level: int = 512, make_id=comm_unique_id):
+def attach_fanout(ctx, dist, rank: int, world: int, min_level: int = 257, make_id=comm_unique_id):
     """Attach `ctx` to a world-size RCCL communicator and enable level fan-out.
     Returns (ok, error): ok is identical on all ranks."""
     err = None

@@ -107,7 +107,7 @@ int fhe_memcpy_d2h(fhe_ctx* ctx, void* dst, const void* src, size_t bytes);
 int fhe_ctx_last_pbs_timing(fhe_ctx* ctx, float* ks_ms, float* br_ms);
 int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
- * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
+ * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 512. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
 /* Throughput blind-rotate kernel for levels above the threshold: 4 waves per ciphertext
  * (FHE_BR_QUAD, the default and only one; FHE_BR_NARROW, the retired 2-wave kernel, is refused with
@@ -130,7 +130,7 @@ int fhe_ctx_set_ks_kernel(fhe_ctx* ctx, int kind);
 int fhe_comm_unique_id(uint8_t id[FHE_COMM_ID_BYTES]);
 int fhe_ctx_attach_comm(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank);
 int fhe_ctx_detach_comm(fhe_ctx* ctx);
-/* split threshold (default 512) and, for single-GPU tests, the number of emulated ranks (0 = off) */
+/* split threshold (default 257: above one ciphertext per CU) and, for single-GPU tests, the number of emulated ranks (0 = off) */
 int fhe_ctx_set_fanout(fhe_ctx* ctx, uint32_t min_level, int emulate_ranks);
 /* rank, world (emulated ranks counted) and the number of levels split so far */
 int fhe_ctx_fanout_info(const fhe_ctx* ctx, int* rank, int* nranks, uint64_t* fanout_levels);
