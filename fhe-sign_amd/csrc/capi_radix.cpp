@@ -1,9 +1,12 @@
 // capi_radix.cpp -- C ABI for radix integers (FheUint<N>) and BigUintFHE.
 #include <cstring>
+#include <memory>
+#include <string>
 #include <stdexcept>
 
 #include "biguint.h"
 #include "fhe_rocm.h"
+#include "serial.h"
 
 struct fhe_radix {
     fhe::Radix r;
@@ -460,6 +463,164 @@ int fhe_biguint_mul(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, int 
         auto* r = new fhe_biguint();
         r->v = biguint_mul(*c->engine, a->v, b->v, mode);
         *out = r;
+        return FHE_OK;
+    });
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------- serialization
+// Radix payload: params, u32 bits, u32 blocks, per block u8 tag (0 trivial: u32 value; 1: u32
+// degree, u32 noise, 2049 u64 words).  BigUint: params, u32 limbs, then per limb u32 bits + blocks.
+namespace {
+bool same_params(const Params& a, const Params& b) {
+    return a.n == b.n && a.pbs_base_log == b.pbs_base_log && a.ks_base_log == b.ks_base_log &&
+           a.ks_level == b.ks_level && a.lwe_noise_log2 == b.lwe_noise_log2 && a.glwe_noise_log2 == b.glwe_noise_log2 &&
+           a.message_modulus == b.message_modulus && a.carry_modulus == b.carry_modulus;
+}
+void put_blocks(ser::Writer& w, fhe_ctx* c, const Radix& r, uint32_t bits) {
+    std::vector<uint64_t> ct(kBigCt);
+    w.u32(bits);
+    w.u32(r.nblocks());
+    for (const Block& b : r.blocks) {
+        if (b.trivial()) {
+            w.u8(0);
+            w.u32(b.value);
+        } else {
+            w.u8(1);
+            w.u32(b.degree);
+            w.u32(b.noise);
+            c->engine->download(b, ct.data());
+            w.words(ct.data(), kBigCt);
+        }
+    }
+}
+bool get_blocks(ser::Reader& r, fhe_ctx* c, Radix* out, uint32_t* bits, std::string* why) {
+    *bits = r.u32();
+    const uint32_t nb = r.u32();
+    if (!r.ok || !valid_bits(*bits) || nb != *bits / 2) {
+        *why = "malformed radix header";
+        return false;
+    }
+    const uint32_t mc = c->p.msg_carry();
+    std::vector<uint64_t> ct(kBigCt);
+    for (uint32_t k = 0; k < nb; ++k) {
+        const uint8_t tag = r.u8();
+        if (tag == 0) {
+            const uint32_t v = r.u32();
+            if (!r.ok || v >= mc) {
+                *why = "malformed trivial block";
+                return false;
+            }
+            out->blocks.push_back(Block::make_trivial(v));
+        } else if (tag == 1) {
+            const uint32_t degree = r.u32(), noise = r.u32();
+            if (!r.ok || degree >= mc || noise == 0 || noise > kMaxNoise || !r.words(ct.data(), kBigCt)) {
+                *why = "malformed block (metadata outside the radix layer's degree / noise budget)";
+                return false;
+            }
+            Block b = c->engine->upload(ct.data(), degree);
+            b.noise = noise;
+            out->blocks.push_back(std::move(b));
+        } else {
+            *why = "malformed block tag";
+            return false;
+        }
+    }
+    return true;
+}
+}  // namespace
+
+extern "C" {
+
+int fhe_radix_serialize(fhe_ctx* c, const fhe_radix* x, uint8_t* buf, size_t cap, size_t* len) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!x || !len) return FHE_ERR_INVALID;
+    return guarded([&] {
+        ser::Writer w;
+        w.params(c->p);
+        put_blocks(w, c, x->r, x->bits);
+        return ser::emit(ser::frame(ser::kRadix, w.b), buf, cap, len);
+    });
+}
+
+int fhe_radix_deserialize(fhe_ctx* c, const uint8_t* buf, size_t len, fhe_radix** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!out) return FHE_ERR_INVALID;
+    return guarded([&] {
+        ser::Reader r;
+        std::string why;
+        Params p;
+        if (!ser::unframe(buf, len, ser::kRadix, &r, &why) || !r.params(&p, &why)) {
+            set_error(why);
+            return FHE_ERR_INVALID;
+        }
+        if (!same_params(p, c->p)) {
+            set_error("ciphertext parameters differ from the context's server key");
+            return FHE_ERR_INVALID;
+        }
+        Radix x;
+        uint32_t bits = 0;
+        if (!get_blocks(r, c, &x, &bits, &why) || !r.done()) {
+            set_error(why.empty() ? "trailing bytes" : why);
+            return FHE_ERR_INVALID;
+        }
+        *out = wrap(std::move(x), bits);
+        return FHE_OK;
+    });
+}
+
+int fhe_biguint_serialize(fhe_ctx* c, const fhe_biguint* x, uint8_t* buf, size_t cap, size_t* len) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!x || !len) return FHE_ERR_INVALID;
+    return guarded([&] {
+        ser::Writer w;
+        w.params(c->p);
+        w.u32((uint32_t)x->v.digits.size());
+        for (const Radix& d : x->v.digits) put_blocks(w, c, d, 32);
+        return ser::emit(ser::frame(ser::kBigUint, w.b), buf, cap, len);
+    });
+}
+
+int fhe_biguint_deserialize(fhe_ctx* c, const uint8_t* buf, size_t len, fhe_biguint** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!out) return FHE_ERR_INVALID;
+    return guarded([&] {
+        ser::Reader r;
+        std::string why;
+        Params p;
+        if (!ser::unframe(buf, len, ser::kBigUint, &r, &why) || !r.params(&p, &why)) {
+            set_error(why);
+            return FHE_ERR_INVALID;
+        }
+        if (!same_params(p, c->p)) {
+            set_error("ciphertext parameters differ from the context's server key");
+            return FHE_ERR_INVALID;
+        }
+        const uint32_t n = r.u32();
+        if (!r.ok || (uint64_t)n * 32 > FHE_RADIX_MAX_BITS * 64ull) {
+            set_error("malformed limb count");
+            return FHE_ERR_INVALID;
+        }
+        auto v = std::make_unique<fhe_biguint>();
+        for (uint32_t i = 0; i < n; ++i) {
+            Radix d;
+            uint32_t bits = 0;
+            if (!get_blocks(r, c, &d, &bits, &why) || bits != 32) {
+                set_error(why.empty() ? "limb is not a 32-bit radix" : why);
+                return FHE_ERR_INVALID;
+            }
+            v->v.digits.push_back(std::move(d));
+        }
+        if (!r.done()) {
+            set_error("trailing bytes");
+            return FHE_ERR_INVALID;
+        }
+        *out = v.release();
         return FHE_OK;
     });
 }

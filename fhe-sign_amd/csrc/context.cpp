@@ -305,6 +305,18 @@ int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** 
 void fhe_client_key_destroy(fhe_client_key* ck) { delete ck; }
 void fhe_server_key_destroy(fhe_server_key* sk) { delete sk; }
 
+int fhe_client_key_params(const fhe_client_key* ck, fhe_params* out) {
+    if (!ck || !out) return FHE_ERR_INVALID;
+    *out = ck->params.to_c();
+    return FHE_OK;
+}
+
+int fhe_server_key_params(const fhe_server_key* sk, fhe_params* out) {
+    if (!sk || !out) return FHE_ERR_INVALID;
+    *out = sk->params.to_c();
+    return FHE_OK;
+}
+
 int fhe_client_key_export(const fhe_client_key* ck, uint64_t* lwe_sk, size_t lwe_len, uint64_t* glwe_sk,
                           size_t glwe_len) {
     if (!ck || lwe_len < ck->lwe_sk.size() || glwe_len < ck->glwe_sk.size()) {

@@ -107,6 +107,26 @@ void ChaChaStream::refill() {
     pos_ = 0;
 }
 
+void ChaChaStream::save(uint32_t* out) const {
+    size_t k = 0;
+    for (uint32_t v : key_) out[k++] = v;
+    for (uint32_t v : nonce_) out[k++] = v;
+    out[k++] = counter_;
+    for (uint32_t v : buf_) out[k++] = v;
+    out[k++] = pos_;
+}
+
+bool ChaChaStream::load(const uint32_t* in) {
+    if (in[kStateWords - 1] > 16) return false;
+    size_t k = 0;
+    for (uint32_t& v : key_) v = in[k++];
+    for (uint32_t& v : nonce_) v = in[k++];
+    counter_ = in[k++];
+    for (uint32_t& v : buf_) v = in[k++];
+    pos_ = in[k++];
+    return true;
+}
+
 uint64_t ChaChaStream::next_u64() {
     if (pos_ >= 16) refill();
     uint64_t lo = buf_[pos_++];

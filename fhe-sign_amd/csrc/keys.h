@@ -41,6 +41,10 @@ public:
     void reset(uint64_t seed, uint32_t stream);
     uint64_t next_u64();
     int64_t tuniform(uint32_t log2_bound);
+    // full state (key, nonce, counter, buffered block, position) for serialization (serial.cpp)
+    static constexpr size_t kStateWords = 8 + 3 + 1 + 16 + 1;
+    void save(uint32_t* out) const;
+    bool load(const uint32_t* in);  // false if the state is malformed
 
 private:
     void refill();

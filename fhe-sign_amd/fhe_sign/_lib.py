@@ -76,6 +76,16 @@ _SIGNATURES = [
     ("fhe_radix_scalar_mul", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_div", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_rem", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("fhe_client_key_params", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("fhe_server_key_params", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("fhe_client_key_serialize", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("fhe_client_key_deserialize", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_server_key_serialize", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("fhe_server_key_deserialize", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_serialize", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("fhe_radix_deserialize", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_biguint_serialize", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("fhe_biguint_deserialize", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_radix_div", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("fhe_radix_rem", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("fhe_radix_divrem", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
@@ -146,3 +156,12 @@ def check(rc: int) -> None:
 def ptr(arr, ctype=C.c_uint64):
     """Pointer to a contiguous numpy array."""
     return arr.ctypes.data_as(C.POINTER(ctype))
+
+
+def serialize_with(fn, *args) -> bytes:
+    """size query (NULL buffer), then fill: the C ABI's serialization convention"""
+    n = C.c_size_t(0)
+    check(fn(*args, None, 0, C.byref(n)))
+    buf = (C.c_uint8 * n.value)()
+    check(fn(*args, buf, n.value, C.byref(n)))
+    return bytes(buf)

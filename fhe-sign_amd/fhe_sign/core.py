@@ -5,7 +5,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import FheParams, check, load, ptr
+from ._lib import FheParams, check, load, ptr, serialize_with
 
 BIG_CT = 2049  # big LWE ciphertext words
 
@@ -37,6 +37,18 @@ class ClientKey:
         check(load().fhe_client_key_export(self._h, ptr(lwe), n, ptr(glwe), glwe.size))
         return lwe, glwe
 
+    def serialize(self) -> bytes:
+        """own versioned format (include/fhe_rocm.h, serial.h), encryption-stream state included"""
+        return serialize_with(load().fhe_client_key_serialize, self._h)
+
+    @classmethod
+    def deserialize(cls, data: bytes) -> "ClientKey":
+        h = C.c_void_p()
+        check(load().fhe_client_key_deserialize(data, len(data), C.byref(h)))
+        p = FheParams()
+        check(load().fhe_client_key_params(h, C.byref(p)))
+        return cls(h, p)
+
     def seed_encryption(self, seed: int, stream: int = 100) -> None:
         check(load().fhe_client_key_seed_encryption(self._h, seed, stream))
 
@@ -65,6 +77,17 @@ class ServerKey:
         if getattr(self, "_h", None):
             load().fhe_server_key_destroy(self._h)
             self._h = None
+
+    def serialize(self) -> bytes:
+        return serialize_with(load().fhe_server_key_serialize, self._h)
+
+    @classmethod
+    def deserialize(cls, data: bytes) -> "ServerKey":
+        h = C.c_void_p()
+        check(load().fhe_server_key_deserialize(data, len(data), C.byref(h)))
+        p = FheParams()
+        check(load().fhe_server_key_params(h, C.byref(p)))
+        return cls(h, p)
 
     def export(self):
         p = self.params

@@ -13,7 +13,7 @@ import threading
 
 import numpy as np
 
-from ._lib import check, load, ptr
+from ._lib import check, load, ptr, serialize_with
 
 COMPAT = 0  # exact replay of src/biguint.rs:214-254 incl. the wrapping add at :247-249
 FAST = 1    # true product/sum, single wide carry propagation
@@ -159,6 +159,18 @@ class FheUint:
             return self._bin("fhe_radix_rem", d)
         return self._scalar_any("fhe_radix_scalar_rem", d, wrap=False)
 
+    def serialize(self) -> bytes:
+        """ciphertext bytes (own format, include/fhe_rocm.h); restore with FheUint.deserialize"""
+        return serialize_with(load().fhe_radix_serialize, _ctx().handle, self._h)
+
+    @classmethod
+    def deserialize(cls, data: bytes):
+        h = C.c_void_p()
+        check(load().fhe_radix_deserialize(_ctx().handle, data, len(data), C.byref(h)))
+        bits = C.c_uint32(0)
+        check(load().fhe_radix_num_bits(h, C.byref(bits)))
+        return FheUint._wrap(h, bits.value)
+
     def div_rem(self, d):
         """(self // d, self % d) for an encrypted divisor, one pass"""
         q, r = C.c_void_p(), C.c_void_p()
@@ -240,6 +252,15 @@ class BigUintFHE:
         limbs = np.array(to_u32_digits(value), dtype=np.uint32)
         h = C.c_void_p()
         check(load().fhe_biguint_encrypt(_ctx().handle, client_key.handle, ptr(limbs, C.c_uint32), limbs.size, C.byref(h)))
+        return cls(h)
+
+    def serialize(self) -> bytes:
+        return serialize_with(load().fhe_biguint_serialize, _ctx().handle, self._h)
+
+    @classmethod
+    def deserialize(cls, data: bytes) -> "BigUintFHE":
+        h = C.c_void_p()
+        check(load().fhe_biguint_deserialize(_ctx().handle, data, len(data), C.byref(h)))
         return cls(h)
 
     @classmethod
