@@ -40,8 +40,19 @@ bool Reader::params(Params* out, std::string* why) {
 }
 
 uint64_t fnv1a(const uint8_t* p, size_t n) {
+    // FNV-1a over little-endian 64-bit words (the tail zero-padded): one multiply per 8 bytes
     uint64_t h = 0xcbf29ce484222325ull;
-    for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0x100000001b3ull;
+    }
+    if (i < n) {
+        uint64_t w = 0;
+        std::memcpy(&w, p + i, n - i);
+        h = (h ^ w) * 0x100000001b3ull;
+    }
     return h;
 }
 

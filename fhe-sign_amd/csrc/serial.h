@@ -3,7 +3,8 @@
 // The reference never serializes (keys are regenerated per run; `grep serial` hits only a doc
 // comment, src/schnorr.rs:47); tfhe-rs's bincode + tfhe-versionable wire format cannot be pinned
 // here (no tfhe-rs fixture, crate absent), so this is this engine's own format, little-endian:
-//   header  magic "FHEROCM\0" | u32 version (1) | u32 kind | u64 payload bytes | u64 FNV-1a(payload)
+//   header  magic "FHEROCM\0" | u32 version (1) | u32 kind | u64 payload bytes | u64 checksum
+//           (FNV-1a over the payload's little-endian u64 words, tail zero-padded)
 //   payload params (8 x u32: n, pbs_base_log, ks_base_log, ks_level, lwe/glwe noise log2, msg,
 //           carry) then the kind's fields (serial.cpp / capi_radix.cpp).
 // Readers check magic, version, kind, length, checksum, parameter ranges and every count before

@@ -70,8 +70,9 @@ def test_rejects_non_binary_secret(keys):
     off = 32 + 8 * 4 + 4                    # header, params, lwe length
     blob[off] = 2                           # lwe_sk[0] = 2
     payload = bytes(blob[32:])
+    payload += b"\0" * (-len(payload) % 8)
     h = 0xcbf29ce484222325
-    for x in payload:
+    for (x,) in struct.iter_unpack("<Q", payload):
         h = ((h ^ x) * 0x100000001b3) & (2**64 - 1)
     blob[24:32] = struct.pack("<Q", h)
     with pytest.raises(FheError, match="malformed"):
