@@ -2,8 +2,9 @@
 // all ciphertext arithmetic runs in the gfx950 kernels of pbs_kernels.hip).
 //
 // Algorithms (published TFHE radix techniques, restated; tfhe 0.10.0 integer layer [ext]):
-//   * carry propagation: block states (generate/propagate/kill) + Hillis-Steele prefix with
-//     bivariate lookups (4*hi + lo), then one final (v + carry) mod 4 bootstrap per block
+//   * carry propagation: block states (generate/propagate/kill) + a radix-3 chain prefix (up to
+//     three states and a resolved carry per lookup, binary-sum encoding 4*s + 2*s + s + c), then
+//     one final (v + carry) mod 4 bootstrap per block
 //   * multiplication: block-pair products through bivariate LUTs (low/high halves), column
 //     compression (<= 15 in degree per group, msg/carry split), then carry propagation
 //   * scalar division: Granlund-Montgomery multiply-high by a public magic constant
@@ -330,14 +331,6 @@ const std::vector<uint32_t>& LUT_GEN() {
     static auto t = lut1([](uint32_t v) { return v >= 4 ? 1u : 0u; });
     return t;
 }
-const std::vector<uint32_t>& LUT_PREFIX_BIT() {  // (hi state, lo carry bit) -> carry bit
-    static auto t = lut2([](uint32_t hi, uint32_t lo) { return (hi == 2 || (hi == 1 && lo == 1)) ? 1u : 0u; });
-    return t;
-}
-const std::vector<uint32_t>& LUT_PREFIX_STATE() {  // (hi state, lo state) -> state
-    static auto t = lut2([](uint32_t hi, uint32_t lo) { return hi == 1 ? lo : hi; });
-    return t;
-}
 }  // namespace
 
 // ============================================================================ basics
@@ -463,6 +456,112 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
     }
 }
 
+// ---------------------------------------------------------------- carry prefix over block states
+// in[p][k], k < m_p: position 0 holds its carry out as a bit {0, 1}, every other position its state
+// alone {0 kill, 1 propagate, 2 generate}.  Returns the carry-out bits of every position.
+//
+// Chains are resolved with the binary-sum identity: for states s_0 (top) .. s_{j-1} of j adjacent
+// positions and carry-in c, x = sum_i 2^(j-1-i) s_i + c is the sum of two j-bit numbers plus c, so
+// the chain's carry out is [x >= 2^j]; without a carry-in, the chain's state is G if x >= 2^j, P if
+// x == 2^j - 1, else K.  One bootstrap takes up to three states (+ a completed carry bit below
+// them): x <= 4*2 + 2*2 + 2 + 1 = 15 fits the 16-value space, noise 16 + 4 + 1 + 1 = 22.  Every
+// level, each unresolved position chains its current window with the two windows below it and, if
+// the next one down is resolved, its carry -- the resolved front grows 1, 4, 13, 40, 121, ...
+// (F_t + 3^(t+1)), i.e. about log3 of the width levels (radix-2 Hillis-Steele: log2).  Only nodes
+// that some requested carry depends on are bootstrapped (`want`: the positions whose carry is
+// needed; empty = all).
+static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const std::vector<std::vector<uint32_t>>& want) {
+    struct Node {
+        uint32_t pos, lo;   // covers positions [lo, pos]
+        bool done;          // lo == 0: the value is the carry-out bit
+        int level;
+        std::vector<int> terms;  // node ids: states top-down, then (if done) the carry bit
+        bool need = false;
+    };
+    const size_t P = in.size();
+    std::vector<std::vector<Node>> nodes(P);
+    std::vector<std::vector<int>> latest(P);
+    int levels = 0;
+    for (size_t p = 0; p < P; ++p) {
+        const uint32_t m = (uint32_t)in[p].size();
+        for (uint32_t k = 0; k < m; ++k) {
+            nodes[p].push_back({k, k, k == 0, 0, {}});
+            latest[p].push_back((int)k);
+        }
+        for (int t = 1;; ++t) {
+            const std::vector<int> snap = latest[p];
+            bool any = false;
+            for (uint32_t k = 0; k < m; ++k) {
+                const Node& top = nodes[p][snap[k]];
+                if (top.done) continue;
+                any = true;
+                Node n{k, top.lo, false, t, {snap[k]}};
+                int states = 1;
+                while (n.lo > 0) {
+                    const Node& below = nodes[p][snap[n.lo - 1]];
+                    if (below.done) {
+                        n.terms.push_back(snap[n.lo - 1]);
+                        n.lo = 0;
+                        n.done = true;
+                        break;
+                    }
+                    if (states == 3) break;
+                    n.terms.push_back(snap[n.lo - 1]);
+                    n.lo = below.lo;
+                    ++states;
+                }
+                latest[p][k] = (int)nodes[p].size();
+                nodes[p].push_back(std::move(n));
+            }
+            if (!any) break;
+            levels = std::max(levels, t);
+        }
+        // mark what the requested carries depend on
+        std::vector<int> stack;
+        if (p < want.size() && !want[p].empty())
+            for (uint32_t k : want[p]) stack.push_back(latest[p][k]);
+        else
+            stack = latest[p];
+        while (!stack.empty()) {
+            Node& n = nodes[p][stack.back()];
+            stack.pop_back();
+            if (n.need) continue;
+            n.need = true;
+            for (int t : n.terms) stack.push_back(t);
+        }
+    }
+    std::vector<std::vector<Block>> val(P);
+    for (size_t p = 0; p < P; ++p) {
+        val[p].resize(nodes[p].size());
+        for (size_t k = 0; k < in[p].size(); ++k) val[p][k] = in[p][k];
+    }
+    for (int t = 1; t <= levels; ++t) {
+        std::vector<PbsItem> items;
+        std::vector<std::pair<size_t, int>> refs;
+        for (size_t p = 0; p < P; ++p)
+            for (size_t id = 0; id < nodes[p].size(); ++id) {
+                const Node& n = nodes[p][id];
+                if (n.level != t || !n.need) continue;
+                const int states = (int)n.terms.size() - (n.done ? 1 : 0);
+                PbsItem it;
+                for (int i = 0; i < states; ++i) it.terms.push_back({val[p][n.terms[i]], 1 << (states - 1 - i)});
+                if (n.done) it.terms.push_back({val[p][n.terms.back()], 1});
+                const uint32_t full = 1u << states;
+                it.table = n.done ? lut1([full](uint32_t x) { return x >= full ? 1u : 0u; })
+                                  : lut1([full](uint32_t x) { return x >= full ? 2u : (x == full - 1 ? 1u : 0u); });
+                items.push_back(std::move(it));
+                refs.push_back({p, (int)id});
+            }
+        if (items.empty()) continue;
+        Blocks outs = e.run(items);
+        for (size_t i = 0; i < outs.size(); ++i) val[refs[i].first][refs[i].second] = outs[i];
+    }
+    std::vector<Blocks> res(P);
+    for (size_t p = 0; p < P; ++p)
+        for (size_t k = 0; k < in[p].size(); ++k) res[p].push_back(val[p][latest[p][k]]);
+    return res;
+}
+
 // Carries of compressed columns (each column sum v_k <= 6, <= 7 at k = 0): cur[p][k] = carry out of
 // position k, k < nblocks - 1.  A problem with one extra empty top column yields its carry out.
 static std::vector<Blocks> propagate_carries(Engine& e, std::vector<ColProblem>& probs) {
@@ -473,48 +572,26 @@ static std::vector<Blocks> propagate_carries(Engine& e, std::vector<ColProblem>&
     }
     compress_columns(e, ptrs);
 
-    // carries c_k (carry out of position k), k < nblocks - 1, for every problem
+    // position states (carry bit at position 0), one level for every problem
     std::vector<Blocks> cur(probs.size());
-    {
-        std::vector<PbsItem> items;
-        for (auto& P : probs) {
-            const uint32_t m = P.nblocks ? P.nblocks - 1 : 0;
-            for (uint32_t k = 0; k < m; ++k) {
-                PbsItem it;
-                for (auto& b : P.cols[k]) it.terms.push_back({b, 1});
-                it.table = k == 0 ? LUT_GEN() : LUT_STATE();
-                items.push_back(it);
-            }
-        }
-        Blocks outs = e.run(items);
-        size_t o = 0;
-        for (size_t pi = 0; pi < probs.size(); ++pi) {
-            const uint32_t m = probs[pi].nblocks ? probs[pi].nblocks - 1 : 0;
-            cur[pi].assign(outs.begin() + o, outs.begin() + o + m);
-            o += m;
+    std::vector<PbsItem> items;
+    for (auto& P : probs) {
+        const uint32_t m = P.nblocks ? P.nblocks - 1 : 0;
+        for (uint32_t k = 0; k < m; ++k) {
+            PbsItem it;
+            for (auto& b : P.cols[k]) it.terms.push_back({b, 1});
+            it.table = k == 0 ? LUT_GEN() : LUT_STATE();
+            items.push_back(it);
         }
     }
-    // Hillis-Steele prefix: after the level with span 2^t, positions < 2^(t+1) are carry bits
-    for (uint32_t span = 1;; span <<= 1) {
-        std::vector<PbsItem> items;
-        struct Ref {
-            size_t pi;
-            uint32_t k;
-        };
-        std::vector<Ref> refs;
-        for (size_t pi = 0; pi < probs.size(); ++pi) {
-            const uint32_t m = (uint32_t)cur[pi].size();
-            for (uint32_t k = span; k < m; ++k) {
-                const bool completes = k < 2 * span;
-                items.push_back(item2(cur[pi][k], cur[pi][k - span], completes ? LUT_PREFIX_BIT() : LUT_PREFIX_STATE()));
-                refs.push_back({pi, k});
-            }
-        }
-        if (items.empty()) break;
-        Blocks outs = e.run(items);
-        for (size_t i = 0; i < outs.size(); ++i) cur[refs[i].pi][refs[i].k] = outs[i];
+    Blocks outs = e.run(items);
+    size_t o = 0;
+    for (size_t pi = 0; pi < probs.size(); ++pi) {
+        const uint32_t m = probs[pi].nblocks ? probs[pi].nblocks - 1 : 0;
+        cur[pi].assign(outs.begin() + o, outs.begin() + o + m);
+        o += m;
     }
-    return cur;
+    return carry_prefix(e, std::move(cur), {});
 }
 
 // out_k = (v_k + c_{k-1}) mod 4 for k < upto (the final level of a carry propagation)
@@ -854,17 +931,7 @@ static Block carry_out_ge(Engine& e, const Radix& a, const Radix& b) {
         items.push_back(it);
     }
     Blocks cur = e.run(items);
-    for (uint32_t span = 1; span < n; span <<= 1) {
-        std::vector<PbsItem> its;
-        std::vector<uint32_t> ks;
-        for (uint32_t k = span; k < n; ++k) {
-            its.push_back(item2(cur[k], cur[k - span], k < 2 * span ? LUT_PREFIX_BIT() : LUT_PREFIX_STATE()));
-            ks.push_back(k);
-        }
-        Blocks outs = e.run(its);
-        for (size_t i = 0; i < outs.size(); ++i) cur[ks[i]] = outs[i];
-    }
-    return cur[n - 1];
+    return carry_prefix(e, {cur}, {{n - 1}})[0][n - 1];
 }
 
 Block radix_lt(Engine& e, const Radix& a, const Radix& b) {

@@ -24,7 +24,7 @@ namespace fhe {
 
 constexpr uint32_t kMsgBits = 2;
 constexpr uint32_t kMsgMod = 4;
-constexpr uint32_t kMaxNoise = 20;  // variance units; bivariate 4a+b of fresh blocks = 17
+constexpr uint32_t kMaxNoise = 25;  // variance units (sigma <= 5 fresh sigmas, tfhe-rs 2_2 max noise level 5)
 
 class BlockPool;
 

@@ -94,3 +94,33 @@ def test_keyswitch_preserves_message(okeys):
         phase = (int(small[n]) - int(np.dot(small[:n].astype(object), okeys.lwe_sk.astype(object)))) % 2**64
         err = (phase - m * okeys.delta() + 2**63) % 2**64 - 2**63
         assert abs(err) < 2**57
+
+
+def test_noise_budget_at_radix_limit_oracle(okeys):
+    """CPU twin of tests/test_pbs_gpu.py::test_noise_budget_at_radix_limit on the oracle: the
+    carry prefix's largest PBS input, 4 s0 + 2 s1 + s2 + c of fresh bootstrap outputs (22 of the
+    radix layer's 25-variance budget), keyswitched and modulus-switched, keeps > 8 sigma of margin
+    against the half step (64 in the 4096-domain)."""
+    rs = np.random.default_rng(6)
+    N = 160
+    s = rs.integers(0, 3, size=(3, N))
+    c = rs.integers(0, 2, size=N)
+    r = okeys.rng(78)
+    fresh = np.stack([okeys.encrypt(r, int(v)) for v in np.concatenate([s.ravel(), c])])
+    ident = okeys.make_lut(list(range(16)))[None, :]
+    unit = okeys.pbs_batch(fresh, ident, np.zeros(len(fresh), np.uint32)).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        comb = (np.uint64(4) * unit[:N] + np.uint64(2) * unit[N:2 * N] + unit[2 * N:3 * N] + unit[3 * N:]).astype(np.uint64)
+    m = 4 * s[0] + 2 * s[1] + s[2] + c
+    n = okeys.params.n
+    sk = okeys.lwe_sk.astype(object)
+    errs = []
+    for i in range(N):
+        small = okeys.keyswitch(comb[i])
+        ms = [((int(w) + (1 << 51)) >> 52) % 4096 for w in small[: n + 1]]
+        phase = (ms[n] - sum(a * b for a, b in zip(ms[:n], sk))) % 4096
+        errs.append((phase - 128 * int(m[i]) + 2048) % 4096 - 2048)
+    errs = np.array(errs, dtype=np.float64)
+    assert np.abs(errs).max() < 64
+    print(f"modulus-switched sigma at 22 units: {errs.std():.2f} (half step 64)")
+    assert errs.std() * 8 < 64, f"modulus-switched sigma {errs.std():.2f}"

@@ -132,3 +132,38 @@ def test_keyswitch_kernels_identical(env):
         assert np.array_equal(valu, mfma), count
     ref = ok.pbs_batch(cts[:4], np.stack([ok.make_lut(t) for t in tables]), np.arange(4, dtype=np.uint32) % len(tables))
     assert np.array_equal(mfma[:4], ref)
+
+
+def test_noise_budget_at_radix_limit(env):
+    """The radix layer admits PBS inputs up to kMaxNoise = 25 fresh-bootstrap variances (sigma <= 5
+    fresh sigmas, tfhe-rs' max noise level 5 for 2_2).  Its largest real input is the carry prefix's
+    4 s0 + 2 s1 + s2 + c (22 units, csrc/radix.cpp:carry_prefix).  Built here from GPU bootstrap
+    outputs, keyswitched and modulus-switched by the oracle: the phase error in the 4096-domain
+    stays far inside the half step (64), and every such input bootstraps to the right value."""
+    _, _, ok, ctx = env
+    ident = ctx.lut(list(range(16)))
+    rs = np.random.default_rng(5)
+    N = 384
+    s = rs.integers(0, 3, size=(3, N))
+    c = rs.integers(0, 2, size=N)
+    r = ok.rng(77)
+    fresh = np.stack([ok.encrypt(r, int(v)) for v in np.concatenate([s.ravel(), c])])
+    unit = ctx.pbs(fresh, ident).astype(np.uint64)  # unit-noise blocks (fresh bootstrap outputs)
+    s0, s1, s2, cb = unit[:N], unit[N:2 * N], unit[2 * N:3 * N], unit[3 * N:]
+    with np.errstate(over="ignore"):
+        comb = (np.uint64(4) * s0 + np.uint64(2) * s1 + s2 + cb).astype(np.uint64)
+    m = 4 * s[0] + 2 * s[1] + s[2] + c
+    n = ok.params.n
+    sk = ok.lwe_sk.astype(object)
+    errs = []
+    for i in range(N):
+        small = ok.keyswitch(comb[i])
+        ms = [((int(w) + (1 << 51)) >> 52) % 4096 for w in small[: n + 1]]
+        phase = (ms[n] - sum(a * b for a, b in zip(ms[:n], sk))) % 4096
+        errs.append((phase - 128 * int(m[i]) + 2048) % 4096 - 2048)
+    errs = np.array(errs, dtype=np.float64)
+    assert np.abs(errs).max() < 64
+    assert errs.std() * 8 < 64, f"modulus-switched sigma {errs.std():.2f} leaves < 8 sigma of margin"
+    carry = ctx.lut([1 if v >= 8 else 0 for v in range(16)])
+    out = ctx.pbs(comb, carry)
+    assert [ok.decrypt(o) for o in out] == [int(v >= 8) for v in m]
