@@ -48,7 +48,8 @@ BigUint biguint_add(Engine& e, const BigUint& A, const BigUint& B, int mode) {
 //    < 2^65 and nothing is dropped (the last, 64-bit window holds the top of a product that fits
 //    la + lb limbs) -- the limbs are the true product;
 //  * otherwise steps whose windows do not overlap commute, so each step runs in the first
-//    dependency wave after every earlier overlapping step, and a wave's window adds share levels.
+//    dependency wave after every earlier overlapping step, and a wave's window adds share levels;
+//    their sums stay lazy (v + c_in - 4 c_out, no final level) until the next wave's state level.
 BigUint biguint_mul(Engine& e, const BigUint& A, const BigUint& B, int mode) {
     const size_t la = A.digits.size(), lb = B.digits.size();
     BigUint out;
@@ -89,23 +90,36 @@ BigUint biguint_mul(Engine& e, const BigUint& A, const BigUint& B, int mode) {
             if ((size_t)wv >= waves.size()) waves.resize(wv + 1);
             waves[wv].push_back({i * lb + j, idx, wl});
         }
+    // Each wave's window adds stay lazy (radix_sum_lazy: no final level); the next wave cleans them
+    // in its state level, and one last level cleans what the final wave left.
     for (auto& wave : waves) {
         std::vector<Radix> W(wave.size());
-        std::vector<std::vector<const Radix*>> xs(wave.size());
-        std::vector<uint32_t> nbs(wave.size());
         for (size_t s = 0; s < wave.size(); ++s) {
             std::vector<const Radix*> wlimbs;
             for (size_t t = 0; t < wave[s].wl; ++t) wlimbs.push_back(&R[wave[s].idx + t]);
             W[s] = concat(wlimbs);
         }
-        for (size_t s = 0; s < wave.size(); ++s) {
-            xs[s] = {&W[s], &prods[wave[s].k]};
-            nbs[s] = (uint32_t)wave[s].wl * kLimbBlocks;
-        }
-        std::vector<Radix> S = radix_sum_many(e, xs, nbs);
+        std::vector<std::pair<const Radix*, const Radix*>> xs;
+        for (size_t s = 0; s < wave.size(); ++s) xs.push_back({&W[s], &prods[wave[s].k]});
+        std::vector<Radix*> refresh;
+        for (auto& r : R) refresh.push_back(&r);
+        std::vector<Radix> S = radix_sum_lazy(e, xs, refresh);
         for (size_t s = 0; s < wave.size(); ++s)
             for (size_t t = 0; t < wave[s].wl; ++t)
                 R[wave[s].idx + t] = slice(S[s], (uint32_t)t * kLimbBlocks, kLimbBlocks);
+    }
+    {
+        Radix all;
+        for (auto& r : R) all.blocks.insert(all.blocks.end(), r.blocks.begin(), r.blocks.end());
+        std::vector<PbsItem> items;
+        std::vector<uint32_t> at;
+        for (uint32_t k = 0; k < all.nblocks(); ++k)
+            if (all.blocks[k].lazy()) at.push_back(k);
+        Radix lazy;
+        for (uint32_t k : at) lazy.blocks.push_back(all.blocks[k]);
+        Radix clean = radix_clean(e, lazy);
+        for (size_t i = 0; i < at.size(); ++i) all.blocks[at[i]] = clean.blocks[i];
+        for (size_t i = 0; i < len; ++i) R[i] = slice(all, (uint32_t)i * kLimbBlocks, kLimbBlocks);
     }
     out.digits = std::move(R);
     return out;

@@ -15,6 +15,9 @@
 #include "radix.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -58,6 +61,9 @@ std::shared_ptr<Slot> BlockPool::alloc() {
 Engine::Engine(fhe_ctx* ctx) : ctx_(ctx) {
     pool_ = std::make_shared<BlockPool>(ctx->device);
     for (auto& ev : desc_ev_) hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+    // FHE_TRACE_LEVELS=1: synchronize after every level and print its size and wall time (stderr);
+    // a diagnostic for schedule work, never set by the bench or the tests.
+    if (const char* t = getenv("FHE_TRACE_LEVELS")) trace_ = atoi(t) != 0;
 }
 
 Engine::~Engine() {
@@ -153,7 +159,8 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         engine_check(ok && (reach >> mc) == 0, "PBS input out of the message space (degree overflow)");
         engine_check(noise <= kMaxNoise, "PBS input noise above the budget");
         uint32_t lo = 0xffffffffu, hi = 0;
-        bool identity = live[i].size() == 1 && live[i][0].coef == 1 && cst == 0 && live[i][0].b.noise <= 1;
+        bool identity = live[i].size() == 1 && live[i][0].coef == 1 && cst == 0 && live[i][0].b.noise <= 1 &&
+                        !live[i][0].b.lazy();
         for (uint32_t v = 0; v < mc; ++v) {
             if (!(reach >> v & 1)) continue;
             const uint32_t f = it.table[v] % mc;
@@ -194,14 +201,30 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         out[i].slot = pool_->alloc();
         PbsDesc d;
         std::memset(&d, 0, sizeof d);
-        engine_check(live[i].size() <= (size_t)kMaxTerms, "too many terms in one PBS input");
-        for (size_t t = 0; t < live[i].size(); ++t) {
-            d.src[t] = live[i][t].b.ptr();
-            d.coef[t] = live[i][t].coef;
+        // flatten lazy terms into their slot blocks (merging repeats)
+        int64_t dcst = csts[i];
+        uint32_t nt = 0;
+        auto put = [&](const Block& b, int32_t coef) {
+            for (uint32_t u = 0; u < nt; ++u)
+                if (d.src[u] == b.ptr()) {
+                    d.coef[u] += coef;
+                    return;
+                }
+            engine_check(nt < (uint32_t)kMaxTerms, "too many terms in one PBS input");
+            d.src[nt] = b.ptr();
+            d.coef[nt++] = coef;
+        };
+        for (const Term& t : live[i]) {
+            if (!t.b.lazy()) {
+                put(t.b, t.coef);
+                continue;
+            }
+            dcst += (int64_t)t.coef * t.b.lin_cst;
+            for (const Term& u : *t.b.lin) put(u.b, t.coef * u.coef);
         }
-        d.nterms = (uint32_t)live[i].size();
+        d.nterms = nt;
         d.lut = lut;
-        d.cst = (uint64_t)csts[i] * delta;
+        d.cst = (uint64_t)dcst * delta;
         // fanned-out levels bootstrap into the gather buffer (segment = owning rank), then scatter
         d.dst = split ? ctx_->d_gather + g * kBigCt : out[i].slot->p;
         if (split) h_scat[g] = out[i].slot->p;
@@ -216,6 +239,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         hip_check(ctx_->keyswitch(nullptr, dev + lo, hi - lo), "keyswitch");
         hip_check(ctx_->blind_rotate(dev + lo, nullptr, nullptr, hi - lo), "blind rotate");
     };
+    const auto t0 = std::chrono::steady_clock::now();
     if (!split) {
         pbs(0, G);
     } else {
@@ -230,10 +254,16 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     }
     pbs_count += G;
     levels += 1;
+    if (trace_) {
+        sync();
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        fprintf(stderr, "[level %llu] %zu PBS %.3f ms\n", (unsigned long long)levels, G, ms);
+    }
     return out;
 }
 
 Block Engine::lincomb(const std::vector<Term>& terms, uint32_t cst) {
+    for (const Term& t : terms) engine_check(!t.b.lazy(), "lincomb of a lazy block");
     int64_t c = cst;
     uint32_t noise = 0;
     std::vector<Term> live;
@@ -283,12 +313,35 @@ Block Engine::upload(const uint64_t* ct, uint32_t degree) {
 }
 
 void Engine::download(const Block& b, uint64_t* ct) {
-    engine_check(!b.trivial(), "download of a trivial block");
+    engine_check(!b.trivial() && !b.lazy(), "download of a trivial or lazy block");
     hip_check(hipMemcpyAsync(ct, b.slot->p, kBigCt * 8, hipMemcpyDeviceToHost, ctx_->stream), "download");
     hip_check(hipStreamSynchronize(ctx_->stream), "download sync");
 }
 
 void Engine::sync() { hip_check(hipStreamSynchronize(ctx_->stream), "sync"); }
+
+Block block_lazy(const std::vector<Term>& terms, int32_t cst, uint32_t degree) {
+    auto lin = std::make_shared<std::vector<Term>>();
+    Block b;
+    b.degree = degree;
+    for (const Term& t : terms) {
+        if (t.coef == 0) continue;
+        engine_check(!t.b.lazy(), "nested lazy block");
+        if (t.b.trivial()) {
+            cst += t.coef * (int32_t)t.b.value;
+            continue;
+        }
+        lin->push_back(t);
+        b.noise += (uint32_t)(t.coef * t.coef) * t.b.noise;
+    }
+    if (lin->empty()) {
+        engine_check(cst >= 0 && (uint32_t)cst <= degree, "lazy constant out of its range");
+        return Block::make_trivial((uint32_t)cst);
+    }
+    b.lin = std::move(lin);
+    b.lin_cst = cst;
+    return b;
+}
 
 // ============================================================================ LUT helpers
 namespace {
@@ -389,27 +442,35 @@ static bool col_live(const Blocks& c) {
     return false;
 }
 
-// Column compression until every column is a sum <= 6 (<= 7 at position 0) of <= 3 blocks.
+// Column compression until every column is a sum <= 6 (<= 7 at position 0) of <= 3 blocks.  A round
+// splits a column (greedy groups of degree <= 15 -> msg part here, carry part into the next column)
+// when the column, together with the carry parts it receives from below in the same round, would not
+// satisfy that bound -- so a column that is fine on its own but gains a carry part is split in the
+// same round (lo <= 3 + incoming hi <= 3), instead of rippling one column per round afterwards.
 static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
     for (;;) {
         std::vector<PbsItem> items;
         struct Dest {
-            ColProblem* p;
+            size_t pi;
             uint32_t col;
         };
         std::vector<Dest> dests;
         std::vector<std::vector<Blocks>> next(probs.size());
+        // degree / noise / count of the carry parts column k receives this round (trivially known)
         bool any = false;
         for (size_t pi = 0; pi < probs.size(); ++pi) {
             ColProblem& P = *probs[pi];
             next[pi].assign(P.nblocks, {});
+            uint32_t in_deg = 0, in_noise = 0, in_cnt = 0;
             for (uint32_t k = 0; k < P.nblocks; ++k) {
                 Blocks c;
                 for (Block& b : P.cols[k])
                     if (!(b.trivial() && b.value == 0)) c.push_back(b);
                 const uint32_t lim = k == 0 ? 7 : 6;
-                if (col_degree(c) <= lim && c.size() <= 3 && col_noise(c) <= kMaxNoise - 1) {
+                uint32_t out_deg = 0, out_noise = 0, out_cnt = 0;
+                if (col_degree(c) + in_deg <= lim && c.size() + in_cnt <= 3 && col_noise(c) + in_noise <= kMaxNoise - 1) {
                     for (auto& b : c) next[pi][k].push_back(b);
+                    in_deg = in_noise = in_cnt = 0;
                     continue;
                 }
                 any = true;
@@ -435,23 +496,26 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
                     lo.terms = g;
                     lo.table = LUT_MOD4();
                     items.push_back(lo);
-                    dests.push_back({probs[pi], k});
+                    dests.push_back({pi, k});
                     if (deg >= 4 && k + 1 < P.nblocks) {
                         PbsItem hi;
                         hi.terms = g;
                         hi.table = LUT_DIV4();
                         items.push_back(hi);
-                        dests.push_back({probs[pi], k + 1});
+                        dests.push_back({pi, k + 1});
+                        out_deg += std::min<uint32_t>(deg >> 2, 3);
+                        out_noise += 1;
+                        out_cnt += 1;
                     }
                 }
+                in_deg = out_deg;
+                in_noise = out_noise;
+                in_cnt = out_cnt;
             }
         }
         if (!any) return;
         Blocks outs = e.run(items);
-        for (size_t i = 0; i < outs.size(); ++i) {
-            size_t pi = std::find(probs.begin(), probs.end(), dests[i].p) - probs.begin();
-            next[pi][dests[i].col].push_back(outs[i]);
-        }
+        for (size_t i = 0; i < outs.size(); ++i) next[dests[i].pi][dests[i].col].push_back(outs[i]);
         for (size_t pi = 0; pi < probs.size(); ++pi) probs[pi]->cols = std::move(next[pi]);
     }
 }
@@ -564,7 +628,9 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
 
 // Carries of compressed columns (each column sum v_k <= 6, <= 7 at k = 0): cur[p][k] = carry out of
 // position k, k < nblocks - 1.  A problem with one extra empty top column yields its carry out.
-static std::vector<Blocks> propagate_carries(Engine& e, std::vector<ColProblem>& probs) {
+// `with`: extra items that run in the state level (their outputs in *with_out).
+static std::vector<Blocks> propagate_carries(Engine& e, std::vector<ColProblem>& probs,
+                                             const std::vector<PbsItem>* with = nullptr, Blocks* with_out = nullptr) {
     std::vector<ColProblem*> ptrs;
     for (auto& p : probs) {
         p.cols.resize(p.nblocks);
@@ -584,7 +650,10 @@ static std::vector<Blocks> propagate_carries(Engine& e, std::vector<ColProblem>&
             items.push_back(it);
         }
     }
+    const size_t nstate = items.size();
+    if (with) items.insert(items.end(), with->begin(), with->end());
     Blocks outs = e.run(items);
+    if (with_out) with_out->assign(outs.begin() + nstate, outs.end());
     size_t o = 0;
     for (size_t pi = 0; pi < probs.size(); ++pi) {
         const uint32_t m = probs[pi].nblocks ? probs[pi].nblocks - 1 : 0;
@@ -616,6 +685,55 @@ static std::vector<Radix> propagate_many(Engine& e, std::vector<ColProblem>& pro
     for (size_t pi = 0; pi < probs.size(); ++pi) {
         res[pi].blocks.assign(outs.begin() + o, outs.begin() + o + probs[pi].nblocks);
         o += probs[pi].nblocks;
+    }
+    return res;
+}
+
+// Window adds whose results stay lazy (see radix.h).
+std::vector<Radix> radix_sum_lazy(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& xs,
+                                  std::vector<Radix*>& refresh) {
+    static const auto LUT_ID = lut1([](uint32_t v) { return v & 3; });
+    // cleaning bootstraps of every lazy block in `refresh` (once per block), in the state level
+    std::vector<PbsItem> with;
+    std::vector<const void*> keys;
+    for (Radix* r : refresh)
+        for (const Block& b : r->blocks)
+            if (b.lazy() && std::find(keys.begin(), keys.end(), b.lin.get()) == keys.end()) {
+                with.push_back(item1(b, LUT_ID));
+                keys.push_back(b.lin.get());
+            }
+    std::vector<ColProblem> probs(xs.size());
+    for (size_t i = 0; i < xs.size(); ++i) {
+        const Radix &w = *xs[i].first, &x = *xs[i].second;
+        const uint32_t n = w.nblocks();
+        probs[i].nblocks = n + 1;  // empty top column: the carry out of the window (dropped)
+        probs[i].cols.assign(n + 1, {});
+        for (uint32_t k = 0; k < n; ++k) {
+            probs[i].cols[k].push_back(w.blocks[k]);
+            if (k < x.nblocks()) probs[i].cols[k].push_back(x.blocks[k]);
+        }
+    }
+    Blocks cleaned;
+    std::vector<Blocks> car = propagate_carries(e, probs, &with, &cleaned);
+    auto clean_of = [&](const Block& b) -> Block {
+        if (!b.lazy()) return b;
+        const size_t j = std::find(keys.begin(), keys.end(), b.lin.get()) - keys.begin();
+        engine_check(j < keys.size(), "lazy window block outside the refresh set");
+        return cleaned[j];
+    };
+    for (Radix* r : refresh)
+        for (Block& b : r->blocks) b = clean_of(b);
+    std::vector<Radix> res(xs.size());
+    for (size_t i = 0; i < xs.size(); ++i) {
+        const uint32_t n = xs[i].first->nblocks();
+        for (uint32_t k = 0; k < n; ++k) {
+            // out_k = v_k + c_{k-1} - 4 c_k, with a lazy window block replaced by its clean copy
+            std::vector<Term> t{{clean_of(xs[i].first->blocks[k]), 1}};
+            if (k < xs[i].second->nblocks()) t.push_back({xs[i].second->blocks[k], 1});
+            if (k > 0) t.push_back({car[i][k - 1], 1});
+            t.push_back({car[i][k], -4});
+            res[i].blocks.push_back(block_lazy(t, 0, 3));
+        }
     }
     return res;
 }

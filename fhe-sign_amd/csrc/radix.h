@@ -34,12 +34,20 @@ struct Slot {
     ~Slot();
 };
 
+struct Term;
+
 struct Block {
-    std::shared_ptr<Slot> slot;  // null => trivial
+    std::shared_ptr<Slot> slot;  // null => trivial (or lazy)
     uint32_t value = 0;          // trivial value
     uint32_t degree = 0;
     uint32_t noise = 0;
-    bool trivial() const { return !slot; }
+    // lazy: an un-bootstrapped linear combination sum coef * block + lin_cst of slot blocks whose
+    // value is known from the op structure to lie in [0, degree] (block_lazy); only ever a PBS
+    // input term, flattened into the descriptor by Engine::run
+    std::shared_ptr<const std::vector<Term>> lin;
+    int32_t lin_cst = 0;
+    bool trivial() const { return !slot && !lin; }
+    bool lazy() const { return (bool)lin; }
     const uint64_t* ptr() const { return slot ? slot->p : nullptr; }
     static Block make_trivial(uint32_t v) {
         Block b;
@@ -71,6 +79,9 @@ struct Term {
     int32_t coef;
 };
 
+// Lazy block of the given semantic range [0, degree] (caller's guarantee; noise = sum coef^2 noise).
+Block block_lazy(const std::vector<Term>& terms, int32_t cst, uint32_t degree);
+
 struct PbsItem {
     std::vector<Term> terms;
     uint32_t cst = 0;             // plaintext constant (units of one message step)
@@ -97,6 +108,7 @@ public:
 private:
     fhe_ctx* ctx_;
     std::shared_ptr<BlockPool> pool_;
+    bool trace_ = false;
     PbsDesc* h_desc_[2] = {nullptr, nullptr};  // pinned, double-buffered
     hipEvent_t desc_ev_[2] = {nullptr, nullptr};
     size_t desc_cap_ = 0;
@@ -129,6 +141,14 @@ Radix radix_sum(Engine& e, const std::vector<const Radix*>& xs, uint32_t nblocks
 // Independent sums advanced through shared levels (one launch pair per level for all of them).
 std::vector<Radix> radix_sum_many(Engine& e, const std::vector<std::vector<const Radix*>>& xs,
                                   const std::vector<uint32_t>& nblocks);
+// Wrapping window adds w_i + x_i (mod 2^(2 |w_i|)) whose results stay lazy: out_k = v_k + c_(k-1)
+// - 4 c_k as an un-bootstrapped combination (range [0, 3], noise 19), so a chain of adds skips the
+// final (v + c) mod 4 level.  Inputs: clean x_i; window blocks clean or lazy, where every lazy block
+// must belong to a Radix in `refresh` -- those get their cleaning bootstrap in this call's state
+// level (updated in place), and the outputs reference the clean copies.  Lazy blocks feed PBS
+// inputs only (one lazy term per input); radix_clean turns them back into blocks.
+std::vector<Radix> radix_sum_lazy(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& xs,
+                                  std::vector<Radix*>& refresh);
 // Carry propagation of raw column blocks (each column may hold several blocks).
 Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks);
 // Wrapping product.

@@ -1,0 +1,28 @@
+"""Per-level schedule trace of the headline ops (FHE_TRACE_LEVELS=1: the engine synchronizes after
+every level and prints its PBS count and wall time to stderr).
+usage: FHE_TRACE_LEVELS=1 python3 tools/level_trace.py [op ...]  (ops: mul_compat mul_fast sign div_enc)"""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd")); sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import random
+from fhe_sign import *
+
+ck, sk = generate_keys(seed=9)
+ctx = Context(0); ctx.set_server_key(sk); set_server_key(ctx)
+rng = random.Random(0xF11E51)
+a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(256) | 1 << 255
+A, B = BigUintFHE.new(a, ck), BigUintFHE.new(b, ck)
+A.add(B, FAST); ctx.sync()
+ops = sys.argv[1:] or ["mul_compat", "mul_fast", "sign"]
+for op in ops:
+    print(f"== {op}", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    if op == "mul_compat": A.mul(B, COMPAT)
+    elif op == "mul_fast": A.mul(B, FAST)
+    elif op == "sign":
+        d = 3; msg = bytes(32); k0 = compute_nonce(d, msg, bytes(32)); dF = BigUintFHE.new(d, ck)
+        Schnorr().sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT)
+    elif op == "div_enc":
+        FheUint64.try_encrypt(a % 2**64, ck).div_rem(FheUint64.try_encrypt(b % 2**40, ck))
+    ctx.sync()
+    print(f"== {op} total {time.perf_counter() - t0:.4f} s", file=sys.stderr, flush=True)
