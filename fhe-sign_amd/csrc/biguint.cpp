@@ -50,7 +50,37 @@ BigUint biguint_add(Engine& e, const BigUint& A, const BigUint& B, int mode) {
 //  * otherwise steps whose windows do not overlap commute, so each step runs in the first
 //    dependency wave after every earlier overlapping step, and a wave's window adds share levels;
 //    their sums stay lazy (v + c_in - 4 c_out, no final level) until the next wave's state level.
-BigUint biguint_mul(Engine& e, const BigUint& A, const BigUint& B, int mode) {
+static BigUint mul_impl(Engine& e, const BigUint& A, const BigUint& B, int mode, bool keep_lazy);
+
+BigUint biguint_mul(Engine& e, const BigUint& A, const BigUint& B, int mode) { return mul_impl(e, A, B, mode, false); }
+
+// k + a * b with the limbs of biguint_add(k, biguint_mul(a, b)) (src/schnorr.rs:274: the FHE block
+// of sign_fhe_with_k0).  When the product is exact (fast mode, or a one-limb factor) k enters the
+// product's columns, so the add costs no level at all; otherwise the compat product's last window
+// adds stay lazy and feed the add's state level directly.  Length rule of the add: max(lk, lp) + 1
+// limbs, a zero (empty) operand returns the other one.
+BigUint biguint_mul_add(Engine& e, const BigUint& A, const BigUint& B, const BigUint& K, int mode) {
+    const size_t la = A.digits.size(), lb = B.digits.size(), lk = K.digits.size();
+    if (la == 0 || lb == 0) return K;
+    const size_t lp = la + lb;
+    if (lk == 0) return biguint_mul(e, A, B, mode);
+    if (mode == kFast || la == 1 || lb == 1) {
+        std::vector<const Radix*> pa, pb, pk;
+        for (auto& d : A.digits) pa.push_back(&d);
+        for (auto& d : B.digits) pb.push_back(&d);
+        for (auto& d : K.digits) pk.push_back(&d);
+        Radix wa = concat(pa), wb = concat(pb), wk = concat(pk);
+        const size_t len = std::max(lk, lp) + 1;
+        Radix s = radix_mul_add(e, wa, wb, wk, (uint32_t)len * kLimbBlocks);
+        BigUint out;
+        for (size_t i = 0; i < len; ++i) out.digits.push_back(slice(s, (uint32_t)i * kLimbBlocks, kLimbBlocks));
+        return out;
+    }
+    BigUint p = mul_impl(e, A, B, mode, true);
+    return biguint_add(e, K, p, mode);
+}
+
+static BigUint mul_impl(Engine& e, const BigUint& A, const BigUint& B, int mode, bool keep_lazy) {
     const size_t la = A.digits.size(), lb = B.digits.size();
     BigUint out;
     if (la == 0 || lb == 0) return out;
@@ -108,7 +138,7 @@ BigUint biguint_mul(Engine& e, const BigUint& A, const BigUint& B, int mode) {
             for (size_t t = 0; t < wave[s].wl; ++t)
                 R[wave[s].idx + t] = slice(S[s], (uint32_t)t * kLimbBlocks, kLimbBlocks);
     }
-    {
+    if (!keep_lazy) {
         Radix all;
         for (auto& r : R) all.blocks.insert(all.blocks.end(), r.blocks.begin(), r.blocks.end());
         std::vector<PbsItem> items;

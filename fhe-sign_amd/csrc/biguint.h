@@ -24,5 +24,7 @@ enum BigUintMode : int {
 
 BigUint biguint_add(Engine& e, const BigUint& a, const BigUint& b, int mode);
 BigUint biguint_mul(Engine& e, const BigUint& a, const BigUint& b, int mode);
+// k + a * b, limbs identical to biguint_add(k, biguint_mul(a, b)) (src/schnorr.rs:274)
+BigUint biguint_mul_add(Engine& e, const BigUint& a, const BigUint& b, const BigUint& k, int mode);
 
 }  // namespace fhe

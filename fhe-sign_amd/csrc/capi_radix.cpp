@@ -467,6 +467,19 @@ int fhe_biguint_mul(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, int 
     });
 }
 
+int fhe_biguint_mul_add(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, const fhe_biguint* k, int mode,
+                        fhe_biguint** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !b || !k || !out) return FHE_ERR_INVALID;
+    return guarded([&] {
+        auto* r = new fhe_biguint();
+        r->v = biguint_mul_add(*c->engine, a->v, b->v, k->v, mode);
+        *out = r;
+        return FHE_OK;
+    });
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------------- serialization

@@ -815,7 +815,7 @@ static void add_products(const Radix& a, const Radix& b, uint32_t nblocks, std::
 }
 
 std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
-                                  uint32_t nblocks) {
+                                  uint32_t nblocks, const std::vector<const Radix*>& addends) {
     std::vector<PbsItem> items;
     std::vector<uint32_t> cols_of;
     std::vector<size_t> start(ops.size() + 1, 0);
@@ -830,12 +830,19 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
         probs[i].nblocks = nblocks;
         probs[i].cols.assign(nblocks, {});
         for (size_t j = start[i]; j < start[i + 1]; ++j) probs[i].cols[cols_of[j]].push_back(outs[j]);
+        if (i < addends.size() && addends[i])
+            for (uint32_t k = 0; k < nblocks && k < addends[i]->nblocks(); ++k)
+                probs[i].cols[k].push_back(addends[i]->blocks[k]);
     }
     return propagate_many(e, probs);
 }
 
 Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {
     return radix_mul_many(e, {{&a, &b}}, nblocks)[0];
+}
+
+Radix radix_mul_add(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks) {
+    return radix_mul_many(e, {{&a, &b}}, nblocks, {&c})[0];
 }
 
 // ============================================================================ scalar ops

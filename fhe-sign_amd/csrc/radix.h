@@ -153,9 +153,12 @@ std::vector<Radix> radix_sum_lazy(Engine& e, const std::vector<std::pair<const R
 Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks);
 // Wrapping product.
 Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks);
-// Batched independent products (one level schedule for all).
+// Batched independent products (one level schedule for all); addends[i], if given, is summed into
+// product i's columns before its carry propagation (a multiply-add costs no extra level).
 std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
-                                  uint32_t nblocks);
+                                  uint32_t nblocks, const std::vector<const Radix*>& addends = {});
+// a * b + c (wrapping at nblocks), one carry propagation.
+Radix radix_mul_add(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks);
 Radix radix_scalar_and(Engine& e, const Radix& a, const BigConst& mask);
 Radix radix_scalar_shr(Engine& e, const Radix& a, uint32_t bits);
 Radix radix_scalar_shl(Engine& e, const Radix& a, uint32_t bits);

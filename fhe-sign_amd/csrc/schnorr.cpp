@@ -412,11 +412,11 @@ int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t
     } else {
         // FHE block (src/schnorr.rs:272-276)
         std::vector<uint32_t> el = u32_digits(c.e), kl = u32_digits(c.k);
-        fhe_biguint *e_fhe = nullptr, *k_fhe = nullptr, *prod = nullptr, *s_fhe = nullptr;
+        fhe_biguint *e_fhe = nullptr, *k_fhe = nullptr, *s_fhe = nullptr;
         rc = fhe_biguint_encrypt(ctx, ck, el.data(), el.size(), &e_fhe);
         if (!rc) rc = fhe_biguint_encrypt(ctx, ck, kl.data(), kl.size(), &k_fhe);
-        if (!rc) rc = fhe_biguint_mul(ctx, e_fhe, privkey_fhe, mode, &prod);
-        if (!rc) rc = fhe_biguint_add(ctx, k_fhe, prod, mode, &s_fhe);
+        // k_fhe + e_fhe * privkey_fhe as one schedule (limbs identical to the mul, then the add)
+        if (!rc) rc = fhe_biguint_mul_add(ctx, e_fhe, privkey_fhe, k_fhe, mode, &s_fhe);
         if (!rc) {
             size_t n = 0;
             fhe_biguint_len(s_fhe, &n);
@@ -426,7 +426,6 @@ int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t
         }
         fhe_biguint_destroy(e_fhe);
         fhe_biguint_destroy(k_fhe);
-        fhe_biguint_destroy(prod);
         fhe_biguint_destroy(s_fhe);
         if (rc) return rc;
     }

@@ -112,6 +112,7 @@ _SIGNATURES = [
     ("fhe_biguint_destroy", None, [C.c_void_p]),
     ("fhe_biguint_add", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_mul", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    ("fhe_biguint_mul_add", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     ("fhe_schnorr_public_key", C.c_int, [u8p, u8p]),
     ("fhe_schnorr_compute_nonce", C.c_int, [u8p, u8p, C.c_size_t, u8p, u8p]),
     ("fhe_schnorr_sign_with_k0", C.c_int, [u8p, C.c_size_t, u8p, u8p, u8p]),

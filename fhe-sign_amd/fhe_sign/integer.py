@@ -337,6 +337,12 @@ class BigUintFHE:
         check(load().fhe_biguint_mul(_ctx().handle, self._h, other._h, mode, C.byref(h)))
         return BigUintFHE(h)
 
+    def mul_add(self, other, addend, mode: int = COMPAT):
+        """addend + self * other, limbs identical to addend.add(self.mul(other)) (one schedule)"""
+        h = C.c_void_p()
+        check(load().fhe_biguint_mul_add(_ctx().handle, self._h, other._h, addend._h, mode, C.byref(h)))
+        return BigUintFHE(h)
+
     __add__ = add
     __mul__ = mul
 

@@ -239,6 +239,11 @@ void fhe_biguint_destroy(fhe_biguint* x);
 /* impl Add / impl Mul for BigUintFHE (src/biguint.rs:120-265); inputs are not consumed */
 int fhe_biguint_add(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, int mode, fhe_biguint** out);
 int fhe_biguint_mul(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, int mode, fhe_biguint** out);
+/* k + a * b with the limbs of fhe_biguint_add(k, fhe_biguint_mul(a, b)) -- the FHE block of
+ * sign_fhe_with_k0 (src/schnorr.rs:274) in one schedule: no level spent on the add when the product
+ * is exact (fast mode or a one-limb factor), one fewer otherwise */
+int fhe_biguint_mul_add(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, const fhe_biguint* k, int mode,
+                        fhe_biguint** out);
 /* serialization of the limb vector (format of fhe_radix_serialize; every limb is a 32-bit radix) */
 int fhe_biguint_serialize(fhe_ctx* ctx, const fhe_biguint* x, uint8_t* buf, size_t cap, size_t* len);
 int fhe_biguint_deserialize(fhe_ctx* ctx, const uint8_t* buf, size_t len, fhe_biguint** out);

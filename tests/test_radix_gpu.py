@@ -166,3 +166,24 @@ def test_sign_fhe_with_k0_vector0_limb_flow(keys):
     s = k + prod
     assert s.decrypt_limbs(ck) == v["sum"]
     assert s.to_biguint(ck) % R.N == int(v["s"], 16)
+
+
+def test_biguint_mul_add_equals_mul_then_add(keys):
+    """fhe_biguint_mul_add (the signer's FHE block k + e*d' in one schedule) gives the limbs of
+    add(k, mul(a, b)) of src/biguint.rs in both modes: exact 8x1 (k enters the product columns), the
+    8x8 compat product with the F7 lost carry (lazy last waves feed the add), fast, zero operands."""
+    ck, _ = keys
+    v = json.load(open(os.path.join(G, "sign_vectors.json")))["vectors"][0]
+    e, d, k = _big(ck, v["e"]), _big(ck, v["d"]), _big(ck, v["k"])
+    assert e.mul_add(d, k).decrypt_limbs(ck) == v["sum"]
+    q = json.load(open(os.path.join(G, "biguint_vectors.json")))["quirk_mul"][0]
+    rng = random.Random(0x5EED)
+    kl = R.to_u32_digits(rng.getrandbits(256))
+    a, b, kk = _big(ck, q["a"]), _big(ck, q["b"]), _big(ck, kl)
+    assert a.mul_add(b, kk, COMPAT).decrypt_limbs(ck) == R.biguint_add(kl, R.biguint_mul(q["a"], q["b"]))
+    got = a.mul_add(b, kk, FAST).decrypt_limbs(ck)
+    assert R.from_limbs(got) == R.from_limbs(kl) + R.from_limbs(q["a"]) * R.from_limbs(q["b"])
+    assert len(got) == max(len(kl), len(q["a"]) + len(q["b"])) + 1
+    zero = BigUintFHE.new(0, ck)
+    assert a.mul_add(zero, kk).decrypt_limbs(ck) == kl
+    assert a.mul_add(b, zero, COMPAT).decrypt_limbs(ck) == R.biguint_mul(q["a"], q["b"])
