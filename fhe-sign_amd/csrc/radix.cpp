@@ -1201,7 +1201,8 @@ Radix radix_clean(Engine& e, const Radix& a) {
 // the carry passes them only where c d's block is zero).  q_i = ge_1 + ge_2 + ge_3 (one bootstrap,
 // in the subtractions' final level), the remainder is the candidate picked by q_i (half-selects
 // f(4 q_i + cand), noise 16 + 1), cleaned.  d = 0 gives q = 2^bits - 1 and r = a (every ge_c = 1),
-// tfhe's convention.  Levels per step: 4 + log2(w + 2).
+// tfhe's convention.  The remainder stays a lazy sum of its half-selects between steps (one
+// cleaning level at the end).  Levels per step: 3 + the carry prefix depth of w + 2 positions.
 std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) {
     const uint32_t n = a.nblocks(), W = n + 1;
     Radix d1 = radix_resize(d, W);
@@ -1295,17 +1296,13 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
                 hs.push_back(it);
             }
         Blocks h = e.run(hs);
-        std::vector<PbsItem> fin;
-        for (uint32_t k = 0; k < w; ++k) {
-            PbsItem it;
-            for (uint32_t c = 0; c < 4; ++c) it.terms.push_back({h[4 * k + c], 1});
-            it.table = LUT_MOD4();
-            fin.push_back(it);
-        }
-        r = e.run(fin);
-        for (Block& b : r) b.degree = std::min<uint32_t>(b.degree, 3);
+        // r_k = sum of the four half-selects (exactly one nonzero): kept lazy (noise 4), it enters
+        // the next step's columns and half-selects directly -- no cleaning level per step
+        r.assign(w, Block());
+        for (uint32_t k = 0; k < w; ++k)
+            r[k] = block_lazy({{h[4 * k], 1}, {h[4 * k + 1], 1}, {h[4 * k + 2], 1}, {h[4 * k + 3], 1}}, 0, 3);
     }
-    return {q, Radix{r}};
+    return {q, radix_clean(e, Radix{r})};
 }
 
 Radix radix_scalar_rem(Engine& e, const Radix& a, const BigConst& d) {
