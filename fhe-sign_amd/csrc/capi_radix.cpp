@@ -321,6 +321,12 @@ int fhe_radix_scalar_mul_words(fhe_ctx* c, const fhe_radix* a, const uint64_t* s
     const BigConst v = words_of(s, nwords);
     return unop(c, a, out, [&v](Engine& e, const Radix& x) { return radix_scalar_mul(e, x, v); });
 }
+int fhe_radix_scalar_mul_add_words(fhe_ctx* c, const fhe_radix* a, const uint64_t* m, size_t nm, const uint64_t* k,
+                                   size_t nk, fhe_radix** out) {
+    if ((!m && nm) || (!k && nk)) return FHE_ERR_INVALID;
+    const BigConst vm = words_of(m, nm), vk = words_of(k, nk);
+    return unop(c, a, out, [&](Engine& e, const Radix& x) { return radix_scalar_mul_add(e, x, vm, vk); });
+}
 static bool all_zero(const uint64_t* s, size_t n) {
     for (size_t i = 0; i < n; ++i)
         if (s[i]) return false;

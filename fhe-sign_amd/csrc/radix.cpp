@@ -534,64 +534,175 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
 // (F_t + 3^(t+1)), i.e. about log3 of the width levels (radix-2 Hillis-Steele: log2).  Only nodes
 // that some requested carry depends on are bootstrapped (`want`: the positions whose carry is
 // needed; empty = all).
+//
+// Top run of propagate-or-kill positions.  When every position from G up can only propagate or
+// kill (state degree <= 1: e.g. a window add whose top limb receives no addend), the chain over
+// [G, k] is an AND: level 1 takes prefix ANDs in chunks of six (sum == count), level 2 joins up to
+// three chunks with the generic state of position G - 1 as x = 4 s + sum(chunks) (state s if every
+// chunk propagates, else kill; noise 16 + 3), and level 3 resolves [0, k] as that node + the level-2
+// chain below G - 1 (<= 2 states + a carry).  For G <= 32 this resolves up to G + 18 positions in
+// three levels, where the generic front reaches 40: a compat-mul window add (48 carries: 32 generic
+// below a 16-block top limb) takes 3 prefix levels instead of 4.
+namespace {
+struct PNode {
+    uint32_t lo;  // covers positions [lo, pos]
+    bool done;    // the value is the carry-out bit of the position
+    int level;
+    std::vector<std::pair<int, int32_t>> terms;  // (node id, coefficient)
+    std::vector<uint32_t> table;
+    bool need = false;
+};
+
+std::vector<uint32_t> chain_table(int states, bool done) {
+    const uint32_t full = 1u << states;
+    return done ? lut1([full](uint32_t x) { return x >= full ? 1u : 0u; })
+                : lut1([full](uint32_t x) { return x >= full ? 2u : (x == full - 1 ? 1u : 0u); });
+}
+
+// One generic greedy level over positions [0, m): each unresolved position chains its window with
+// up to two windows below it and, if the next one down is resolved, its carry.
+bool greedy_level(std::vector<PNode>& nodes, std::vector<int>& latest, uint32_t m, int t) {
+    const std::vector<int> snap = latest;
+    bool any = false;
+    for (uint32_t k = 0; k < m; ++k) {
+        const PNode& top = nodes[snap[k]];
+        if (top.done) continue;
+        any = true;
+        PNode n{top.lo, false, t, {{snap[k], 0}}, {}};
+        int states = 1;
+        while (n.lo > 0) {
+            const PNode& below = nodes[snap[n.lo - 1]];
+            if (below.done) {
+                n.terms.push_back({snap[n.lo - 1], 1});
+                n.lo = 0;
+                n.done = true;
+                break;
+            }
+            if (states == 3) break;
+            n.terms.push_back({snap[n.lo - 1], 0});
+            n.lo = below.lo;
+            ++states;
+        }
+        for (int i = 0; i < states; ++i) n.terms[i].second = 1 << (states - 1 - i);
+        n.table = chain_table(states, n.done);
+        latest[k] = (int)nodes.size();
+        nodes.push_back(std::move(n));
+    }
+    return any;
+}
+}  // namespace
+
 static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const std::vector<std::vector<uint32_t>>& want) {
-    struct Node {
-        uint32_t pos, lo;   // covers positions [lo, pos]
-        bool done;          // lo == 0: the value is the carry-out bit
-        int level;
-        std::vector<int> terms;  // node ids: states top-down, then (if done) the carry bit
-        bool need = false;
-    };
     const size_t P = in.size();
-    std::vector<std::vector<Node>> nodes(P);
-    std::vector<std::vector<int>> latest(P);
+    std::vector<std::vector<PNode>> nodes(P);
+    std::vector<std::vector<int>> result(P);
     int levels = 0;
     for (size_t p = 0; p < P; ++p) {
         const uint32_t m = (uint32_t)in[p].size();
+        std::vector<PNode> base;
+        std::vector<int> latest;
         for (uint32_t k = 0; k < m; ++k) {
-            nodes[p].push_back({k, k, k == 0, 0, {}});
-            latest[p].push_back((int)k);
+            base.push_back({k, k == 0, 0, {}, {}});
+            latest.push_back((int)k);
         }
-        for (int t = 1;; ++t) {
-            const std::vector<int> snap = latest[p];
-            bool any = false;
-            for (uint32_t k = 0; k < m; ++k) {
-                const Node& top = nodes[p][snap[k]];
-                if (top.done) continue;
-                any = true;
-                Node n{k, top.lo, false, t, {snap[k]}};
+        // generic plan over all positions
+        std::vector<PNode> gen = base;
+        std::vector<int> glat = latest;
+        int glev = 0;
+        while (greedy_level(gen, glat, m, glev + 1)) ++glev;
+        // top propagate/kill run [G, m)
+        uint32_t G = m;
+        while (G > 1 && in[p][G - 1].degree <= 1) --G;
+        bool special = glev > 3 && G >= 2 && G <= 32 && m - G <= 18;
+        if (special) {
+            std::vector<PNode> nd = base;
+            std::vector<int> lat = latest;
+            std::vector<std::vector<int>> snaps{lat};
+            int lev = 0;
+            // generic part below G, recording every level's latest nodes
+            while (lev < 3 && greedy_level(nd, lat, G, lev + 1)) {
+                ++lev;
+                snaps.push_back(lat);
+            }
+            while ((int)snaps.size() < 4) snaps.push_back(lat);
+            std::vector<int> top(m, -1);
+            // level 1: prefix ANDs inside chunks of six
+            std::vector<int> q(m, -1);
+            for (uint32_t k = G; k < m; ++k) {
+                const uint32_t start = G + 6 * ((k - G) / 6);
+                PNode n{start, false, 1, {}, {}};
+                for (uint32_t j = start; j <= k; ++j) n.terms.push_back({(int)j, 1});
+                const uint32_t cnt = k - start + 1;
+                n.table = lut1([cnt](uint32_t x) { return x == cnt ? 1u : 0u; });
+                q[k] = (int)nd.size();
+                nd.push_back(std::move(n));
+            }
+            // level 2: T_k = state of [G - 1, k]
+            std::vector<int> T(m, -1);
+            for (uint32_t k = G; k < m; ++k) {
+                const uint32_t chunk = (k - G) / 6;
+                PNode n{G - 1, false, 2, {{(int)(G - 1), 4}}, {}};
+                for (uint32_t c = 0; c < chunk; ++c) n.terms.push_back({q[G + 6 * c + 5], 1});
+                n.terms.push_back({q[k], 1});
+                const uint32_t na = chunk + 1;
+                n.table = lut1([na](uint32_t x) { return (x & 3) == na ? (x >> 2) : 0u; });
+                T[k] = (int)nd.size();
+                nd.push_back(std::move(n));
+            }
+            // level 3: T_k + the level-2 chain below G - 1
+            for (uint32_t k = G; k < m && special; ++k) {
+                PNode n{G - 1, false, 3, {{T[k], 0}}, {}};
                 int states = 1;
+                const std::vector<int>& s2 = snaps[2];
                 while (n.lo > 0) {
-                    const Node& below = nodes[p][snap[n.lo - 1]];
+                    const PNode& below = nd[s2[n.lo - 1]];
                     if (below.done) {
-                        n.terms.push_back(snap[n.lo - 1]);
+                        n.terms.push_back({s2[n.lo - 1], 1});
                         n.lo = 0;
                         n.done = true;
                         break;
                     }
                     if (states == 3) break;
-                    n.terms.push_back(snap[n.lo - 1]);
+                    n.terms.push_back({s2[n.lo - 1], 0});
                     n.lo = below.lo;
                     ++states;
                 }
-                latest[p][k] = (int)nodes[p].size();
-                nodes[p].push_back(std::move(n));
+                if (!n.done) {
+                    special = false;
+                    break;
+                }
+                for (int i = 0; i < states; ++i) n.terms[i].second = 1 << (states - 1 - i);
+                n.table = chain_table(states, true);
+                top[k] = (int)nd.size();
+                nd.push_back(std::move(n));
             }
-            if (!any) break;
-            levels = std::max(levels, t);
+            // the generic part must be resolved by level 3 as well
+            for (uint32_t k = 0; k < G && special; ++k)
+                if (!nd[lat[k]].done) special = false;
+            if (special) {
+                for (uint32_t k = G; k < m; ++k) lat[k] = top[k];
+                nodes[p] = std::move(nd);
+                result[p] = std::move(lat);
+                levels = std::max(levels, 3);
+            }
+        }
+        if (!special) {
+            nodes[p] = std::move(gen);
+            result[p] = std::move(glat);
+            levels = std::max(levels, glev);
         }
         // mark what the requested carries depend on
         std::vector<int> stack;
         if (p < want.size() && !want[p].empty())
-            for (uint32_t k : want[p]) stack.push_back(latest[p][k]);
+            for (uint32_t k : want[p]) stack.push_back(result[p][k]);
         else
-            stack = latest[p];
+            stack = result[p];
         while (!stack.empty()) {
-            Node& n = nodes[p][stack.back()];
+            PNode& n = nodes[p][stack.back()];
             stack.pop_back();
             if (n.need) continue;
             n.need = true;
-            for (int t : n.terms) stack.push_back(t);
+            for (auto& t : n.terms) stack.push_back(t.first);
         }
     }
     std::vector<std::vector<Block>> val(P);
@@ -604,15 +715,11 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
         std::vector<std::pair<size_t, int>> refs;
         for (size_t p = 0; p < P; ++p)
             for (size_t id = 0; id < nodes[p].size(); ++id) {
-                const Node& n = nodes[p][id];
+                const PNode& n = nodes[p][id];
                 if (n.level != t || !n.need) continue;
-                const int states = (int)n.terms.size() - (n.done ? 1 : 0);
                 PbsItem it;
-                for (int i = 0; i < states; ++i) it.terms.push_back({val[p][n.terms[i]], 1 << (states - 1 - i)});
-                if (n.done) it.terms.push_back({val[p][n.terms.back()], 1});
-                const uint32_t full = 1u << states;
-                it.table = n.done ? lut1([full](uint32_t x) { return x >= full ? 1u : 0u; })
-                                  : lut1([full](uint32_t x) { return x >= full ? 2u : (x == full - 1 ? 1u : 0u); });
+                for (auto& tm : n.terms) it.terms.push_back({val[p][tm.first], tm.second});
+                it.table = n.table;
                 items.push_back(std::move(it));
                 refs.push_back({p, (int)id});
             }
@@ -622,7 +729,7 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
     }
     std::vector<Blocks> res(P);
     for (size_t p = 0; p < P; ++p)
-        for (size_t k = 0; k < in[p].size(); ++k) res[p].push_back(val[p][latest[p][k]]);
+        for (size_t k = 0; k < in[p].size(); ++k) res[p].push_back(val[p][result[p][k]]);
     return res;
 }
 
@@ -910,6 +1017,10 @@ Radix radix_scalar_add(Engine& e, const Radix& a, const BigConst& s) {
 Radix radix_scalar_mul(Engine& e, const Radix& a, const BigConst& s) {
     Radix t = radix_trivial(s, a.nblocks());
     return radix_mul(e, a, t, a.nblocks());
+}
+Radix radix_scalar_mul_add(Engine& e, const Radix& a, const BigConst& m, const BigConst& c) {
+    Radix tm = radix_trivial(m, a.nblocks()), tc = radix_trivial(c, a.nblocks());
+    return radix_mul_add(e, a, tm, tc, a.nblocks());
 }
 
 // ---- clear multi-word arithmetic for the division constants (host only, a few hundred bits)

@@ -164,6 +164,8 @@ Radix radix_scalar_shr(Engine& e, const Radix& a, uint32_t bits);
 Radix radix_scalar_shl(Engine& e, const Radix& a, uint32_t bits);
 Radix radix_scalar_add(Engine& e, const Radix& a, const BigConst& s);
 Radix radix_scalar_mul(Engine& e, const Radix& a, const BigConst& s);
+// a * m + c for clear m, c (wrapping), one carry propagation
+Radix radix_scalar_mul_add(Engine& e, const Radix& a, const BigConst& m, const BigConst& c);
 // floor(a / d) and a mod d for a clear divisor d != 0 of any width (Granlund-Montgomery multiply)
 Radix radix_scalar_div(Engine& e, const Radix& a, const BigConst& d);
 Radix radix_scalar_rem(Engine& e, const Radix& a, const BigConst& d);

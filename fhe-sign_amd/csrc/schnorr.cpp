@@ -391,22 +391,20 @@ int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t
         fhe_biguint_len(privkey_fhe, &L);
         const uint32_t kBits = (uint32_t)(32 * L + 258);
         if (kBits > FHE_RADIX_MAX_BITS) return FHE_ERR_INVALID;
-        fhe_radix *d = nullptr, *ed = nullptr, *sr = nullptr;
+        fhe_radix *d = nullptr, *sr = nullptr;
         uint64_t ew[4], kw[4];
         for (int i = 0; i < 4; ++i) {
             ew[i] = c.e.w[i];
             kw[i] = c.k.w[i];
         }
         rc = fhe_biguint_to_radix(privkey_fhe, kBits, &d);
-        if (!rc) rc = fhe_radix_scalar_mul_words(ctx, d, ew, 4, &ed);
-        if (!rc) rc = fhe_radix_scalar_add_words(ctx, ed, kw, 4, &sr);
+        if (!rc) rc = fhe_radix_scalar_mul_add_words(ctx, d, ew, 4, kw, 4, &sr);
         if (!rc) {
             std::vector<uint64_t> w((kBits + 63) / 64);
             rc = fhe_radix_decrypt(ctx, ck, sr, w.data(), w.size());
             for (uint32_t i = 0; i < kBits / 32 + 1 && !rc; ++i) limbs.push_back((uint32_t)(w[i / 2] >> (32 * (i % 2))));
         }
         fhe_radix_destroy(d);
-        fhe_radix_destroy(ed);
         fhe_radix_destroy(sr);
         if (rc) return rc;
     } else {

@@ -92,6 +92,8 @@ _SIGNATURES = [
     ("fhe_radix_scalar_and_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_add_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_mul_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_mul_add_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t,
+                                                C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_div_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_rem_words", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_radix_cast", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),

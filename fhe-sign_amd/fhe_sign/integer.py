@@ -134,6 +134,15 @@ class FheUint:
     def __mul__(self, o):
         return self._bin("fhe_radix_mul", o) if isinstance(o, FheUint) else self._scalar_any("fhe_radix_scalar_mul", o)
 
+    def scalar_mul_add(self, m: int, k: int):
+        """self * m + k for clear m, k (wrapping), one carry propagation"""
+        wm, wk = _words(m, self.bits), _words(k, self.bits)
+        h = C.c_void_p()
+        P = C.POINTER(C.c_uint64)
+        check(load().fhe_radix_scalar_mul_add_words(_ctx().handle, self._h, wm.ctypes.data_as(P), len(wm),
+                                                     wk.ctypes.data_as(P), len(wk), C.byref(h)))
+        return self._wrap(h, self.bits)
+
     def __and__(self, o):
         return self._bin("fhe_radix_bitand", o) if isinstance(o, FheUint) else self._scalar_any("fhe_radix_scalar_and", o)
 

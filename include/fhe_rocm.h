@@ -189,6 +189,9 @@ int fhe_radix_scalar_rem(fhe_ctx* ctx, const fhe_radix* a, uint64_t d, fhe_radix
 int fhe_radix_scalar_and_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out);
 int fhe_radix_scalar_add_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out);
 int fhe_radix_scalar_mul_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* s, size_t nwords, fhe_radix** out);
+/* a * m + k for clear m, k (wrapping at a's width) in one carry propagation */
+int fhe_radix_scalar_mul_add_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* m, size_t nm, const uint64_t* k,
+                                   size_t nk, fhe_radix** out);
 int fhe_radix_scalar_div_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* d, size_t nwords, fhe_radix** out);
 int fhe_radix_scalar_rem_words(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* d, size_t nwords, fhe_radix** out);
 /* Ciphertext serialization (radix integers and BigUintFHE limb vectors; same format as the keys).

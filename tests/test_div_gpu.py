@@ -69,6 +69,8 @@ def test_wide_scalar_ops(keys):
     assert (A & s).decrypt(ck) == a & s
     assert (A + s).decrypt(ck) == (a + s) & m
     assert (A * s).decrypt(ck) == (a * s) & m
+    k = rng.getrandbits(128)
+    assert A.scalar_mul_add(s, k).decrypt(ck) == (a * s + k) & m
 
 
 @pytest.mark.parametrize("bits,cls", [(8, FheUint8), (32, FheUint32)])
