@@ -474,18 +474,28 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
                     continue;
                 }
                 any = true;
-                // greedy groups: degree sum <= 15, noise sum <= kMaxNoise, <= kMaxTerms blocks
+                // groups: degree sum <= 15, noise sum <= kMaxNoise, <= kMaxTerms blocks.  Largest
+                // first while the group's remaining slots can still take the smallest blocks, else
+                // the smallest: mixes degree-3 low and degree-2 high product halves 3 + 3 (six
+                // blocks per split) where largest-first packs five.
                 std::sort(c.begin(), c.end(), [](const Block& a, const Block& b) { return a.degree > b.degree; });
-                size_t s = 0;
-                while (s < c.size()) {
+                size_t s = 0, end = c.size();  // unassigned: c[s, end)
+                while (s < end) {
                     std::vector<Term> g;
                     uint32_t deg = 0, noi = 0;
-                    while (s < c.size() && g.size() < (size_t)kMaxTerms && deg + c[s].degree <= 15 &&
-                           noi + c[s].noise <= kMaxNoise) {
-                        g.push_back({c[s], 1});
-                        deg += c[s].degree;
-                        noi += c[s].noise;
-                        ++s;
+                    while (s < end && g.size() < (size_t)kMaxTerms) {
+                        const uint32_t mn = c[end - 1].degree;
+                        const size_t slots = std::min<size_t>((size_t)kMaxTerms - g.size() - 1, end - s - 1);
+                        const Block* pick = nullptr;
+                        if (deg + c[s].degree + slots * mn <= 15 && noi + c[s].noise <= kMaxNoise)
+                            pick = &c[s++];
+                        else if (deg + mn <= 15 && noi + c[end - 1].noise <= kMaxNoise)
+                            pick = &c[--end];
+                        else
+                            break;
+                        g.push_back({*pick, 1});
+                        deg += pick->degree;
+                        noi += pick->noise;
                     }
                     engine_check(!g.empty(), "column block too large to compress");
                     if (g.size() == 1 && deg <= 3 && g[0].b.noise <= 1) {
