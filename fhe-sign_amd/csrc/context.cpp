@@ -488,6 +488,14 @@ int fhe_ctx_export_fourier_bsk(fhe_ctx* c, double* out, size_t len) {
 
 int fhe_ctx_sync(fhe_ctx* c) {
     if (!c) return FHE_ERR_INVALID;
+    if (c->engine) {
+        try {
+            c->engine->flush();  // launch the deferred radix graph
+        } catch (const std::exception& e) {
+            set_error(e.what());
+            return FHE_ERR_HIP;
+        }
+    }
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
     return FHE_OK;
 }

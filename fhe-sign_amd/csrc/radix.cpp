@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <queue>
 #include <stdexcept>
 
 namespace fhe {
@@ -64,6 +65,8 @@ Engine::Engine(fhe_ctx* ctx) : ctx_(ctx) {
     // FHE_TRACE_LEVELS=1: synchronize after every level and print its size and wall time (stderr);
     // a diagnostic for schedule work, never set by the bench or the tests.
     if (const char* t = getenv("FHE_TRACE_LEVELS")) trace_ = atoi(t) != 0;
+    // FHE_SCHED=1: forward (deadline-driven) list scheduling instead of the default backward one
+    if (const char* t = getenv("FHE_SCHED")) sched_ = atoi(t);
 }
 
 Engine::~Engine() {
@@ -182,25 +185,16 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     }
     if (gpu.empty()) return out;
 
-    // register LUTs, allocate destinations, build descriptors
-    const size_t G = gpu.size();
-    const int W = ctx_->fanout_world();
-    const bool split = W > 1 && G >= ctx_->fanout_min;
-    const size_t chunk = split ? (G + W - 1) / W : G;
-    if (split) engine_check(ctx_->ensure_gather(chunk * W) == FHE_OK, "gather workspace");
-    // descriptors, then (fanned-out levels) the destination slot table, in one pinned staging copy
-    const size_t ndesc = G + (split ? (G * sizeof(uint64_t*) + sizeof(PbsDesc) - 1) / sizeof(PbsDesc) : 0);
-    PbsDesc* dev = nullptr;
-    PbsDesc* h = stage_desc(ndesc, &dev);
-    uint64_t** h_scat = reinterpret_cast<uint64_t**>(h + G);
+    // register LUTs, allocate destinations, record pending nodes
     const uint64_t delta = p.delta();
-    for (size_t g = 0; g < G; ++g) {
-        const size_t i = gpu[g];
+    for (size_t i : gpu) {
         uint32_t lut = 0;
         engine_check(ctx_->register_lut(items[i].table.data(), &lut) == FHE_OK, "LUT registration");
         out[i].slot = pool_->alloc();
-        PbsDesc d;
+        Pending n;
+        PbsDesc& d = n.d;
         std::memset(&d, 0, sizeof d);
+        n.hold.push_back(out[i].slot);
         // flatten lazy terms into their slot blocks (merging repeats)
         int64_t dcst = csts[i];
         uint32_t nt = 0;
@@ -213,6 +207,8 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
             engine_check(nt < (uint32_t)kMaxTerms, "too many terms in one PBS input");
             d.src[nt] = b.ptr();
             d.coef[nt++] = coef;
+            n.hold.push_back(b.slot);
+            if (b.slot->node >= 0) n.deps.push_back((int32_t)b.slot->node);
         };
         for (const Term& t : live[i]) {
             if (!t.b.lazy()) {
@@ -225,45 +221,183 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         d.nterms = nt;
         d.lut = lut;
         d.cst = (uint64_t)dcst * delta;
-        // fanned-out levels bootstrap into the gather buffer (segment = owning rank), then scatter
-        d.dst = split ? ctx_->d_gather + g * kBigCt : out[i].slot->p;
-        if (split) h_scat[g] = out[i].slot->p;
-        h[g] = d;
+        d.dst = out[i].slot->p;
+        out[i].slot->node = (int64_t)pending_.size();
+        pending_.push_back(std::move(n));
     }
-    engine_check(ctx_->sync_luts() == FHE_OK, "LUT upload");
-    engine_check(ctx_->ensure_ms(chunk) == FHE_OK, "workspace");
-    hip_check(hipMemcpyAsync(dev, h, ndesc * sizeof(PbsDesc), hipMemcpyHostToDevice, ctx_->stream), "desc copy");
-    hip_check(hipEventRecord(desc_ev_[desc_turn_], ctx_->stream), "desc event");
-    auto pbs = [&](size_t lo, size_t hi) {
-        if (hi <= lo) return;
-        hip_check(ctx_->keyswitch(nullptr, dev + lo, hi - lo), "keyswitch");
-        hip_check(ctx_->blind_rotate(dev + lo, nullptr, nullptr, hi - lo), "blind rotate");
-    };
-    const auto t0 = std::chrono::steady_clock::now();
-    if (!split) {
-        pbs(0, G);
-    } else {
-        // own slice (every slice when ranks are emulated on one GPU)
-        for (int r = 0; r < W; ++r)
-            if (!ctx_->comm || r == ctx_->rank) pbs(r * chunk, std::min(G, (r + 1) * chunk));
-        engine_check(ctx_->allgather(ctx_->d_gather, chunk * kBigCt) == FHE_OK, "all-gather");
-        hip_check(launch_scatter_blocks(ctx_->d_gather, reinterpret_cast<uint64_t* const*>(dev + G), (int)G,
-                                        ctx_->stream),
-                  "scatter");
-        fanout_levels += 1;
-    }
-    pbs_count += G;
-    levels += 1;
-    if (trace_) {
-        sync();
-        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        fprintf(stderr, "[level %llu] %zu PBS %.3f ms\n", (unsigned long long)levels, G, ms);
+    if (pending_.size() >= (size_t)1 << 20) flush();  // bound the deferred graph (host memory)
+    // the first large batch with nothing pending before it (e.g. a wide multiplication's block
+    // products) is one throughput level under any schedule: launch it now, so the GPU works while
+    // the host builds the rest of the graph (once per explicit flush: later independent batches,
+    // e.g. the compressions that follow, stay in the graph to be spread over idle capacity)
+    if (eager_ok_ && pending_.size() >= kEagerBatch && pending_.front().deps.empty() && pending_.back().deps.empty()) {
+        bool independent = true;
+        for (const Pending& n : pending_)
+            if (!n.deps.empty()) {
+                independent = false;
+                break;
+            }
+        if (independent) {
+            flush();
+            eager_ok_ = false;
+        }
     }
     return out;
 }
 
+void Engine::flush() {
+    const size_t N = pending_.size();
+    if (N == 0) return;
+    const auto f0 = std::chrono::steady_clock::now();
+    // ASAP depth, critical path, ALAP deadlines
+    std::vector<int32_t> asap(N, 1), alap(N), ndeps(N, 0);
+    std::vector<std::vector<int32_t>> users(N);
+    int32_t L = 0;
+    for (size_t i = 0; i < N; ++i) {
+        for (int32_t d : pending_[i].deps) {
+            asap[i] = std::max(asap[i], asap[d] + 1);
+            users[d].push_back((int32_t)i);
+        }
+        ndeps[i] = (int32_t)pending_[i].deps.size();
+        L = std::max(L, asap[i]);
+    }
+    for (size_t k = N; k-- > 0;) {
+        alap[k] = L;
+        for (int32_t u : users[k]) alap[k] = std::min(alap[k], alap[u] - 1);
+    }
+    constexpr size_t kRound = 256;
+    using Key = std::pair<int32_t, int32_t>;
+    std::vector<std::vector<int32_t>> lv;
+    if (sched_ == 0) {
+        // backward list scheduling from the last level: a level takes every candidate (all users
+        // placed later) that cannot go any earlier (asap == t), then fills up to a whole round with
+        // the least flexible other candidates; what does not fit lands at its earliest level, where
+        // the unabsorbed throughput work forms large batches
+        std::vector<int32_t> nusers(N);
+        std::priority_queue<Key> cand;  // (asap, node), largest asap first
+        for (size_t i = 0; i < N; ++i) {
+            nusers[i] = (int32_t)users[i].size();
+            if (!nusers[i]) cand.push({asap[i], (int32_t)i});
+        }
+        for (int32_t t = L; t >= 1; --t) {
+            std::vector<int32_t> cur;
+            while (!cand.empty() && cand.top().first >= t) {
+                cur.push_back(cand.top().second);
+                cand.pop();
+            }
+            const size_t cap = std::max<size_t>(1, (cur.size() + kRound - 1) / kRound) * kRound;
+            while (!cand.empty() && cur.size() < cap) {
+                cur.push_back(cand.top().second);
+                cand.pop();
+            }
+            for (int32_t i : cur)
+                for (int32_t d : pending_[i].deps)
+                    if (--nusers[d] == 0) cand.push({asap[d], d});
+            lv.push_back(std::move(cur));
+        }
+        engine_check(cand.empty(), "scheduler left nodes unplaced");
+        std::reverse(lv.begin(), lv.end());
+    } else {
+        // forward list scheduling: deadline nodes always, then the most urgent ready ones up to a
+        // whole round
+        std::priority_queue<Key, std::vector<Key>, std::greater<Key>> ready;  // (deadline, node)
+        for (size_t i = 0; i < N; ++i)
+            if (!ndeps[i]) ready.push({alap[i], (int32_t)i});
+        for (int32_t t = 1; !ready.empty(); ++t) {
+            std::vector<int32_t> cur;
+            while (!ready.empty() && ready.top().first <= t) {
+                cur.push_back(ready.top().second);
+                ready.pop();
+            }
+            const size_t cap = std::max<size_t>(1, (cur.size() + kRound - 1) / kRound) * kRound;
+            while (!ready.empty() && cur.size() < cap) {
+                cur.push_back(ready.top().second);
+                ready.pop();
+            }
+            for (int32_t i : cur)
+                for (int32_t u : users[i])
+                    if (--ndeps[u] == 0) ready.push({alap[u], u});
+            lv.push_back(std::move(cur));
+        }
+    }
+    // one staging copy of every level's descriptors (+ fanned-out levels' destination tables)
+    const int W = ctx_->fanout_world();
+    size_t ndesc = 0, maxchunk = 0, maxgather = 0;
+    for (auto& l : lv) {
+        const size_t G = l.size();
+        const bool split = W > 1 && G >= ctx_->fanout_min;
+        const size_t chunk = split ? (G + W - 1) / W : G;
+        ndesc += G + (split ? (G * sizeof(uint64_t*) + sizeof(PbsDesc) - 1) / sizeof(PbsDesc) : 0);
+        maxchunk = std::max(maxchunk, chunk);
+        if (split) maxgather = std::max(maxgather, chunk * W);
+    }
+    if (maxgather) engine_check(ctx_->ensure_gather(maxgather) == FHE_OK, "gather workspace");
+    engine_check(ctx_->ensure_ms(maxchunk) == FHE_OK, "workspace");
+    engine_check(ctx_->sync_luts() == FHE_OK, "LUT upload");
+    PbsDesc* dev = nullptr;
+    PbsDesc* h = stage_desc(ndesc, &dev);
+    std::vector<size_t> at(lv.size());
+    size_t o = 0;
+    for (size_t li = 0; li < lv.size(); ++li) {
+        const size_t G = lv[li].size();
+        const bool split = W > 1 && G >= ctx_->fanout_min;
+        at[li] = o;
+        uint64_t** h_scat = reinterpret_cast<uint64_t**>(h + o + G);
+        for (size_t g = 0; g < G; ++g) {
+            PbsDesc d = pending_[lv[li][g]].d;
+            if (split) {
+                // fanned-out levels bootstrap into the gather buffer (segment = owning rank), then scatter
+                h_scat[g] = d.dst;
+                d.dst = ctx_->d_gather + g * kBigCt;
+            }
+            h[o + g] = d;
+        }
+        o += G + (split ? (G * sizeof(uint64_t*) + sizeof(PbsDesc) - 1) / sizeof(PbsDesc) : 0);
+    }
+    hip_check(hipMemcpyAsync(dev, h, ndesc * sizeof(PbsDesc), hipMemcpyHostToDevice, ctx_->stream), "desc copy");
+    hip_check(hipEventRecord(desc_ev_[desc_turn_], ctx_->stream), "desc event");
+    if (trace_)
+        fprintf(stderr, "[flush] %zu nodes, %zu levels, scheduled in %.3f ms\n", N, lv.size(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count());
+    for (size_t li = 0; li < lv.size(); ++li) {
+        const size_t G = lv[li].size();
+        const bool split = W > 1 && G >= ctx_->fanout_min;
+        const size_t chunk = split ? (G + W - 1) / W : G;
+        PbsDesc* ld = dev + at[li];
+        auto pbs = [&](size_t lo, size_t hi) {
+            if (hi <= lo) return;
+            hip_check(ctx_->keyswitch(nullptr, ld + lo, hi - lo), "keyswitch");
+            hip_check(ctx_->blind_rotate(ld + lo, nullptr, nullptr, hi - lo), "blind rotate");
+        };
+        const auto t0 = std::chrono::steady_clock::now();
+        if (!split) {
+            pbs(0, G);
+        } else {
+            // own slice (every slice when ranks are emulated on one GPU)
+            for (int r = 0; r < W; ++r)
+                if (!ctx_->comm || r == ctx_->rank) pbs(r * chunk, std::min(G, (r + 1) * chunk));
+            engine_check(ctx_->allgather(ctx_->d_gather, chunk * kBigCt) == FHE_OK, "all-gather");
+            hip_check(launch_scatter_blocks(ctx_->d_gather, reinterpret_cast<uint64_t* const*>(ld + G), (int)G,
+                                            ctx_->stream),
+                      "scatter");
+            fanout_levels += 1;
+        }
+        pbs_count += G;
+        levels += 1;
+        if (trace_) {
+            hip_check(hipStreamSynchronize(ctx_->stream), "trace sync");
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            fprintf(stderr, "[level %llu] %zu PBS %.3f ms\n", (unsigned long long)levels, G, ms);
+        }
+    }
+    for (auto& n : pending_) n.hold[0]->node = -1;
+    pending_.clear();  // the stream orders any later reuse of the held slots behind these launches
+    eager_ok_ = true;
+}
+
 Block Engine::lincomb(const std::vector<Term>& terms, uint32_t cst) {
     for (const Term& t : terms) engine_check(!t.b.lazy(), "lincomb of a lazy block");
+    flush();
     int64_t c = cst;
     uint32_t noise = 0;
     std::vector<Term> live;
@@ -314,11 +448,15 @@ Block Engine::upload(const uint64_t* ct, uint32_t degree) {
 
 void Engine::download(const Block& b, uint64_t* ct) {
     engine_check(!b.trivial() && !b.lazy(), "download of a trivial or lazy block");
+    flush();
     hip_check(hipMemcpyAsync(ct, b.slot->p, kBigCt * 8, hipMemcpyDeviceToHost, ctx_->stream), "download");
     hip_check(hipStreamSynchronize(ctx_->stream), "download sync");
 }
 
-void Engine::sync() { hip_check(hipStreamSynchronize(ctx_->stream), "sync"); }
+void Engine::sync() {
+    flush();
+    hip_check(hipStreamSynchronize(ctx_->stream), "sync");
+}
 
 Block block_lazy(const std::vector<Term>& terms, int32_t cst, uint32_t degree) {
     auto lin = std::make_shared<std::vector<Term>>();

@@ -31,6 +31,7 @@ class BlockPool;
 struct Slot {
     uint64_t* p = nullptr;
     std::shared_ptr<BlockPool> pool;
+    int64_t node = -1;  // index of the pending bootstrap that writes this slot (Engine::flush), or -1
     ~Slot();
 };
 
@@ -88,14 +89,25 @@ struct PbsItem {
     std::vector<uint32_t> table;  // LUT over [0, msg*carry)
 };
 
-// Executes dependency levels of PBS items on a context.
+// Executes PBS items on a context as a deferred dependency graph.  run() does the host-side
+// bookkeeping at once (trivial folding, degrees, noise, output slots) and records each remaining
+// bootstrap as a pending node that depends on the pending producers of its inputs; flush() (called
+// before any host read: sync, download, lincomb) schedules all pending nodes into launch levels
+// and runs them.  Scheduling: as-late-as-possible deadlines from the critical path, each level
+// takes every node at its deadline and fills up to the next whole round of the latency kernel (a
+// multiple of 256) with the most urgent ready nodes -- work off the critical path (e.g. the
+// products a later window add needs) rides in the idle CUs of latency-bound levels.  The level
+// count equals the critical path.
 class Engine {
 public:
     explicit Engine(fhe_ctx* ctx);
     ~Engine();
     fhe_ctx* ctx() const { return ctx_; }
-    // Runs one level; returns one output block per item (possibly trivial).  Throws on error.
+    // Records one dependency level of items; returns one output block per item (possibly trivial).
+    // Throws on error.
     Blocks run(std::vector<PbsItem>& items);
+    // Schedules and launches every pending bootstrap (asynchronously on the context's stream).
+    void flush();
     // Linear combination without bootstrap (caller guarantees degree/noise stay legal).
     Block lincomb(const std::vector<Term>& terms, uint32_t cst);
     // Upload client-encrypted blocks.
@@ -109,6 +121,15 @@ private:
     fhe_ctx* ctx_;
     std::shared_ptr<BlockPool> pool_;
     bool trace_ = false;
+    int sched_ = 0;
+    static constexpr size_t kEagerBatch = 4096;
+    bool eager_ok_ = true;
+    struct Pending {
+        PbsDesc d;
+        std::vector<std::shared_ptr<Slot>> hold;  // [0] output, then inputs: alive until launched
+        std::vector<int32_t> deps;                // pending producers of the inputs
+    };
+    std::vector<Pending> pending_;
     PbsDesc* h_desc_[2] = {nullptr, nullptr};  // pinned, double-buffered
     hipEvent_t desc_ev_[2] = {nullptr, nullptr};
     size_t desc_cap_ = 0;

@@ -24,5 +24,6 @@ for op in ops:
         Schnorr().sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT)
     elif op == "div_enc":
         FheUint64.try_encrypt(a % 2**64, ck).div_rem(FheUint64.try_encrypt(b % 2**40, ck))
+    print(f"== {op} host graph built {time.perf_counter() - t0:.4f} s", file=sys.stderr, flush=True)
     ctx.sync()
     print(f"== {op} total {time.perf_counter() - t0:.4f} s", file=sys.stderr, flush=True)
