@@ -354,6 +354,24 @@ int fhe_radix_cast(fhe_ctx* c, const fhe_radix* a, uint32_t bits, fhe_radix** ou
     (void)c;
     return FHE_OK;
 }
+int fhe_schedule_levels(const int32_t* off, const int32_t* deps, size_t n, int mode, int32_t* level_of,
+                        int32_t* nlevels) {
+    if ((n && (!off || !level_of)) || !nlevels || (mode != 0 && mode != 1)) return FHE_ERR_INVALID;
+    return guarded([&] {
+        std::vector<std::vector<int32_t>> g(n);
+        for (size_t i = 0; i < n; ++i)
+            for (int32_t k = off[i]; k < off[i + 1]; ++k) {
+                engine_check(deps && deps[k] >= 0 && (size_t)deps[k] < i, "dependency must name an earlier node");
+                g[i].push_back(deps[k]);
+            }
+        std::vector<std::vector<int32_t>> lv = schedule_levels(g, mode);
+        for (size_t l = 0; l < lv.size(); ++l)
+            for (int32_t i : lv[l]) level_of[i] = (int32_t)l + 1;
+        *nlevels = (int32_t)lv.size();
+        return FHE_OK;
+    });
+}
+
 int fhe_ctx_stats(fhe_ctx* c, uint64_t* pbs, uint64_t* levels) {
     if (!c) return FHE_ERR_INVALID;
     if (pbs) *pbs = c->engine ? c->engine->pbs_count : 0;

@@ -245,20 +245,23 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     return out;
 }
 
-void Engine::flush() {
-    const size_t N = pending_.size();
-    if (N == 0) return;
-    const auto f0 = std::chrono::steady_clock::now();
+// Level schedule of a dependency graph (deps[i]: earlier nodes node i reads).  Returns the nodes of
+// each launch level, in order; the level count is the critical path.  mode 0: backward list
+// scheduling (default), 1: forward deadline-driven.  See Engine (radix.h).
+std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<int32_t>>& deps, int mode) {
+    const size_t N = deps.size();
+    std::vector<std::vector<int32_t>> lv;
+    if (N == 0) return lv;
     // ASAP depth, critical path, ALAP deadlines
     std::vector<int32_t> asap(N, 1), alap(N), ndeps(N, 0);
     std::vector<std::vector<int32_t>> users(N);
     int32_t L = 0;
     for (size_t i = 0; i < N; ++i) {
-        for (int32_t d : pending_[i].deps) {
+        for (int32_t d : deps[i]) {
             asap[i] = std::max(asap[i], asap[d] + 1);
             users[d].push_back((int32_t)i);
         }
-        ndeps[i] = (int32_t)pending_[i].deps.size();
+        ndeps[i] = (int32_t)deps[i].size();
         L = std::max(L, asap[i]);
     }
     for (size_t k = N; k-- > 0;) {
@@ -267,8 +270,7 @@ void Engine::flush() {
     }
     constexpr size_t kRound = 256;
     using Key = std::pair<int32_t, int32_t>;
-    std::vector<std::vector<int32_t>> lv;
-    if (sched_ == 0) {
+    if (mode == 0) {
         // backward list scheduling from the last level: a level takes every candidate (all users
         // placed later) that cannot go any earlier (asap == t), then fills up to a whole round with
         // the least flexible other candidates; what does not fit lands at its earliest level, where
@@ -291,7 +293,7 @@ void Engine::flush() {
                 cand.pop();
             }
             for (int32_t i : cur)
-                for (int32_t d : pending_[i].deps)
+                for (int32_t d : deps[i])
                     if (--nusers[d] == 0) cand.push({asap[d], d});
             lv.push_back(std::move(cur));
         }
@@ -320,6 +322,16 @@ void Engine::flush() {
             lv.push_back(std::move(cur));
         }
     }
+    return lv;
+}
+
+void Engine::flush() {
+    const size_t N = pending_.size();
+    if (N == 0) return;
+    const auto f0 = std::chrono::steady_clock::now();
+    std::vector<std::vector<int32_t>> deps(N);
+    for (size_t k = 0; k < N; ++k) deps[k] = pending_[k].deps;
+    std::vector<std::vector<int32_t>> lv = schedule_levels(deps, sched_);
     // one staging copy of every level's descriptors (+ fanned-out levels' destination tables)
     const int W = ctx_->fanout_world();
     size_t ndesc = 0, maxchunk = 0, maxgather = 0;

@@ -217,6 +217,12 @@ int fhe_radix_shl(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* amount, fhe
 int fhe_radix_bitand(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
 /* engine statistics since context creation: bootstraps executed and dependency levels */
 int fhe_ctx_stats(fhe_ctx* ctx, uint64_t* pbs_count, uint64_t* levels);
+/* The engine's level scheduler on an explicit dependency graph (host only, no GPU): node i reads
+ * nodes deps[dep_offsets[i] .. dep_offsets[i+1]) (all < i).  Writes each node's launch level
+ * (1-based) to level_of[i] and the level count (= the critical path) to *nlevels.  mode 0: backward
+ * list scheduling (the engine's default), 1: forward deadline-driven (FHE_SCHED=1). */
+int fhe_schedule_levels(const int32_t* dep_offsets, const int32_t* deps, size_t n, int mode, int32_t* level_of,
+                        int32_t* nlevels);
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */

@@ -1,0 +1,92 @@
+"""The radix engine's level scheduler (csrc/radix.cpp:schedule_levels, C ABI fhe_schedule_levels),
+host logic only: on random dependency graphs and on the shape of a compat window-add chain, every
+node runs after its inputs, the level count is the critical path, levels are filled to whole
+latency-kernel rounds (256) only with work that could run there, and the backward schedule keeps
+the throughput work off the chain levels' critical capacity."""
+import ctypes as C
+import random
+
+import numpy as np
+import pytest
+
+from fhe_sign import _lib
+
+
+def schedule(deps, mode=0):
+    n = len(deps)
+    off = np.zeros(n + 1, np.int32)
+    for i, d in enumerate(deps):
+        off[i + 1] = off[i] + len(d)
+    flat = np.array([x for d in deps for x in d] or [0], np.int32)
+    level = np.zeros(max(n, 1), np.int32)
+    nl = C.c_int32()
+    P = C.POINTER(C.c_int32)
+    rc = _lib.load().fhe_schedule_levels(off.ctypes.data_as(P), flat.ctypes.data_as(P), n, mode,
+                                         level.ctypes.data_as(P), C.byref(nl))
+    assert rc == 0, _lib.load().fhe_last_error()
+    return level[:n].tolist(), nl.value
+
+
+def critical_path(deps):
+    d = []
+    for i, ds in enumerate(deps):
+        d.append(1 + max((d[j] for j in ds), default=0))
+    return max(d, default=0)
+
+
+def check(deps, level, nl):
+    assert nl == critical_path(deps)
+    for i, ds in enumerate(deps):
+        assert 1 <= level[i] <= nl
+        for j in ds:
+            assert level[j] < level[i], (i, j)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_random_graphs(mode):
+    rng = random.Random(7 + mode)
+    for trial in range(30):
+        n = rng.randrange(1, 3000)
+        deps = []
+        for i in range(n):
+            k = rng.choice([0, 0, 1, 2, 3, 6]) if i else 0
+            deps.append(sorted(set(rng.randrange(0, i) for _ in range(min(k, i)))))
+        level, nl = schedule(deps, mode)
+        check(deps, level, nl)
+
+
+def test_chain_with_background_work():
+    """A 100-level chain of 64-node steps beside 20000 independent two-stage jobs each needed by
+    one chain step: the level count stays the chain's, the chain levels are filled to one round
+    (256), and what does not fit runs early in large levels (backward schedule)."""
+    deps, prev = [], []
+    jobs = []
+    for j in range(20000):  # stage 1, then stage 2 reading it
+        deps.append([])
+        deps.append([len(deps) - 1])
+        jobs.append(len(deps) - 1)
+    for step in range(100):
+        cur = []
+        for k in range(64):
+            d = list(prev[max(0, k - 2):k + 1]) + [jobs[(step * 200 + k) % len(jobs)]]
+            deps.append(sorted(set(d)))
+            cur.append(len(deps) - 1)
+        prev = cur
+    level, nl = schedule(deps, 0)
+    check(deps, level, nl)
+    sizes = np.bincount(level, minlength=nl + 1)[1:]
+    assert nl == 102
+    assert (sizes[5:] <= 256).all() and (sizes[5:] >= 200).sum() > 80  # chain levels filled to a round
+    assert sizes[:2].sum() > 20000  # the rest as large early batches
+    lf, nf = schedule(deps, 1)
+    check(deps, lf, nf)
+
+
+def test_invalid_graph_rejected():
+    off = np.array([0, 1], np.int32)
+    bad = np.array([0], np.int32)  # node 0 reading itself
+    level = np.zeros(1, np.int32)
+    nl = C.c_int32()
+    P = C.POINTER(C.c_int32)
+    assert _lib.load().fhe_schedule_levels(off.ctypes.data_as(P), bad.ctypes.data_as(P), 1, 0,
+                                           level.ctypes.data_as(P), C.byref(nl)) != 0
