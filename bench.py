@@ -157,6 +157,19 @@ def ops_legs(ck, ctx, seed):
     leg("sign_fhe_with_k0_v0_compat", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT), lambda r: r == ref)
     leg("sign_fhe_with_k0_v0_fast", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, FAST), lambda r: r == ref)
     leg("sign_fhe_with_k0_v0_public", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, PUBLIC), lambda r: r == ref)
+    # config 5b's batch on one GPU: 8 signatures (BIP-340 vectors 0, 1, 2, 15, 16, 17, 18, 0; SURVEY
+    # 8d) as ONE engine schedule; signs/s = 8 / seconds
+    import csv
+    rows = {r["index"]: r for r in csv.DictReader(open(os.path.join(ROOT, "tests", "golden", "bip340_vectors.csv")))}
+    jobs, want = [], []
+    for idx in ("0", "1", "2", "15", "16", "17", "18", "0"):
+        dd = int(rows[idx]["secret key"], 16)
+        mm, aux = bytes.fromhex(rows[idx]["message"]), bytes.fromhex(rows[idx]["aux_rand"])
+        kk = compute_nonce(dd, mm, aux)
+        jobs.append((mm, kk, dd, BigUintFHE.new(dd, ck)))
+        want.append(s.sign_with_k0(mm, kk, dd))
+    leg("sign_fhe_with_k0_batch8_compat", lambda: s.sign_fhe_with_k0_batch(jobs, ck, COMPAT), lambda r: r == want)
+    out["sign_fhe_with_k0_batch8_compat"]["signs_per_s"] = 8 / out["sign_fhe_with_k0_batch8_compat"]["seconds"]
     return out
 
 
@@ -287,6 +300,9 @@ def main():
     if ops is not None and dist is not None:
         for k in ops:
             ops[k]["seconds"] = allmax(dist, ops[k]["seconds"])
+        # every rank signs its own batch of 8 (config 5b): whole-job signatures per second
+        b8 = ops["sign_fhe_with_k0_batch8_compat"]
+        b8["signs_per_s"] = world * 8 / b8["seconds"]
     fan = fanout_legs(ck, ctx, dist, rank, world, a.seed) if (world > 1 and not a.no_ops) else None
 
     total = world * B * a.steps

@@ -377,56 +377,80 @@ int fhe_schnorr_sign(const uint8_t* msg, size_t len, const uint8_t aux[32], cons
     return fhe_schnorr_sign_with_k0(msg, len, k0, privkey, sig);
 }
 
-// Schnorr::sign_fhe_with_k0 (src/schnorr.rs:235-290)
-int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t len, const uint8_t k0[32],
-                                 const uint8_t privkey[32], const fhe_biguint* privkey_fhe, int mode, uint8_t sig[64]) {
-    if (!ctx || !ck || (len && !msg) || !k0 || !privkey || !privkey_fhe || !sig) return FHE_ERR_INVALID;
-    SignCore c = core(msg, len, U256::from_be(k0), U256::from_be(privkey));
-    std::vector<uint32_t> limbs;
+}  // extern "C"
+
+namespace {
+// One signature in flight: the plaintext prologue and the (not yet launched) FHE block.  Phase 1
+// (sign_begin) records the FHE block in the engine's deferred graph; phase 2 (sign_end) decrypts,
+// which flushes the graph -- so a batch of signatures begun together runs as ONE schedule whose
+// levels hold every signature's bootstraps.
+struct SignJob {
+    SignCore c;
+    fhe_biguint *e_fhe = nullptr, *k_fhe = nullptr, *s_fhe = nullptr;
+    fhe_radix* s_rad = nullptr;
+    uint32_t bits = 0;
+    ~SignJob() {
+        fhe_biguint_destroy(e_fhe);
+        fhe_biguint_destroy(k_fhe);
+        fhe_biguint_destroy(s_fhe);
+        fhe_radix_destroy(s_rad);
+    }
+};
+
+// plaintext prologue and the client-side encryptions (uploads) of e and k
+int sign_prepare(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t len, const uint8_t k0[32],
+                 const uint8_t privkey[32], const fhe_biguint* privkey_fhe, int mode, SignJob* j) {
+    if (!ctx || !ck || (len && !msg) || !k0 || !privkey || !privkey_fhe) return FHE_ERR_INVALID;
+    j->c = core(msg, len, U256::from_be(k0), U256::from_be(privkey));
+    if (mode == FHE_SIGN_PUBLIC_OPERANDS) return FHE_OK;
+    std::vector<uint32_t> el = u32_digits(j->c.e), kl = u32_digits(j->c.k);
+    int rc = fhe_biguint_encrypt(ctx, ck, el.data(), el.size(), &j->e_fhe);
+    if (!rc) rc = fhe_biguint_encrypt(ctx, ck, kl.data(), kl.size(), &j->k_fhe);
+    return rc;
+}
+
+// the FHE block, recorded in the engine's deferred graph
+int sign_begin(fhe_ctx* ctx, const fhe_biguint* privkey_fhe, int mode, SignJob* j) {
+    const SignCore& c = j->c;
     int rc = FHE_OK;
     if (mode == FHE_SIGN_PUBLIC_OPERANDS) {
         // s = e * Enc(d') + k with e, k clear: one radix wide enough for the exact value
         // (d' < 2^(32 L), e, k < 2^256  =>  s < 2^(32 L + 257))
         size_t L = 0;
         fhe_biguint_len(privkey_fhe, &L);
-        const uint32_t kBits = (uint32_t)(32 * L + 258);
-        if (kBits > FHE_RADIX_MAX_BITS) return FHE_ERR_INVALID;
-        fhe_radix *d = nullptr, *sr = nullptr;
+        j->bits = (uint32_t)(32 * L + 258);
+        if (j->bits > FHE_RADIX_MAX_BITS) return FHE_ERR_INVALID;
+        fhe_radix* d = nullptr;
         uint64_t ew[4], kw[4];
         for (int i = 0; i < 4; ++i) {
             ew[i] = c.e.w[i];
             kw[i] = c.k.w[i];
         }
-        rc = fhe_biguint_to_radix(privkey_fhe, kBits, &d);
-        if (!rc) rc = fhe_radix_scalar_mul_add_words(ctx, d, ew, 4, kw, 4, &sr);
-        if (!rc) {
-            std::vector<uint64_t> w((kBits + 63) / 64);
-            rc = fhe_radix_decrypt(ctx, ck, sr, w.data(), w.size());
-            for (uint32_t i = 0; i < kBits / 32 + 1 && !rc; ++i) limbs.push_back((uint32_t)(w[i / 2] >> (32 * (i % 2))));
-        }
+        rc = fhe_biguint_to_radix(privkey_fhe, j->bits, &d);
+        if (!rc) rc = fhe_radix_scalar_mul_add_words(ctx, d, ew, 4, kw, 4, &j->s_rad);
         fhe_radix_destroy(d);
-        fhe_radix_destroy(sr);
-        if (rc) return rc;
-    } else {
-        // FHE block (src/schnorr.rs:272-276)
-        std::vector<uint32_t> el = u32_digits(c.e), kl = u32_digits(c.k);
-        fhe_biguint *e_fhe = nullptr, *k_fhe = nullptr, *s_fhe = nullptr;
-        rc = fhe_biguint_encrypt(ctx, ck, el.data(), el.size(), &e_fhe);
-        if (!rc) rc = fhe_biguint_encrypt(ctx, ck, kl.data(), kl.size(), &k_fhe);
-        // k_fhe + e_fhe * privkey_fhe as one schedule (limbs identical to the mul, then the add)
-        if (!rc) rc = fhe_biguint_mul_add(ctx, e_fhe, privkey_fhe, k_fhe, mode, &s_fhe);
-        if (!rc) {
-            size_t n = 0;
-            fhe_biguint_len(s_fhe, &n);
-            limbs.resize(n + 1);
-            rc = fhe_biguint_decrypt(ctx, ck, s_fhe, limbs.data(), limbs.size(), &n);
-            limbs.resize(n);
-        }
-        fhe_biguint_destroy(e_fhe);
-        fhe_biguint_destroy(k_fhe);
-        fhe_biguint_destroy(s_fhe);
-        if (rc) return rc;
+        return rc;
     }
+    // FHE block (src/schnorr.rs:272-276): k_fhe + e_fhe * privkey_fhe as one schedule (limbs
+    // identical to the reference's mul, then add)
+    return fhe_biguint_mul_add(ctx, j->e_fhe, privkey_fhe, j->k_fhe, mode, &j->s_fhe);
+}
+
+int sign_end(fhe_ctx* ctx, fhe_client_key* ck, SignJob* j, uint8_t sig[64]) {
+    std::vector<uint32_t> limbs;
+    int rc = FHE_OK;
+    if (j->s_rad) {
+        std::vector<uint64_t> w((j->bits + 63) / 64);
+        rc = fhe_radix_decrypt(ctx, ck, j->s_rad, w.data(), w.size());
+        for (uint32_t i = 0; i < j->bits / 32 + 1 && !rc; ++i) limbs.push_back((uint32_t)(w[i / 2] >> (32 * (i % 2))));
+    } else {
+        size_t n = 0;
+        fhe_biguint_len(j->s_fhe, &n);
+        limbs.resize(n + 1);
+        rc = fhe_biguint_decrypt(ctx, ck, j->s_fhe, limbs.data(), limbs.size(), &n);
+        limbs.resize(n);
+    }
+    if (rc) return rc;
     // s = s_without_mod % n (to_biguint then %, src/schnorr.rs:275-276)
     std::vector<uint64_t> big((limbs.size() + 1) / 2 + 1, 0);
     for (size_t i = 0; i < limbs.size(); ++i) big[i / 2] |= (uint64_t)limbs[i] << (32 * (i % 2));
@@ -439,8 +463,43 @@ int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t
         for (int k = 0; k < 4; ++k) v[k + 1] = s.w[k];
         s = mod512(v, kN);
     }
-    c.r.x.to_be(sig);
+    j->c.r.x.to_be(sig);
     s.to_be(sig + 32);
+    return FHE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+// Schnorr::sign_fhe_with_k0 (src/schnorr.rs:235-290)
+int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t len, const uint8_t k0[32],
+                                 const uint8_t privkey[32], const fhe_biguint* privkey_fhe, int mode, uint8_t sig[64]) {
+    if (!sig) return FHE_ERR_INVALID;
+    SignJob j;
+    int rc = sign_prepare(ctx, ck, msg, len, k0, privkey, privkey_fhe, mode, &j);
+    if (!rc) rc = sign_begin(ctx, privkey_fhe, mode, &j);
+    return rc ? rc : sign_end(ctx, ck, &j, sig);
+}
+
+// A batch of independent sign_fhe_with_k0 calls run as one engine schedule (their bootstraps share
+// launch levels); signature i is byte-identical to the single call's.
+int fhe_schnorr_sign_fhe_with_k0_batch(fhe_ctx* ctx, fhe_client_key* ck, size_t count, const uint8_t* const* msgs,
+                                       const size_t* lens, const uint8_t* k0s, const uint8_t* privkeys,
+                                       const fhe_biguint* const* privkeys_fhe, int mode, uint8_t* sigs) {
+    if (count && (!msgs || !lens || !k0s || !privkeys || !privkeys_fhe || !sigs)) return FHE_ERR_INVALID;
+    std::vector<SignJob> jobs(count);
+    for (size_t i = 0; i < count; ++i) {  // uploads first: the engine graph is not started yet
+        int rc = sign_prepare(ctx, ck, msgs[i], lens[i], k0s + 32 * i, privkeys + 32 * i, privkeys_fhe[i], mode, &jobs[i]);
+        if (rc) return rc;
+    }
+    for (size_t i = 0; i < count; ++i) {
+        int rc = sign_begin(ctx, privkeys_fhe[i], mode, &jobs[i]);
+        if (rc) return rc;
+    }
+    for (size_t i = 0; i < count; ++i) {
+        int rc = sign_end(ctx, ck, &jobs[i], sigs + 64 * i);
+        if (rc) return rc;
+    }
     return FHE_OK;
 }
 

@@ -122,6 +122,9 @@ _SIGNATURES = [
     ("fhe_schnorr_sign_with_k0", C.c_int, [u8p, C.c_size_t, u8p, u8p, u8p]),
     ("fhe_schnorr_sign", C.c_int, [u8p, C.c_size_t, u8p, u8p, u8p]),
     ("fhe_schnorr_sign_fhe_with_k0", C.c_int, [C.c_void_p, C.c_void_p, u8p, C.c_size_t, u8p, u8p, C.c_void_p, C.c_int, u8p]),
+    ("fhe_schnorr_sign_fhe_with_k0_batch", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p),
+                                                    C.POINTER(C.c_size_t), C.c_char_p, C.c_char_p,
+                                                    C.POINTER(C.c_void_p), C.c_int, C.c_char_p]),
     ("fhe_schnorr_sign_fhe", C.c_int, [C.c_void_p, C.c_void_p, u8p, C.c_size_t, u8p, u8p, C.c_int, u8p]),
     ("fhe_schnorr_verify", C.c_int, [u8p, C.c_size_t, u8p, C.c_size_t, u8p, C.c_size_t]),
 ]

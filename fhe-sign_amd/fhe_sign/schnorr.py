@@ -48,6 +48,21 @@ class Schnorr:
                                                   _buf(_b32(k0)), _buf(_b32(privkey)), privkey_fhe.handle, mode, sig))
         return bytes(sig)
 
+    def sign_fhe_with_k0_batch(self, jobs, client_key, mode: int = COMPAT) -> list:
+        """jobs: [(message, k0, privkey, privkey_fhe)]; one engine schedule for all, signatures
+        identical to sign_fhe_with_k0 one by one"""
+        n = len(jobs)
+        bufs = [C.create_string_buffer(bytes(m), max(1, len(m))) for m, _, _, _ in jobs]
+        msgs = (C.c_void_p * max(1, n))(*[C.cast(b, C.c_void_p) for b in bufs])
+        lens = (C.c_size_t * max(1, n))(*[len(m) for m, _, _, _ in jobs])
+        k0s = b"".join(_b32(k) for _, k, _, _ in jobs)
+        pks = b"".join(_b32(d) for _, _, d, _ in jobs)
+        fh = (C.c_void_p * max(1, n))(*[f.handle for _, _, _, f in jobs])
+        sigs = C.create_string_buffer(64 * max(1, n))
+        check(load().fhe_schnorr_sign_fhe_with_k0_batch(_ctx().handle, client_key.handle, n, msgs, lens, k0s, pks, fh,
+                                                        mode, sigs))
+        return [sigs.raw[64 * i:64 * i + 64] for i in range(n)]
+
     def sign_fhe(self, message: bytes, aux_rand: bytes, privkey: int, client_key, mode: int = COMPAT) -> bytes:
         sig = (C.c_uint8 * 64)()
         check(load().fhe_schnorr_sign_fhe(_ctx().handle, client_key.handle, _buf(message), len(message),

@@ -278,6 +278,12 @@ int fhe_schnorr_sign(const uint8_t* msg, size_t msg_len, const uint8_t aux_rand[
 int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t msg_len,
                                  const uint8_t k0[32], const uint8_t privkey[32],
                                  const fhe_biguint* privkey_fhe, int mode, uint8_t sig[64]);
+/* count independent sign_fhe_with_k0 calls as ONE engine schedule (their bootstraps share launch
+ * levels: a batch of signatures costs far less than count single calls on one GPU).  msgs[i] /
+ * lens[i]; k0s, privkeys: count x 32 bytes; sigs: count x 64 bytes, each identical to the single call */
+int fhe_schnorr_sign_fhe_with_k0_batch(fhe_ctx* ctx, fhe_client_key* ck, size_t count, const uint8_t* const* msgs,
+                                       const size_t* lens, const uint8_t* k0s, const uint8_t* privkeys,
+                                       const fhe_biguint* const* privkeys_fhe, int mode, uint8_t* sigs);
 /* Schnorr::sign_fhe (src/schnorr.rs:154-211) */
 int fhe_schnorr_sign_fhe(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t msg_len,
                          const uint8_t aux_rand[32], const uint8_t privkey[32], int mode, uint8_t sig[64]);

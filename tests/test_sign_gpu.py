@@ -70,3 +70,24 @@ def test_biguint_to_radix(env):
     x = BigUintFHE.new(v, env)
     assert x.to_radix(300).decrypt(env) == v
     assert x.to_radix(64).decrypt(env) == v & (2**64 - 1)
+
+
+@pytest.mark.parametrize("mode", [COMPAT, PUBLIC])
+def test_sign_fhe_with_k0_batch(env, mode):
+    """config 5b on one GPU: several independent signatures as ONE engine schedule
+    (fhe_schnorr_sign_fhe_with_k0_batch) -- each byte-identical to sign_with_k0 (and to the CSV
+    where the reference's F8 deviation does not apply); 1-limb and 8-limb private keys mixed."""
+    ck = env
+    s = Schnorr()
+    jobs, want = [], []
+    for idx in ("0", "1", "2", "15", "3"):
+        row = ROWS[idx]
+        d = int(row["secret key"], 16)
+        msg, aux = bytes.fromhex(row["message"]), bytes.fromhex(row["aux_rand"])
+        k0 = compute_nonce(d, msg, aux)
+        jobs.append((msg, k0, d, BigUintFHE.new(d, ck)))
+        want.append(s.sign_with_k0(msg, k0, d))
+    got = s.sign_fhe_with_k0_batch(jobs, ck, mode)
+    assert got == want
+    for idx, sig in zip(("0", "1", "2", "15"), got):
+        assert sig.hex().upper() == ROWS[idx]["signature"].upper()

@@ -22,6 +22,16 @@ for op in ops:
     elif op == "sign":
         d = 3; msg = bytes(32); k0 = compute_nonce(d, msg, bytes(32)); dF = BigUintFHE.new(d, ck)
         Schnorr().sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT)
+    elif op == "sign_batch8":
+        import csv
+        rows = {r["index"]: r for r in csv.DictReader(open(os.path.join(ROOT, "tests", "golden", "bip340_vectors.csv")))}
+        jobs = []
+        for idx in ("0", "1", "2", "15", "16", "17", "18", "0"):
+            dd = int(rows[idx]["secret key"], 16)
+            mm, aux = bytes.fromhex(rows[idx]["message"]), bytes.fromhex(rows[idx]["aux_rand"])
+            jobs.append((mm, compute_nonce(dd, mm, aux), dd, BigUintFHE.new(dd, ck)))
+        t0 = time.perf_counter()
+        Schnorr().sign_fhe_with_k0_batch(jobs, ck, COMPAT)
     elif op == "div_enc":
         FheUint64.try_encrypt(a % 2**64, ck).div_rem(FheUint64.try_encrypt(b % 2**40, ck))
     print(f"== {op} host graph built {time.perf_counter() - t0:.4f} s", file=sys.stderr, flush=True)
