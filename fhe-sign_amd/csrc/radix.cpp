@@ -247,8 +247,10 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
 
 // Level schedule of a dependency graph (deps[i]: earlier nodes node i reads).  Returns the nodes of
 // each launch level, in order; the level count is the critical path.  mode 0: backward list
-// scheduling (default), 1: forward deadline-driven.  See Engine (radix.h).
-std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<int32_t>>& deps, int mode) {
+// scheduling (default), 1: forward deadline-driven; levels are filled to multiples of `round`
+// (one latency-kernel round: 256 bootstraps per GPU).  See Engine (radix.h).
+std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<int32_t>>& deps, int mode,
+                                                  size_t round) {
     const size_t N = deps.size();
     std::vector<std::vector<int32_t>> lv;
     if (N == 0) return lv;
@@ -268,7 +270,7 @@ std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<
         alap[k] = L;
         for (int32_t u : users[k]) alap[k] = std::min(alap[k], alap[u] - 1);
     }
-    constexpr size_t kRound = 256;
+    const size_t kRound = std::max<size_t>(1, round);
     using Key = std::pair<int32_t, int32_t>;
     if (mode == 0) {
         // backward list scheduling from the last level: a level takes every candidate (all users
@@ -331,7 +333,9 @@ void Engine::flush() {
     const auto f0 = std::chrono::steady_clock::now();
     std::vector<std::vector<int32_t>> deps(N);
     for (size_t k = 0; k < N; ++k) deps[k] = pending_[k].deps;
-    std::vector<std::vector<int32_t>> lv = schedule_levels(deps, sched_);
+    // a fanned-out level's round is one latency-kernel round on every rank
+    const size_t round = 256 * (size_t)std::max(1, ctx_->fanout_world());
+    std::vector<std::vector<int32_t>> lv = schedule_levels(deps, sched_, round);
     // one staging copy of every level's descriptors (+ fanned-out levels' destination tables)
     const int W = ctx_->fanout_world();
     size_t ndesc = 0, maxchunk = 0, maxgather = 0;

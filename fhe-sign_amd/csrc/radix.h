@@ -142,7 +142,8 @@ private:
 
 void engine_check(bool ok, const char* what);
 // The Engine's level scheduler (deps[i]: earlier nodes node i reads; mode 0 backward, 1 forward).
-std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<int32_t>>& deps, int mode);
+std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<int32_t>>& deps, int mode,
+                                                  size_t round = 256);
 
 // ----------------------------------------------------------------------------- radix ops
 // All take/return clean blocks (degree <= 3, noise <= 1) unless stated; widths in blocks.
