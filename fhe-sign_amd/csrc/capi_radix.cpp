@@ -103,12 +103,12 @@ int fhe_radix_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint64_t* words, uin
     }
     return guarded([&] {
         Radix r;
-        std::vector<uint64_t> ct(kBigCt);
+        std::vector<uint64_t> ct((size_t)(bits / 2) * kBigCt);
         for (uint32_t k = 0; k < bits / 2; ++k) {
             const uint32_t m = word_bits(words, 2 * k, bits);
-            encrypt_big(ck, (uint64_t)m * ck->params.delta(), ct.data());
-            r.blocks.push_back(c->engine->upload(ct.data(), 3));
+            encrypt_big(ck, (uint64_t)m * ck->params.delta(), ct.data() + (size_t)k * kBigCt);
         }
+        r.blocks = c->engine->upload_many(ct.data(), bits / 2, 3);
         *out = wrap(std::move(r), bits);
         return FHE_OK;
     });
@@ -386,13 +386,15 @@ int fhe_biguint_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint32_t* limbs, s
     if (!ck || !out || (n && !limbs)) return FHE_ERR_INVALID;
     return guarded([&] {
         auto* b = new fhe_biguint();
-        std::vector<uint64_t> ct(kBigCt);
+        std::vector<uint64_t> ct(n * kLimbBlocks * kBigCt);
+        for (size_t i = 0; i < n; ++i)
+            for (uint32_t k = 0; k < kLimbBlocks; ++k)
+                encrypt_big(ck, (uint64_t)((limbs[i] >> (2 * k)) & 3u) * ck->params.delta(),
+                            ct.data() + (i * kLimbBlocks + k) * kBigCt);
+        Blocks all = c->engine->upload_many(ct.data(), n * kLimbBlocks, 3);
         for (size_t i = 0; i < n; ++i) {
             Radix r;
-            for (uint32_t k = 0; k < kLimbBlocks; ++k) {
-                encrypt_big(ck, (uint64_t)((limbs[i] >> (2 * k)) & 3u) * ck->params.delta(), ct.data());
-                r.blocks.push_back(c->engine->upload(ct.data(), 3));
-            }
+            r.blocks.assign(all.begin() + i * kLimbBlocks, all.begin() + (i + 1) * kLimbBlocks);
             b->v.digits.push_back(std::move(r));
         }
         *out = b;

@@ -77,6 +77,7 @@ Engine::~Engine() {
     for (auto ev : desc_ev_)
         if (ev) (void)hipEventDestroy(ev);
     if (d_desc_) (void)hipFree(d_desc_);
+    if (d_up_) (void)hipFree(d_up_);
 }
 
 void Engine::ensure_desc(size_t n) {
@@ -460,6 +461,31 @@ Block Engine::upload(const uint64_t* ct, uint32_t degree) {
     hip_check(hipMemcpyAsync(b.slot->p, ct, kBigCt * 8, hipMemcpyHostToDevice, ctx_->stream), "upload");
     hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");
     return b;
+}
+
+Blocks Engine::upload_many(const uint64_t* cts, size_t n, uint32_t degree) {
+    Blocks out(n);
+    if (n == 0) return out;
+    const size_t words = n * kBigCt + n;  // ciphertexts, then the slot pointers
+    if (words > up_cap_) {
+        hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");
+        if (d_up_) hip_check(hipFree(d_up_), "hipFree");
+        hip_check(hipMalloc(&d_up_, words * 8), "hipMalloc upload");
+        up_cap_ = words;
+    }
+    std::vector<uint64_t*> dst(n);
+    for (size_t i = 0; i < n; ++i) {
+        out[i].slot = pool_->alloc();
+        out[i].degree = degree;
+        out[i].noise = 1;
+        dst[i] = out[i].slot->p;
+    }
+    uint64_t** d_dst = reinterpret_cast<uint64_t**>(d_up_ + n * kBigCt);
+    hip_check(hipMemcpyAsync(d_up_, cts, n * kBigCt * 8, hipMemcpyHostToDevice, ctx_->stream), "upload");
+    hip_check(hipMemcpyAsync(d_dst, dst.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice, ctx_->stream), "upload");
+    hip_check(launch_scatter_blocks(d_up_, d_dst, (int)n, ctx_->stream), "upload scatter");
+    hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");  // host buffers may go
+    return out;
 }
 
 void Engine::download(const Block& b, uint64_t* ct) {

@@ -112,6 +112,8 @@ public:
     Block lincomb(const std::vector<Term>& terms, uint32_t cst);
     // Upload client-encrypted blocks.
     Block upload(const uint64_t* ct, uint32_t degree);
+    // n client-encrypted blocks (contiguous big LWEs): one copy + one scatter into their slots
+    Blocks upload_many(const uint64_t* cts, size_t n, uint32_t degree);
     void download(const Block& b, uint64_t* ct);
     void sync();
     // statistics
@@ -120,6 +122,8 @@ public:
 private:
     fhe_ctx* ctx_;
     std::shared_ptr<BlockPool> pool_;
+    uint64_t* d_up_ = nullptr;  // upload staging: n big LWEs, then n destination pointers
+    size_t up_cap_ = 0;
     bool trace_ = false;
     int sched_ = 0;
     static constexpr size_t kEagerBatch = 4096;

@@ -187,3 +187,30 @@ def test_biguint_mul_add_equals_mul_then_add(keys):
     zero = BigUintFHE.new(0, ck)
     assert a.mul_add(zero, kk).decrypt_limbs(ck) == kl
     assert a.mul_add(b, zero, COMPAT).decrypt_limbs(ck) == R.biguint_mul(q["a"], q["b"])
+
+
+def test_deferred_graph_lifetimes_and_raw_pbs(keys):
+    """The engine defers bootstraps until a host read (csrc/radix.h Engine): operands and results
+    dropped before that read keep what the pending graph still needs, raw fhe_pbs_batch calls in
+    between (same stream, same workspace) neither see nor disturb pending work, and a graph built
+    over several calls runs as one schedule with every value right."""
+    import numpy as np
+    ck, ctx = keys
+    rng = random.Random(0xDEF)
+    xs = [rng.getrandbits(32) for _ in range(6)]
+    a = [FheUint32.try_encrypt(x, ck) for x in xs]
+    s01 = a[0] + a[1]
+    p23 = a[2] * a[3]
+    dropped = a[4] * a[5]  # never read
+    del dropped
+    del a[4:]
+    q = (s01 * p23) + a[0]
+    del a[1:]  # operands of pending bootstraps
+    inc = ctx.lut([(m + 1) % 16 for m in range(16)])
+    cts = np.stack([ck.encrypt_block(m) for m in range(8)])
+    raw = ctx.pbs(cts, inc)  # raw path while the radix graph is still pending
+    assert [ck.decrypt_block(c) for c in raw] == [(m + 1) % 16 for m in range(8)]
+    m = 2**32
+    assert q.decrypt(ck) == (((xs[0] + xs[1]) % m) * ((xs[2] * xs[3]) % m) + xs[0]) % m
+    assert s01.decrypt(ck) == (xs[0] + xs[1]) % m
+    assert p23.decrypt(ck) == (xs[2] * xs[3]) % m
