@@ -130,6 +130,7 @@ def ops_legs(ck, ctx, seed):
         out[name] = {"seconds": dt, "pbs": p1 - p0, "levels": l1 - l0}
 
     A.add(B, FAST)  # warm-up (LUT registration, pools)
+    A.mul(B, COMPAT).decrypt_limbs(ck)  # grows the block pool / staging buffers to their steady-state size
     import ref_semantics as R
     leg("biguint256_mul_compat", lambda: A.mul(B, COMPAT),
         lambda r: r.decrypt_limbs(ck) == R.biguint_mul(R.to_u32_digits(a), R.to_u32_digits(b)))

@@ -1090,8 +1090,12 @@ Radix radix_sum(Engine& e, const std::vector<const Radix*>& xs, uint32_t nblocks
 }
 
 // ============================================================================ multiplication
+// Block-pair products of a * b into columns.  Two encrypted blocks: low and high halves through
+// bivariate lookups.  An encrypted block x times a public block t needs no bootstrap at all: t = 1
+// is x itself, t = 2, 3 the lazy block t x (degree 3t, noise t^2) that the column compression
+// splits like any other column entry -- a scalar multiply saves its whole product level.
 static void add_products(const Radix& a, const Radix& b, uint32_t nblocks, std::vector<PbsItem>& items,
-                         std::vector<uint32_t>& cols_of) {
+                         std::vector<uint32_t>& cols_of, std::vector<std::pair<uint32_t, Block>>& direct) {
     static const auto LUT_MUL_LO = lut2([](uint32_t x, uint32_t y) { return (x * y) & 3; });
     static const auto LUT_MUL_HI = lut2([](uint32_t x, uint32_t y) { return (x * y) >> 2; });
     for (uint32_t p = 0; p < a.nblocks(); ++p) {
@@ -1101,6 +1105,15 @@ static void add_products(const Radix& a, const Radix& b, uint32_t nblocks, std::
             const Block& bq = b.blocks[q];
             if (bq.trivial() && bq.value == 0) continue;
             engine_check(ap.degree <= 3 && bq.degree <= 3, "mul needs clean operands");
+            if (ap.trivial() || bq.trivial()) {
+                const Block& x = ap.trivial() ? bq : ap;
+                const uint32_t t = ap.trivial() ? ap.value : bq.value;
+                if (x.trivial())
+                    direct.push_back({p + q, Block::make_trivial(ap.value * bq.value)});
+                else
+                    direct.push_back({p + q, t == 1 ? x : block_lazy({{x, (int32_t)t}}, 0, t * x.degree)});
+                continue;
+            }
             items.push_back(item2(ap, bq, LUT_MUL_LO));
             cols_of.push_back(p + q);
             if (p + q + 1 < nblocks && ap.degree * bq.degree >= 4) {
@@ -1115,10 +1128,11 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
                                   uint32_t nblocks, const std::vector<const Radix*>& addends) {
     std::vector<PbsItem> items;
     std::vector<uint32_t> cols_of;
+    std::vector<std::vector<std::pair<uint32_t, Block>>> direct(ops.size());
     std::vector<size_t> start(ops.size() + 1, 0);
     for (size_t i = 0; i < ops.size(); ++i) {
         start[i] = items.size();
-        add_products(*ops[i].first, *ops[i].second, nblocks, items, cols_of);
+        add_products(*ops[i].first, *ops[i].second, nblocks, items, cols_of, direct[i]);
     }
     start[ops.size()] = items.size();
     Blocks outs = e.run(items);
@@ -1127,6 +1141,7 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
         probs[i].nblocks = nblocks;
         probs[i].cols.assign(nblocks, {});
         for (size_t j = start[i]; j < start[i + 1]; ++j) probs[i].cols[cols_of[j]].push_back(outs[j]);
+        for (auto& d : direct[i]) probs[i].cols[d.first].push_back(d.second);
         if (i < addends.size() && addends[i])
             for (uint32_t k = 0; k < nblocks && k < addends[i]->nblocks(); ++k)
                 probs[i].cols[k].push_back(addends[i]->blocks[k]);
