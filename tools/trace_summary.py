@@ -3,7 +3,7 @@ bucketed by level size."""
 import re, sys
 cur = None; d = {}
 for line in open(sys.argv[1]):
-    if line.startswith("== ") and "total" not in line:
+    if line.startswith("== ") and len(line.split()) == 2:
         cur = line.split()[1]; d[cur] = []
     m = re.match(r"\[level (\d+)\] (\d+) PBS ([\d.]+) ms", line)
     if m and cur:
