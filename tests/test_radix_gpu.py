@@ -214,3 +214,23 @@ def test_deferred_graph_lifetimes_and_raw_pbs(keys):
     assert q.decrypt(ck) == (((xs[0] + xs[1]) % m) * ((xs[2] * xs[3]) % m) + xs[0]) % m
     assert s01.decrypt(ck) == (xs[0] + xs[1]) % m
     assert p23.decrypt(ck) == (xs[2] * xs[3]) % m
+
+
+def test_biguint_compat_uneven_limbs(keys):
+    """Compat mul / mul_add on uneven limb counts (2x3, 5x2, 3x4, 4x4 with all-ones limbs that make
+    the reference drop carries): the lazy window waves, the 2-limb last windows and the top-run
+    carry prefix against oracle/ref_semantics.py's replay of src/biguint.rs:194-265."""
+    ck, _ = keys
+    rng = random.Random(0xC0DA)
+    for la, lb in ((2, 3), (5, 2), (3, 4), (4, 4)):
+        for trial in range(2):
+            if trial == 0:
+                al = [rng.getrandbits(32) | 1 << 31 for _ in range(la)]
+                bl = [rng.getrandbits(32) | 1 << 31 for _ in range(lb)]
+            else:
+                al, bl = [0xFFFFFFFF] * la, [0xFFFFFFFF] * lb
+            kl = [rng.getrandbits(32) | 1 for _ in range(3)]
+            a, b, k = _big(ck, al), _big(ck, bl), _big(ck, kl)
+            want = R.biguint_mul(al, bl)
+            assert a.mul(b, COMPAT).decrypt_limbs(ck) == want, (la, lb, trial)
+            assert a.mul_add(b, k, COMPAT).decrypt_limbs(ck) == R.biguint_add(kl, want), (la, lb, trial)
