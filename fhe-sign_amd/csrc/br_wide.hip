@@ -14,10 +14,12 @@
 //   C  regs (b5,b4)   idx = 64 (L>>2) + 16 r + 4 (L&3) + q     stages 4,5
 //   D  regs (b3,b2)   idx = 16 L + 4 r + q                     stages 6,7
 //   E  regs (b1,b0)   idx = 256 q + 4 L + r  (= the BSK layout R = 4q + r)  stages 8,9
-// A<->B<->C<->D keep (b1,b0) = q fixed, so those exchanges are wave-private 2x2 transposes of
-// register bits with lane bits, done in registers: v_permlane32_swap / v_permlane16_swap for lane
-// bits 5,4 and DPP row shifts + select for lane bits 3..0.  Only D<->E crosses waves (LDS, linear
-// bit-weight layout found by tools/lds_layout_search.py).
+// A<->B<->C<->D keep (b1,b0) = q fixed, so those exchanges are wave-private transposes of register
+// bits with lane bits: v_permlane32_swap / v_permlane16_swap for lane bits 5,4, bank-masked DPP
+// moves for lane bits 3,2, and a wave-private LDS region (no barrier, conflict-free XOR map) for lane
+// bits 1,0, whose DPP form needed two moves + two selects per dword (measured: 2-4 % lower level
+// latency; the same LDS form for lane bits 3,2 was 11 % slower than its DPP moves).  Only D<->E
+// crosses waves (LDS, linear bit-weight layout found by tools/lds_layout_search.py).
 #include "device_math.h"
 #include "kernels.h"
 
@@ -29,6 +31,11 @@ namespace {
 // (tools/lds_layout_wide3.py; the additive map of earlier rounds was 4-way on three of the four)
 constexpr int XA[10] = {0x038, 0x190, 0x144, 0x184, 0x001, 0x002, 0x004, 0x008, 0x040, 0x200};
 constexpr int CROSS_SZ = 1024;
+// wave-private C <-> D exchange (register bits <-> lane bits 1,0 inside 4-lane groups g = L >> 2):
+// element (g, a = C lane bits 1..0, r = C register) at 20 g + 4 a + (r ^ a) -- conflict-free for
+// both directions' b128 stores (8-lane groups) and loads (16-lane groups)
+constexpr int CD_SZ = 20 * 15 + 16;
+FHE_DEV constexpr int cdpos(int g, int a, int r) { return 20 * g + 4 * a + (r ^ a); }
 constexpr int ROT_SZ = 2560;  // accumulator staging (f64): pos(c) = c + (c >> 2)
 
 FHE_DEV constexpr int fx(int x) {
@@ -72,27 +79,6 @@ FHE_DEV void xpose_permlane(cplx& X, cplx& Y) {
     X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
     Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
 }
-// K in 0..3: DPP row shifts by 2^K inside 16-lane rows, then a per-lane select
-template <int K>
-FHE_DEV void xpose_dpp(cplx& X, cplx& Y, bool hi) {
-    constexpr int SH = 1 << K;
-    uint32_t x[4], y[4];
-    u64_split(X.x, x[0], x[1]);
-    u64_split(X.y, x[2], x[3]);
-    u64_split(Y.x, y[0], y[1]);
-    u64_split(Y.y, y[2], y[3]);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const uint32_t ys = (uint32_t)__builtin_amdgcn_mov_dpp((int)y[d], 0x110 + SH, 0xF, 0xF, false);  // row_shr: y[l - SH]
-        const uint32_t xs = (uint32_t)__builtin_amdgcn_mov_dpp((int)x[d], 0x100 + SH, 0xF, 0xF, false);  // row_shl: x[l + SH]
-        const uint32_t nx = hi ? ys : x[d];
-        const uint32_t ny = hi ? y[d] : xs;
-        x[d] = nx;
-        y[d] = ny;
-    }
-    X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
-    Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
-}
 // K in 2..3: the lanes with lane bit K set are whole 4-lane DPP banks, so each half of the
 // transpose is ONE bank-masked DPP move (disabled lanes keep the old value): 2 ops per dword, no select
 template <int K>
@@ -129,15 +115,6 @@ FHE_DEV void xpose_AB(cplx (&x)[4]) {
     xpose_permlane<4>(x[0], x[1]);
     xpose_permlane<4>(x[2], x[3]);
 }
-template <int KH, int KL>
-FHE_DEV void xpose_dpp2(cplx (&x)[4], int L) {
-    const bool h = (L >> KH) & 1, l = (L >> KL) & 1;
-    xpose_dpp<KH>(x[0], x[2], h);
-    xpose_dpp<KH>(x[1], x[3], h);
-    xpose_dpp<KL>(x[0], x[1], l);
-    xpose_dpp<KL>(x[2], x[3], l);
-}
-
 // two stages of the twisted forward (oracle fho_fft_forward_twisted) on register bits 1 then 0: the
 // first shares one block zeta z0, the second's blocks are siblings (z1, i z1)
 FHE_DEV void ct2(cplx (&x)[4], cplx z0, cplx z1) {
@@ -186,6 +163,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     __shared__ __attribute__((aligned(16))) double s_rot[2][ROT_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_inv[2][CROSS_SZ];  // inverse E -> D exchange
+    __shared__ __attribute__((aligned(16))) cplx s_cd[8][CD_SZ];      // C <-> D, one region per wave
 
     const int ct = blockIdx.x;
     const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
@@ -218,6 +196,8 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         }
     }
     double* rot_me = s_rot[p];
+    cplx* cd = s_cd[w];
+    const int gL = L >> 2, aL = L & 3;
     cplx* cross = s_cross[p];
     // lane parts of the linear LDS maps
     const int xD = fx(16 * L + q), xE = fx(256 * q + 4 * L);
@@ -268,7 +248,11 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         ct2(x, ZT[2], ZT[3]);
         xpose_dpp32(x);              // B -> C: regs <-> lane bits 3,2
         ct2(x, ZT[4], ZT[5]);
-        xpose_dpp2<1, 0>(x, L);      // C -> D: regs <-> lane bits 1,0
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cd[cdpos(gL, aL, r)] = x[r];  // C -> D: regs <-> lane bits 1,0
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = cd[cdpos(gL, r, aL)];
         ct2(x, ZT[6], ZT[7]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) cross[xD ^ fx(4 * r)] = x[r];
@@ -308,7 +292,11 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = inv[xD ^ fx(4 * r)];
         dit2(x, T[9], T[10], T[11]);
-        xpose_dpp2<1, 0>(x, L);      // D -> C
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cd[cdpos(gL, r, aL)] = x[r];  // D -> C
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = cd[cdpos(gL, aL, r)];
         dit2(x, T[6], T[7], T[8]);
         xpose_dpp32(x);              // C -> B
         dit2(x, T[3], T[4], T[5]);

@@ -224,6 +224,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         d.cst = (uint64_t)dcst * delta;
         d.dst = out[i].slot->p;
         out[i].slot->node = (int64_t)pending_.size();
+        if (!n.deps.empty()) ++pending_dependent_;
         pending_.push_back(std::move(n));
     }
     if (pending_.size() >= (size_t)1 << 20) flush();  // bound the deferred graph (host memory)
@@ -231,17 +232,9 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     // products) is one throughput level under any schedule: launch it now, so the GPU works while
     // the host builds the rest of the graph (once per explicit flush: later independent batches,
     // e.g. the compressions that follow, stay in the graph to be spread over idle capacity)
-    if (eager_ok_ && pending_.size() >= kEagerBatch && pending_.front().deps.empty() && pending_.back().deps.empty()) {
-        bool independent = true;
-        for (const Pending& n : pending_)
-            if (!n.deps.empty()) {
-                independent = false;
-                break;
-            }
-        if (independent) {
-            flush();
-            eager_ok_ = false;
-        }
+    if (eager_ok_ && pending_.size() >= kEagerBatch && pending_dependent_ == 0) {
+        flush();
+        eager_ok_ = false;
     }
     return out;
 }
@@ -409,6 +402,7 @@ void Engine::flush() {
     }
     for (auto& n : pending_) n.hold[0]->node = -1;
     pending_.clear();  // the stream orders any later reuse of the held slots behind these launches
+    pending_dependent_ = 0;
     eager_ok_ = true;
 }
 

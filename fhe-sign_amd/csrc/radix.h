@@ -134,6 +134,7 @@ private:
         std::vector<int32_t> deps;                // pending producers of the inputs
     };
     std::vector<Pending> pending_;
+    size_t pending_dependent_ = 0;  // pending nodes with at least one pending producer
     PbsDesc* h_desc_[2] = {nullptr, nullptr};  // pinned, double-buffered
     hipEvent_t desc_ev_[2] = {nullptr, nullptr};
     size_t desc_cap_ = 0;
