@@ -82,6 +82,83 @@ int fhe_ctx_detach_comm(fhe_ctx* c) {
     return FHE_OK;
 }
 
+// the server key lives on one rank (e.g. deserialized from the client) and is
+// replicated device-to-device over xGMI.  Rank `root` broadcasts its parameters, then its
+// standard-layout KSK and Fourier BSK (123 MB at the default parameters); every other rank
+// derives the kernels' layouts (KSK byte planes, quad BSK) with its own conversion kernels, exactly
+// as fhe_set_server_key would.  Collective: every rank of the communicator calls it.
+int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
+    if (!c || !c->comm || root < 0 || root >= c->nranks) {
+        set_error("broadcast_server_key needs an attached communicator and a valid root");
+        return FHE_ERR_INVALID;
+    }
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    const bool is_root = c->rank == root;
+    if (is_root && !c->has_key) {
+        set_error("the root rank has no server key installed");
+        return FHE_ERR_NO_KEY;
+    }
+    if (c->engine) c->engine->flush();  // pending work of the old key runs first
+    // parameters (a few words; also tells the receivers the buffer sizes)
+    fhe_params hp = c->p.to_c();
+    fhe_params* dp = nullptr;
+    FHE_HIP_CHECK(hipMalloc(&dp, sizeof(fhe_params)));
+    FHE_HIP_CHECK(hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, c->stream));
+    int rc = nccl_check(ncclBroadcast(dp, dp, sizeof(fhe_params), ncclUint8, root, comm, c->stream), "ncclBroadcast");
+    if (!rc) rc = hipMemcpyAsync(&hp, dp, sizeof hp, hipMemcpyDeviceToHost, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    (void)hipFree(dp);
+    if (rc) return rc;
+    Params p;
+    const char* why = nullptr;
+    if (!Params::from_c(hp, &p, &why)) {
+        set_error(why);
+        return FHE_ERR_UNSUPPORTED;
+    }
+    const size_t ksk_words = (size_t)kBigDim * p.ks_level * (p.n + 1);
+    const int npoly = (int)(p.n * 4);
+    const size_t bsk_doubles = (size_t)npoly * 1024 * 2;
+    if (!is_root) {
+        if (c->has_key) {
+            FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+            FHE_HIP_CHECK(hipFree(c->d_ksk));
+            FHE_HIP_CHECK(hipFree(c->d_bsk));
+            FHE_HIP_CHECK(hipFree(c->d_bsk_quad));
+            FHE_HIP_CHECK(hipFree(c->d_ksk_planes));
+            c->has_key = false;
+        }
+        FHE_HIP_CHECK(hipMalloc(&c->d_ksk, ksk_words * 8));
+        FHE_HIP_CHECK(hipMalloc(&c->d_ksk_planes, fhe::ks_planes_bytes((int)p.n)));
+        FHE_HIP_CHECK(hipMalloc(&c->d_bsk, bsk_doubles * 8));
+        FHE_HIP_CHECK(hipMalloc(&c->d_bsk_quad, bsk_doubles * 8));
+    }
+    rc = nccl_check(ncclBroadcast(c->d_ksk, c->d_ksk, ksk_words, ncclUint64, root, comm, c->stream), "ncclBroadcast");
+    if (!rc) rc = nccl_check(ncclBroadcast(c->d_bsk, c->d_bsk, bsk_doubles, ncclFloat64, root, comm, c->stream), "ncclBroadcast");
+    if (rc) return rc;
+    if (!is_root) {
+        FHE_HIP_CHECK(launch_ksk_to_planes(c->d_ksk, (int)p.n, c->d_ksk_planes, c->stream));
+        FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, c->d_bsk_quad, c->stream));
+        if (!(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
+            c->lut_ids.clear();
+            c->h_luts.clear();
+            c->luts_dirty = true;
+        }
+        c->p = p;
+        c->has_key = true;
+        if (!c->engine) {
+            try {
+                c->engine = new fhe::Engine(c);
+            } catch (const std::exception& ex) {
+                set_error(ex.what());
+                return FHE_ERR_HIP;
+            }
+        }
+    }
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return FHE_OK;
+}
+
 int fhe_ctx_set_fanout(fhe_ctx* c, uint32_t min_level, int emulate_ranks) {
     if (!c || emulate_ranks < 0) return FHE_ERR_INVALID;
     c->fanout_min = min_level;

@@ -486,6 +486,16 @@ int fhe_ctx_export_fourier_bsk(fhe_ctx* c, double* out, size_t len) {
     return FHE_OK;
 }
 
+int fhe_ctx_params(const fhe_ctx* c, fhe_params* out) {
+    if (!c || !out) return FHE_ERR_INVALID;
+    if (!c->has_key) {
+        set_error("no server key installed");
+        return FHE_ERR_NO_KEY;
+    }
+    *out = c->p.to_c();
+    return FHE_OK;
+}
+
 int fhe_ctx_sync(fhe_ctx* c) {
     if (!c) return FHE_ERR_INVALID;
     if (c->engine) {

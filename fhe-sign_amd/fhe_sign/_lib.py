@@ -56,6 +56,8 @@ _SIGNATURES = [
     ("fhe_ctx_set_ks_kernel", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("fhe_ctx_attach_comm", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+    ("fhe_ctx_broadcast_server_key", C.c_int, [C.c_void_p, C.c_int]),
+    ("fhe_ctx_params", C.c_int, [C.c_void_p, C.POINTER(FheParams)]),
     ("fhe_ctx_detach_comm", C.c_int, [C.c_void_p]),
     ("fhe_ctx_set_fanout", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
     ("fhe_ctx_fanout_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint64)]),

@@ -195,6 +195,13 @@ class Context:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         check(load().fhe_ctx_attach_comm(self._h, buf, nranks, rank))
 
+    def broadcast_server_key(self, root: int = 0) -> None:
+        """collective: replicate rank `root`'s installed server key to every rank (RCCL)"""
+        check(load().fhe_ctx_broadcast_server_key(self._h, int(root)))
+        p = FheParams()
+        check(load().fhe_ctx_params(self._h, C.byref(p)))
+        self.params = p
+
     def detach_comm(self) -> None:
         check(load().fhe_ctx_detach_comm(self._h))
 

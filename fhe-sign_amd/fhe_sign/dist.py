@@ -55,3 +55,17 @@ def attach_fanout(ctx, dist, rank: int, world: int, min_level: int = 257, make_i
             pass
         return False, err or "another rank failed to attach"
     return True, None
+
+
+def replicate_server_key(ctx, dist, rank: int, root: int = 0) -> tuple[bool, str | None]:
+    """After attach_fanout: rank `root` (which called ctx.set_server_key) replicates its server key
+    to every rank's context over RCCL (fhe_ctx_broadcast_server_key).  The ranks first agree that
+    the root has a key, so nobody enters the collective alone.  Returns (ok, error) on every rank."""
+    ok = rank != root or getattr(ctx, "params", None) is not None  # set by Context.set_server_key
+    if not all_ok(dist, ok):
+        return False, "the root rank has no server key"
+    try:
+        ctx.broadcast_server_key(root)
+    except Exception as e:  # noqa: BLE001
+        return False, str(e)
+    return True, None

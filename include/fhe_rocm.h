@@ -142,6 +142,13 @@ int fhe_ctx_set_ks_kernel(fhe_ctx* ctx, int kind);
 #define FHE_COMM_ID_BYTES 128
 int fhe_comm_unique_id(uint8_t id[FHE_COMM_ID_BYTES]);
 int fhe_ctx_attach_comm(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank);
+/* Collective over the attached communicator: rank `root` (which has a server key installed)
+ * replicates it to every rank device-to-device (RCCL broadcast over xGMI: parameters, KSK, Fourier
+ * BSK; each receiver derives the kernels' layouts itself).  Afterwards every rank's context is as if
+ * fhe_set_server_key had been called with the root's key. */
+int fhe_ctx_broadcast_server_key(fhe_ctx* ctx, int root);
+/* parameters of the server key installed in a context */
+int fhe_ctx_params(const fhe_ctx* ctx, fhe_params* out);
 int fhe_ctx_detach_comm(fhe_ctx* ctx);
 /* split threshold (default 257: above one ciphertext per CU) and, for single-GPU tests, the number of emulated ranks (0 = off) */
 int fhe_ctx_set_fanout(fhe_ctx* ctx, uint32_t min_level, int emulate_ranks);

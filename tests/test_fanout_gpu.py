@@ -79,3 +79,30 @@ def test_rccl_world1_all_gather(keys):
     set_server_key(None)
     ctx.close()
     ref_ctx.close()
+
+
+def test_rccl_world1_server_key_broadcast(keys):
+    """fhe_ctx_broadcast_server_key (the key replicated over xGMI) on a world-1 RCCL
+    communicator: the root's key survives the collective bit for bit and keeps computing; misuse
+    (no communicator, a root without a key) is refused.  The receiving side (ranks != root) needs a
+    second GPU: it runs on the driver's multi-GPU node only."""
+    ck, sk = keys
+    ctx = Context(0)
+    with pytest.raises(RuntimeError):
+        ctx.broadcast_server_key(0)  # no communicator attached
+    ctx.attach_comm(comm_unique_id(), 1, 0)
+    with pytest.raises(RuntimeError):
+        ctx.broadcast_server_key(0)  # root without a key
+    ctx.set_server_key(sk)
+    before = ctx.export_fourier_bsk()
+    ctx.broadcast_server_key(0)
+    assert np.array_equal(ctx.export_fourier_bsk().view(np.uint64), before.view(np.uint64))
+    _, val = run_ops(ctx, ck)
+    ref_ctx = Context(0)
+    ref_ctx.set_server_key(sk)
+    _, ref_val = run_ops(ref_ctx, ck)
+    assert val == ref_val
+    ctx.detach_comm()
+    set_server_key(None)
+    ctx.close()
+    ref_ctx.close()
