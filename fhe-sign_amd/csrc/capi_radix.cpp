@@ -103,11 +103,9 @@ int fhe_radix_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint64_t* words, uin
     }
     return guarded([&] {
         Radix r;
-        std::vector<uint64_t> ct((size_t)(bits / 2) * kBigCt);
-        for (uint32_t k = 0; k < bits / 2; ++k) {
-            const uint32_t m = word_bits(words, 2 * k, bits);
-            encrypt_big(ck, (uint64_t)m * ck->params.delta(), ct.data() + (size_t)k * kBigCt);
-        }
+        std::vector<uint64_t> ct((size_t)(bits / 2) * kBigCt), pts(bits / 2);
+        for (uint32_t k = 0; k < bits / 2; ++k) pts[k] = (uint64_t)word_bits(words, 2 * k, bits) * ck->params.delta();
+        encrypt_big_many(ck, pts.data(), pts.size(), ct.data());
         r.blocks = c->engine->upload_many(ct.data(), bits / 2, 3);
         *out = wrap(std::move(r), bits);
         return FHE_OK;
@@ -386,11 +384,11 @@ int fhe_biguint_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint32_t* limbs, s
     if (!ck || !out || (n && !limbs)) return FHE_ERR_INVALID;
     return guarded([&] {
         auto* b = new fhe_biguint();
-        std::vector<uint64_t> ct(n * kLimbBlocks * kBigCt);
+        std::vector<uint64_t> ct(n * kLimbBlocks * kBigCt), pts(n * kLimbBlocks);
         for (size_t i = 0; i < n; ++i)
             for (uint32_t k = 0; k < kLimbBlocks; ++k)
-                encrypt_big(ck, (uint64_t)((limbs[i] >> (2 * k)) & 3u) * ck->params.delta(),
-                            ct.data() + (i * kLimbBlocks + k) * kBigCt);
+                pts[i * kLimbBlocks + k] = (uint64_t)((limbs[i] >> (2 * k)) & 3u) * ck->params.delta();
+        encrypt_big_many(ck, pts.data(), pts.size(), ct.data());
         Blocks all = c->engine->upload_many(ct.data(), n * kLimbBlocks, 3);
         for (size_t i = 0; i < n; ++i) {
             Radix r;

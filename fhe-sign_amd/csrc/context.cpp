@@ -354,6 +354,20 @@ int fhe_encrypt_block(fhe_client_key* ck, uint64_t value, uint64_t* ct) {
     return FHE_OK;
 }
 
+int fhe_encrypt_blocks(fhe_client_key* ck, const uint64_t* values, size_t n, uint64_t* cts) {
+    if (!ck || (n && (!values || !cts))) return FHE_ERR_INVALID;
+    std::vector<uint64_t> pts(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (values[i] >= ck->params.msg_carry()) {
+            set_error("block value out of range");
+            return FHE_ERR_INVALID;
+        }
+        pts[i] = values[i] * ck->params.delta();
+    }
+    encrypt_big_many(ck, pts.data(), n, cts);
+    return FHE_OK;
+}
+
 int fhe_decrypt_block(const fhe_client_key* ck, const uint64_t* ct, uint64_t* value) {
     if (!ck || !ct || !value) return FHE_ERR_INVALID;
     *value = decode_block(ck->params, decrypt_phase_big(ck, ct));

@@ -6,6 +6,7 @@
 // consumes the server key produced here.
 #include "keys.h"
 
+#include <algorithm>
 #include <cstring>
 #include <thread>
 
@@ -127,6 +128,18 @@ bool ChaChaStream::load(const uint32_t* in) {
     return true;
 }
 
+bool ChaChaStream::seek(uint64_t word) {
+    const uint64_t blk = word / 16;
+    if (blk >= (1ull << 32) - 1) return false;
+    counter_ = (uint32_t)blk;
+    pos_ = 16;
+    if (word % 16) {
+        refill();
+        pos_ = (uint32_t)(word % 16);
+    }
+    return true;
+}
+
 uint64_t ChaChaStream::next_u64() {
     if (pos_ >= 16) refill();
     uint64_t lo = buf_[pos_++];
@@ -217,14 +230,38 @@ void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_serve
     for (auto& th : pool) th.join();
 }
 
-void encrypt_big(fhe_client_key* ck, uint64_t pt, uint64_t* ct) {
+static void encrypt_with(ChaChaStream& rng, const fhe_client_key* ck, uint64_t pt, uint64_t* ct) {
     uint64_t dot = 0;
     for (uint32_t j = 0; j < kBigDim; ++j) {
-        ct[j] = ck->enc_rng.next_u64();
+        ct[j] = rng.next_u64();
         dot += ct[j] * ck->glwe_sk[j];
     }
-    const int64_t e = ck->enc_rng.tuniform(ck->params.glwe_noise_log2);
+    const int64_t e = rng.tuniform(ck->params.glwe_noise_log2);
     ct[kBigDim] = dot + pt + (uint64_t)e;
+}
+
+void encrypt_big(fhe_client_key* ck, uint64_t pt, uint64_t* ct) { encrypt_with(ck->enc_rng, ck, pt, ct); }
+
+void encrypt_big_many(fhe_client_key* ck, const uint64_t* pts, size_t n, uint64_t* cts) {
+    constexpr uint64_t kWords = 2 * (uint64_t)kBigCt;  // 32-bit stream words one encryption consumes
+    const uint64_t w0 = ck->enc_rng.word_pos();
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t T = std::min<size_t>(std::min<size_t>(hw, 16), n / 32);
+    ChaChaStream probe = ck->enc_rng;
+    if (T <= 1 || !probe.seek(w0 + kWords * n)) {
+        for (size_t i = 0; i < n; ++i) encrypt_with(ck->enc_rng, ck, pts[i], cts + i * kBigCt);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            const size_t lo = n * t / T, hi = n * (t + 1) / T;
+            ChaChaStream r = ck->enc_rng;
+            r.seek(w0 + kWords * lo);
+            for (size_t i = lo; i < hi; ++i) encrypt_with(r, ck, pts[i], cts + i * kBigCt);
+        });
+    for (auto& x : th) x.join();
+    ck->enc_rng = probe;  // positioned after the n-th encryption
 }
 
 uint64_t decrypt_phase_big(const fhe_client_key* ck, const uint64_t* ct) {

@@ -41,6 +41,11 @@ public:
     void reset(uint64_t seed, uint32_t stream);
     uint64_t next_u64();
     int64_t tuniform(uint32_t log2_bound);
+    // absolute position (32-bit words) of the next output within the current nonce epoch, and a
+    // jump to such a position (false if it leaves the epoch): lets independent encryptions of a
+    // batch run in parallel on copies of the stream with exactly the sequential outputs
+    uint64_t word_pos() const { return (uint64_t)counter_ * 16 - (16 - pos_); }
+    bool seek(uint64_t word);
     // full state (key, nonce, counter, buffered block, position) for serialization (serial.cpp)
     static constexpr size_t kStateWords = 8 + 3 + 1 + 16 + 1;
     void save(uint32_t* out) const;
@@ -76,6 +81,9 @@ struct fhe_server_key {
 namespace fhe {
 void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_server_key* sk);
 void encrypt_big(fhe_client_key* ck, uint64_t plaintext, uint64_t* ct);
+// n encryptions (plaintexts already scaled), outputs and stream state identical to n encrypt_big
+// calls; large batches run on several host threads over seeked copies of the stream
+void encrypt_big_many(fhe_client_key* ck, const uint64_t* plaintexts, size_t n, uint64_t* cts);
 uint64_t decrypt_phase_big(const fhe_client_key* ck, const uint64_t* ct);
 uint64_t decode_block(const Params& p, uint64_t phase);  // value incl. carry, mod msg*carry
 }  // namespace fhe

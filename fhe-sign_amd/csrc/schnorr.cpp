@@ -258,14 +258,76 @@ Pt padd(const Pt& a, const Pt& b) {  // affine add/double (src/secp256k1.rs:50-9
     U256 y3 = fsub(fmul(lam, fsub(a.x, x3)), a.y);
     return mkpt(x3, y3);
 }
-Pt pmul(Pt p, const U256& k_in) {  // double-and-add (src/secp256k1.rs:106-127), scalar mod n
-    U256 k = nmod(k_in);
-    Pt r;
-    for (int i = 0; i < 256; ++i) {
-        if (k.bit(i)) r = padd(r, p);
-        p = padd(p, p);
-    }
+// k * p (src/secp256k1.rs:106-127 computes it by affine double-and-add with the scalar mod n).
+// Same point, computed in Jacobian coordinates (X / Z^2, Y / Z^3): left-to-right doubling and mixed
+// additions of the affine p, ONE field inversion at the end instead of one per step (the affine
+// steps' inversions made a signature's two scalar multiplications ~10 ms of host time).  Every
+// special case of the affine law is kept: k = 0 (mod n) or p at infinity gives infinity, an
+// addition of opposite points gives infinity, an addition of equal points doubles.
+namespace {
+struct Jac {
+    U256 X, Y, Z;  // Z = 0: infinity
+    bool inf() const { return Z.w[0] == 0 && Z.w[1] == 0 && Z.w[2] == 0 && Z.w[3] == 0; }
+};
+Jac jdbl(const Jac& a) {  // dbl-2009-l (a = 0)
+    if (a.inf()) return a;
+    const U256 A = fmul(a.X, a.X), B = fmul(a.Y, a.Y), C = fmul(B, B);
+    const U256 xb = fadd(a.X, B);
+    U256 D = fsub(fsub(fmul(xb, xb), A), C);
+    D = fadd(D, D);
+    const U256 E = fadd(fadd(A, A), A), F = fmul(E, E);
+    Jac r;
+    r.X = fsub(F, fadd(D, D));
+    U256 c8 = fadd(C, C);
+    c8 = fadd(c8, c8);
+    c8 = fadd(c8, c8);
+    r.Y = fsub(fmul(E, fsub(D, r.X)), c8);
+    const U256 yz = fmul(a.Y, a.Z);
+    r.Z = fadd(yz, yz);
     return r;
+}
+Jac jmadd(const Jac& a, const Pt& b) {  // madd-2007-bl: a + affine b
+    if (b.inf) return a;
+    if (a.inf()) {
+        Jac r;
+        r.X = b.x;
+        r.Y = b.y;
+        r.Z.w[0] = 1;
+        return r;
+    }
+    const U256 Z1Z1 = fmul(a.Z, a.Z);
+    const U256 U2 = fmul(b.x, Z1Z1), S2 = fmul(b.y, fmul(a.Z, Z1Z1));
+    const U256 H = fsub(U2, a.X);
+    U256 rr = fsub(S2, a.Y);
+    if (H.w[0] == 0 && H.w[1] == 0 && H.w[2] == 0 && H.w[3] == 0) {
+        if (rr.w[0] == 0 && rr.w[1] == 0 && rr.w[2] == 0 && rr.w[3] == 0) return jdbl(a);  // equal points
+        return Jac();  // opposite points
+    }
+    rr = fadd(rr, rr);
+    const U256 HH = fmul(H, H);
+    U256 I = fadd(HH, HH);
+    I = fadd(I, I);
+    const U256 J = fmul(H, I), V = fmul(a.X, I);
+    Jac r;
+    r.X = fsub(fsub(fmul(rr, rr), J), fadd(V, V));
+    const U256 yj = fmul(a.Y, J);
+    r.Y = fsub(fmul(rr, fsub(V, r.X)), fadd(yj, yj));
+    const U256 zh = fadd(a.Z, H);
+    r.Z = fsub(fsub(fmul(zh, zh), Z1Z1), HH);
+    return r;
+}
+}  // namespace
+
+Pt pmul(Pt p, const U256& k_in) {
+    const U256 k = nmod(k_in);
+    Jac r;
+    for (int i = 255; i >= 0; --i) {
+        r = jdbl(r);
+        if (k.bit(i)) r = jmadd(r, p);
+    }
+    if (r.inf()) return Pt();
+    const U256 zi = finv(r.Z), zi2 = fmul(zi, zi);
+    return mkpt(fmul(r.X, zi2), fmul(r.Y, fmul(zi2, zi)));
 }
 Pt generator() {
     static const uint8_t gx[32] = {0x79, 0xBE, 0x66, 0x7E, 0xF9, 0xDC, 0xBB, 0xAC, 0x55, 0xA0, 0x62, 0x95, 0xCE, 0x87, 0x0B, 0x07,

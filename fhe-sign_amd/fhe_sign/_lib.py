@@ -36,6 +36,7 @@ _SIGNATURES = [
     ("fhe_server_key_export", C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
     ("fhe_client_key_seed_encryption", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32]),
     ("fhe_encrypt_block", C.c_int, [C.c_void_p, C.c_uint64, u64p]),
+    ("fhe_encrypt_blocks", C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p]),
     ("fhe_decrypt_block", C.c_int, [C.c_void_p, u64p, u64p]),
     ("fhe_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     ("fhe_ctx_destroy", None, [C.c_void_p]),

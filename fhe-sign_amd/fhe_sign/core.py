@@ -57,6 +57,13 @@ class ClientKey:
         check(load().fhe_encrypt_block(self._h, value, ptr(ct)))
         return ct
 
+    def encrypt_blocks(self, values) -> np.ndarray:
+        """many blocks at once: identical to encrypt_block in a loop (multi-threaded on the host)"""
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.uint64))
+        out = np.zeros((v.size, BIG_CT), np.uint64)
+        check(load().fhe_encrypt_blocks(self._h, ptr(v), v.size, ptr(out)))
+        return out
+
     def decrypt_block(self, ct: np.ndarray) -> int:
         ct = np.ascontiguousarray(ct, dtype=np.uint64)
         out = C.c_uint64(0)

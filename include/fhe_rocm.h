@@ -88,6 +88,9 @@ int fhe_client_key_seed_encryption(fhe_client_key* ck, uint64_t seed, uint32_t s
 /* Shortint block encrypt/decrypt (the per-block step under FheUint32::try_encrypt,
  * src/biguint.rs:26, and FheDecrypt, src/biguint.rs:70).  value < message*carry modulus. */
 int fhe_encrypt_block(fhe_client_key* ck, uint64_t value, uint64_t* ct /*2049*/);
+/* n blocks at once (cts: n x 2049 words): the same ciphertexts and stream state as n calls of
+ * fhe_encrypt_block, computed on several host threads (each on a seeked copy of the stream) */
+int fhe_encrypt_blocks(fhe_client_key* ck, const uint64_t* values, size_t n, uint64_t* cts);
 int fhe_decrypt_block(const fhe_client_key* ck, const uint64_t* ct, uint64_t* value /*msg+carry*/);
 
 /* ------------------------------------------------------------------------------- context */

@@ -58,3 +58,24 @@ def test_ksk_rows_decrypt_to_gadget(keys):
             expect = (int(ok.glwe_sk[j]) << (64 - 3 * (lv + 1))) % 2**64
             err = (phase - expect + 2**63) % 2**64 - 2**63
             assert abs(err) <= 2**44
+
+
+def test_batch_encryption_equals_sequential():
+    """fhe_encrypt_blocks (multi-threaded over seeked copies of the encryption stream, used by every
+    radix / BigUintFHE encryption) gives the sequential loop's ciphertexts and leaves the stream where
+    the loop would, for batch sizes around the threading threshold and a stream mid-block."""
+    import numpy as np
+    from fhe_sign import generate_keys
+    ck, _ = generate_keys(seed=0xB1)
+    ck2, _ = generate_keys(seed=0xB1)
+    for n in (1, 31, 64, 257, 1000):
+        ck.seed_encryption(n, 100)
+        ck2.seed_encryption(n, 100)
+        ck.encrypt_block(3)  # start mid-way through a ChaCha block
+        ck2.encrypt_block(3)
+        vals = [(7 * i + n) % 16 for i in range(n)]
+        seq = np.stack([ck.encrypt_block(v) for v in vals])
+        bat = ck2.encrypt_blocks(vals)
+        assert np.array_equal(seq, bat), n
+        assert np.array_equal(ck.encrypt_block(5), ck2.encrypt_block(5))  # same stream position after
+        assert [ck2.decrypt_block(c) for c in bat[:20]] == vals[:20]
