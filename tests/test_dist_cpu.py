@@ -107,3 +107,46 @@ def test_fanout_attach_failure_is_agreed():
     got = _run_fanout(fail_rank=1)
     assert [ok for _, ok, _ in got] == [False, False]
     assert got[0][2][-1] == ("detach",)
+
+
+class _KeyCtx:
+    """fhe_sign.Context stand-in for the key-replication control plane."""
+
+    def __init__(self, has_key):
+        self.params = object() if has_key else None
+        self.broadcasts = []
+
+    def broadcast_server_key(self, root):
+        self.broadcasts.append(root)
+
+
+def _replicate_rank(rank, world, port, root_has_key, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
+    import torch.distributed as dist
+    from fhe_sign.dist import replicate_server_key
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = _KeyCtx(has_key=(rank == 0 and root_has_key))
+    ok, err = replicate_server_key(ctx, dist, rank, root=0)
+    q.put((rank, ok, ctx.broadcasts))
+    dist.destroy_process_group()
+
+
+def _run_replicate(root_has_key):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replicate_rank, args=(r, 2, port, root_has_key, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    return sorted(q.get() for _ in range(2))
+
+
+def test_server_key_replication_world2():
+    """SURVEY 8e key replication: with a key on the root every rank enters the broadcast; without
+    one, no rank enters the collective and all report failure (nobody waits alone)."""
+    assert _run_replicate(True) == [(0, True, [0]), (1, True, [0])]
+    assert [(r, ok, b) for r, ok, b in _run_replicate(False)] == [(0, False, []), (1, False, [])]
