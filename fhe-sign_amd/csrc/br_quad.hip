@@ -12,9 +12,12 @@
 //   B  idx = 512 h + 256 L5 + 128 L4 + 16 r + (L&15)  regs (b6 b5 b4)  stages 3-5
 //   C  idx = 512 h + 16 (L>>1) + 2 r + (L&1)          regs (b3 b2 b1)  stages 6-8
 //   stage 9 pairs lanes L, L^1 (b0 = L0): DPP quad_perm, one signed add per value.
-// A<->B crosses the two waves of a polynomial (LDS + barrier); B<->C keeps h and stays inside
-// the half (b9 = h) of the exchange region this wave itself read -- no barrier.  All exchanges
-// use one linear LDS map fq (weights by tools/lds_layout_quad*.py: A 1-way, B 1/2-way, C 2-way).
+// A<->B crosses the two waves of a polynomial (LDS + barrier).  B<->C keeps h and swaps register
+// bits (2,1,0) with lane bits (3,2,1) inside the wave: done in registers (bank-masked DPP moves for
+// lane bits 3,2, DPP row shifts + select for lane bit 1) -- the kernel is LDS-bound as much as
+// VALU-bound, and dropping those 16 LDS stores + 16 loads per CMUX beat the +320 VALU ops (71.3 ->
+// 70.5 ms per 8192).  The remaining LDS exchanges use one linear map fq (weights by
+// tools/lds_layout_quad*.py: A 1-way, B 1/2-way, C 2-way).
 // The accumulator coefficients c = 128 r + t (r < 16) are the phase-A points j = 128 r + t and
 // j + 1024 of the folded transform; the BSK is stored in the phase-C layout (k_bsk_to_quad).
 #include "device_math.h"
@@ -110,6 +113,60 @@ FHE_DEV void q_stage9(cplx (&x)[8], uint32_t signbit) {
         x[r] = make_double2(p.x + flip_if(x[r].x, signbit), p.y + flip_if(x[r].y, signbit));
     }
 }
+// ---- B <-> C as register transposes (no LDS): register bits (2,1,0) <-> lane bits (3,2,1)
+FHE_DEV void qsplit(double d, uint32_t& lo, uint32_t& hi) {
+    const uint64_t b = (uint64_t)__double_as_longlong(d);
+    lo = (uint32_t)b;
+    hi = (uint32_t)(b >> 32);
+}
+FHE_DEV double qjoin(uint32_t lo, uint32_t hi) { return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)); }
+template <int K>  // lane bit K in {2, 3}: whole 4-lane DPP banks, one masked move per half
+FHE_DEV void qx_banked(cplx& X, cplx& Y) {
+    constexpr int SH = 1 << K;
+    constexpr int HI = K == 3 ? 0xC : 0xA, LO = K == 3 ? 0x3 : 0x5;
+    uint32_t x[4], y[4];
+    qsplit(X.x, x[0], x[1]);
+    qsplit(X.y, x[2], x[3]);
+    qsplit(Y.x, y[0], y[1]);
+    qsplit(Y.y, y[2], y[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)x[d], (int)y[d], 0x110 + SH, 0xF, HI, false);
+        const uint32_t ny = (uint32_t)__builtin_amdgcn_update_dpp((int)y[d], (int)x[d], 0x100 + SH, 0xF, LO, false);
+        x[d] = nx;
+        y[d] = ny;
+    }
+    X = make_double2(qjoin(x[0], x[1]), qjoin(x[2], x[3]));
+    Y = make_double2(qjoin(y[0], y[1]), qjoin(y[2], y[3]));
+}
+// lane bit 1: row shifts by 2 and a per-lane select
+FHE_DEV void qx_bit1(cplx& X, cplx& Y, bool hi) {
+    uint32_t x[4], y[4];
+    qsplit(X.x, x[0], x[1]);
+    qsplit(X.y, x[2], x[3]);
+    qsplit(Y.x, y[0], y[1]);
+    qsplit(Y.y, y[2], y[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t ys = (uint32_t)__builtin_amdgcn_mov_dpp((int)y[d], 0x112, 0xF, 0xF, false);  // row_shr:2
+        const uint32_t xs = (uint32_t)__builtin_amdgcn_mov_dpp((int)x[d], 0x102, 0xF, 0xF, false);  // row_shl:2
+        const uint32_t nx = hi ? ys : x[d];
+        const uint32_t ny = hi ? y[d] : xs;
+        x[d] = nx;
+        y[d] = ny;
+    }
+    X = make_double2(qjoin(x[0], x[1]), qjoin(x[2], x[3]));
+    Y = make_double2(qjoin(y[0], y[1]), qjoin(y[2], y[3]));
+}
+FHE_DEV void q_xpose_bc(cplx (&x)[8], bool l1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) qx_banked<3>(x[r], x[r + 4]);  // reg bit 2 <-> lane bit 3
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+        if (!(r & 2)) qx_banked<2>(x[r], x[r + 2]);  // reg bit 1 <-> lane bit 2
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) qx_bit1(x[r], x[r + 1], l1);  // reg bit 0 <-> lane bit 1
+}
 }  // namespace
 
 // One workgroup (4 waves) per ciphertext.  W = twiddles W[0..512), ps = [2][8][128]: twist factors
@@ -203,12 +260,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         q_ct<2>(x, s_z[B3], s_z[B3]);
         q_ct<1>(x, s_z[8 + B3], s_z[8 + B3]);
         q_ct<0>(x, s_z[16 + B3], s_z[24 + B3]);
-        wave_sync();  // own half: A->B reads of this wave precede its B->C writes
-#pragma unroll
-        for (int r = 0; r < 8; ++r) reg[bB + fq(16 * r)] = x[r];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = reg[bC + fq(2 * r)];
+        q_xpose_bc(x, (L >> 1) & 1);
         // BSK ring head, in flight across phase C and the digit swap
         constexpr int QR = 4;
         cplx Bq0[QR], Bq1[QR];
@@ -252,12 +304,8 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         q_dit<0>(x, s_w, tpos(256 * (L & 1)));
         q_dit<1>(x, s_w, tpos(128 * (L & 1)));
         q_dit<2>(x, s_w, tpos(64 * (L & 1)));
+        q_xpose_bc(x, (L >> 1) & 1);
         __syncthreads();  // the other polynomial's waves have read this wave's digits
-#pragma unroll
-        for (int r = 0; r < 8; ++r) reg[bC + fq(2 * r)] = x[r];
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = reg[bB + fq(16 * r)];
         q_dit<0>(x, s_w, tpos(32 * (L & 15)));
         q_dit<1>(x, s_w, tpos(16 * (L & 15)));
         q_dit<2>(x, s_w, tpos(8 * (L & 15)));
