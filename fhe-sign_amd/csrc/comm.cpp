@@ -99,7 +99,14 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
         set_error("the root rank has no server key installed");
         return FHE_ERR_NO_KEY;
     }
-    if (c->engine) c->engine->flush();  // pending work of the old key runs first
+    if (c->engine) {
+        try {
+            c->engine->flush();  // pending work of the old key runs first
+        } catch (const std::exception& e) {
+            set_error(e.what());
+            return FHE_ERR_HIP;
+        }
+    }
     // parameters (a few words; also tells the receivers the buffer sizes)
     fhe_params hp = c->p.to_c();
     fhe_params* dp = nullptr;
