@@ -7,17 +7,18 @@
 // ciphertexts x 4 waves resident instead of 4 x 2: the CMUX chain is latency-bound and more
 // waves hide more of it.
 //
-// FFT index bits b9..b0 per phase (thread t = 64 h + L, register r = 0..7):
-//   A  idx = 128 r + t                                regs (b9 b8 b7)  DIF stages 0-2
-//   B  idx = 512 h + 256 L5 + 128 L4 + 16 r + (L&15)  regs (b6 b5 b4)  stages 3-5
-//   C  idx = 512 h + 16 (L>>1) + 2 r + (L&1)          regs (b3 b2 b1)  stages 6-8
+// FFT index bits b9..b0 per phase (thread t = 64 h + L, register r = 0..7, lane bits L5..L0):
+//   A  idx = 128 r + t                                   regs (b9 b8 b7), h = b6   DIF stages 0-2
+//   B  regs (b6 b5 b4), h = b9, lanes L5 L4 L3 = b3 b2 b1, L2 L1 = b8 b7, L0 = b0  stages 3-5
+//   C  regs (b3 b2 b1), h = b9, lanes L5 L4 L3 = b6 b5 b4, L2 L1 = b8 b7, L0 = b0  stages 6-8
 //   stage 9 pairs lanes L, L^1 (b0 = L0): DPP quad_perm, one signed add per value.
-// A<->B crosses the two waves of a polynomial (LDS + barrier).  B<->C keeps h and swaps register
-// bits (2,1,0) with lane bits (3,2,1) inside the wave: done in registers (bank-masked DPP moves for
-// lane bits 3,2, DPP row shifts + select for lane bit 1) -- the kernel is LDS-bound as much as
-// VALU-bound, and dropping those 16 LDS stores + 16 loads per CMUX beat the +320 VALU ops (71.3 ->
-// 70.5 ms per 8192).  The remaining LDS exchanges use one linear map fq (weights by
-// tools/lds_layout_quad*.py: A 1-way, B 1/2-way, C 2-way).
+// A<->B crosses the two waves of a polynomial (LDS + barrier).  B<->C swaps register bits (2,1,0)
+// with lane bits (5,4,3) inside the wave, in registers: v_permlane32_swap / v_permlane16_swap (one
+// instruction per dword pair) for lane bits 5,4 and a bank-masked DPP move for lane bit 3.  The
+// kernel is latency-bound: this took the B<->C exchange off LDS (16 stores + 16 loads and a round
+// trip per CMUX) and, with lanes chosen for the cheap swaps, cost 71.2 -> 66.7 ms per 8192 (the LDS
+// exchange: 71.3; lane bits 3,2,1 via DPP: 70.5).  The remaining LDS exchanges (A <-> B, the digit
+// swap) use one additive map fq, weights searched for these layouts (A 1-way, B 1.5, C 1.5).
 // The accumulator coefficients c = 128 r + t (r < 16) are the phase-A points j = 128 r + t and
 // j + 1024 of the folded transform; the BSK is stored in the phase-C layout (k_bsk_to_quad).
 #include "device_math.h"
@@ -26,7 +27,7 @@
 namespace fhe {
 
 namespace {
-constexpr int WQ[10] = {1, 2, 4, 8, 16, 34, 68, 135, 276, 548};
+constexpr int WQ[10] = {1, 2, 4, 8, 16, 32, 66, 132, 274, 541};
 constexpr int QX_SZ = 1093;  // complex entries per polynomial region (>= 1024 u64 pairs for the rotation)
 
 FHE_DEV constexpr int fq(int i) {
@@ -41,7 +42,7 @@ FHE_DEV constexpr int fq(int i) {
 constexpr int QTW_SZ = 512 + 16;
 // Zetas of the twisted forward transform that vary across lanes, in the order of
 // context.cpp:quad_zetas: stage 3 [B3], 4 [8 + B3], 5 [16 + 8j + B3], 6 [32 + B6], 7 [96 + B6],
-// 8 [160 + 64j + B6], 9 [288 + 64 r2 + 32 h + u] (B3 = 4h + (L >> 4), B6 = 32h + u, u = L >> 1, even
+// 8 [160 + 64j + B6], 9 [288 + 64 r2 + 32 h + u] (B3 = 4h + (b8 b7), B6 = 32h + u, u = (b8 .. b4), even
 // blocks only: odd ones are i times them), then 1 and -i (stage 9, lanes L0 = 0) and the uniform
 // zetas of stages 0-2 (read from global memory: Z[1], Z[2], Z[4], Z[6]).
 constexpr int QZ_LDS = 546, QZ_ONE = 544, QZ_MINUS_I = 545, QZ_UNIFORM = 546;
@@ -113,17 +114,17 @@ FHE_DEV void q_stage9(cplx (&x)[8], uint32_t signbit) {
         x[r] = make_double2(p.x + flip_if(x[r].x, signbit), p.y + flip_if(x[r].y, signbit));
     }
 }
-// ---- B <-> C as register transposes (no LDS): register bits (2,1,0) <-> lane bits (3,2,1)
+// ---- B <-> C as register transposes (no LDS): register bits (2,1,0) <-> lane bits (5,4,3)
 FHE_DEV void qsplit(double d, uint32_t& lo, uint32_t& hi) {
     const uint64_t b = (uint64_t)__double_as_longlong(d);
     lo = (uint32_t)b;
     hi = (uint32_t)(b >> 32);
 }
 FHE_DEV double qjoin(uint32_t lo, uint32_t hi) { return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)); }
-template <int K>  // lane bit K in {2, 3}: whole 4-lane DPP banks, one masked move per half
-FHE_DEV void qx_banked(cplx& X, cplx& Y) {
-    constexpr int SH = 1 << K;
-    constexpr int HI = K == 3 ? 0xC : 0xA, LO = K == 3 ? 0x3 : 0x5;
+// X holds register bit 0, Y register bit 1 of the pair; afterwards that register bit and lane bit K
+// are swapped.  K = 5, 4: v_permlane32_swap / v_permlane16_swap, one instruction per dword pair.
+template <int K>
+FHE_DEV void qx_permlane(cplx& X, cplx& Y) {
     uint32_t x[4], y[4];
     qsplit(X.x, x[0], x[1]);
     qsplit(X.y, x[2], x[3]);
@@ -131,16 +132,16 @@ FHE_DEV void qx_banked(cplx& X, cplx& Y) {
     qsplit(Y.y, y[2], y[3]);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)x[d], (int)y[d], 0x110 + SH, 0xF, HI, false);
-        const uint32_t ny = (uint32_t)__builtin_amdgcn_update_dpp((int)y[d], (int)x[d], 0x100 + SH, 0xF, LO, false);
-        x[d] = nx;
-        y[d] = ny;
+        auto r = K == 5 ? __builtin_amdgcn_permlane32_swap(x[d], y[d], false, false)
+                        : __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+        x[d] = r[0];
+        y[d] = r[1];
     }
     X = make_double2(qjoin(x[0], x[1]), qjoin(x[2], x[3]));
     Y = make_double2(qjoin(y[0], y[1]), qjoin(y[2], y[3]));
 }
-// lane bit 1: row shifts by 2 and a per-lane select
-FHE_DEV void qx_bit1(cplx& X, cplx& Y, bool hi) {
+// K = 3: lanes with lane bit 3 set are whole 4-lane DPP banks, one masked move per half
+FHE_DEV void qx_banked3(cplx& X, cplx& Y) {
     uint32_t x[4], y[4];
     qsplit(X.x, x[0], x[1]);
     qsplit(X.y, x[2], x[3]);
@@ -148,24 +149,22 @@ FHE_DEV void qx_bit1(cplx& X, cplx& Y, bool hi) {
     qsplit(Y.y, y[2], y[3]);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const uint32_t ys = (uint32_t)__builtin_amdgcn_mov_dpp((int)y[d], 0x112, 0xF, 0xF, false);  // row_shr:2
-        const uint32_t xs = (uint32_t)__builtin_amdgcn_mov_dpp((int)x[d], 0x102, 0xF, 0xF, false);  // row_shl:2
-        const uint32_t nx = hi ? ys : x[d];
-        const uint32_t ny = hi ? y[d] : xs;
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)x[d], (int)y[d], 0x118, 0xF, 0xC, false);
+        const uint32_t ny = (uint32_t)__builtin_amdgcn_update_dpp((int)y[d], (int)x[d], 0x108, 0xF, 0x3, false);
         x[d] = nx;
         y[d] = ny;
     }
     X = make_double2(qjoin(x[0], x[1]), qjoin(x[2], x[3]));
     Y = make_double2(qjoin(y[0], y[1]), qjoin(y[2], y[3]));
 }
-FHE_DEV void q_xpose_bc(cplx (&x)[8], bool l1) {
+FHE_DEV void q_xpose_bc(cplx (&x)[8]) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) qx_banked<3>(x[r], x[r + 4]);  // reg bit 2 <-> lane bit 3
+    for (int r = 0; r < 4; ++r) qx_permlane<5>(x[r], x[r + 4]);  // reg bit 2 <-> lane bit 5
 #pragma unroll
     for (int r = 0; r < 8; ++r)
-        if (!(r & 2)) qx_banked<2>(x[r], x[r + 2]);  // reg bit 1 <-> lane bit 2
+        if (!(r & 2)) qx_permlane<4>(x[r], x[r + 2]);  // reg bit 1 <-> lane bit 4
 #pragma unroll
-    for (int r = 0; r < 8; r += 2) qx_bit1(x[r], x[r + 1], l1);  // reg bit 0 <-> lane bit 1
+    for (int r = 0; r < 8; r += 2) qx_banked3(x[r], x[r + 1]);  // reg bit 0 <-> lane bit 3
 }
 }  // namespace
 
@@ -194,13 +193,18 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
     double* rot = reinterpret_cast<double*>(reg);
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
     const uint32_t sign9 = (uint32_t)(L & 1) << 31;
-    const int B3 = 4 * h + (L >> 4), B6 = 32 * h + (L >> 1);  // twisted-transform block bases of phases B, C
-    const int z9 = 288 + 32 * h + (L >> 1);                   // stage-9 zeta of this lane (r2 = 0)
+    // lane bits of phases B and C (see the layout table above): L5 L4 L3 = (b3 b2 b1) in B, (b6 b5 b4)
+    // in C; L2 L1 = b8 b7 and L0 = b0 in both
+    const int l0 = L & 1, l1 = (L >> 1) & 1, l2 = (L >> 2) & 1, l3 = (L >> 3) & 1, l4 = (L >> 4) & 1, l5 = (L >> 5) & 1;
+    const int u = 16 * l2 + 8 * l1 + 4 * l5 + 2 * l4 + l3;     // (b8 .. b4) in phase C
+    const int lowB = 8 * l5 + 4 * l4 + 2 * l3 + l0;              // (b3 .. b0) in phase B
+    const int B3 = 4 * h + 2 * l2 + l1, B6 = 32 * h + u;        // twisted-transform block bases of phases B, C
+    const int z9 = 288 + 32 * h + u;                             // stage-9 zeta of this lane (r2 = 0)
 
     // lane parts of the exchange addresses (register parts are compile-time constants)
     const int bA = fq(t);
-    const int bB = fq(512 * h + 256 * ((L >> 5) & 1) + 128 * ((L >> 4) & 1) + (L & 15));
-    const int bC = fq(512 * h + 16 * (L >> 1) + (L & 1));
+    const int bB = fq(512 * h + 256 * l2 + 128 * l1 + lowB);
+    const int bC = fq(512 * h + 16 * u + l0);
 
     double acc[16];  // coefficients 128 r + t (f64 torus representatives)
     {
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         q_ct<2>(x, s_z[B3], s_z[B3]);
         q_ct<1>(x, s_z[8 + B3], s_z[8 + B3]);
         q_ct<0>(x, s_z[16 + B3], s_z[24 + B3]);
-        q_xpose_bc(x, (L >> 1) & 1);
+        q_xpose_bc(x);
         // BSK ring head, in flight across phase C and the digit swap
         constexpr int QR = 4;
         cplx Bq0[QR], Bq1[QR];
@@ -304,11 +308,11 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         q_dit<0>(x, s_w, tpos(256 * (L & 1)));
         q_dit<1>(x, s_w, tpos(128 * (L & 1)));
         q_dit<2>(x, s_w, tpos(64 * (L & 1)));
-        q_xpose_bc(x, (L >> 1) & 1);
+        q_xpose_bc(x);
         __syncthreads();  // the other polynomial's waves have read this wave's digits
-        q_dit<0>(x, s_w, tpos(32 * (L & 15)));
-        q_dit<1>(x, s_w, tpos(16 * (L & 15)));
-        q_dit<2>(x, s_w, tpos(8 * (L & 15)));
+        q_dit<0>(x, s_w, tpos(32 * lowB));
+        q_dit<1>(x, s_w, tpos(16 * lowB));
+        q_dit<2>(x, s_w, tpos(8 * lowB));
         wave_sync();
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bB + fq(16 * r)] = x[r];
@@ -348,13 +352,15 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 }
 
 // Fourier BSK: blind-rotate layout (R = 4v + q, lane L' <-> idx = 4 (L' + 64 v) + q) -> quad layout
-// (h, r, L <-> idx = 512 h + 16 (L >> 1) + 2 r + (L & 1)), one workgroup per polynomial.
+// (h, r, L <-> idx = 512 h + 16 u + 2 r + L0 with u = (b8 .. b4) from the lane bits as in phase C),
+// one workgroup per polynomial.
 __global__ __launch_bounds__(256) void k_bsk_to_quad(const cplx* __restrict__ src, cplx* __restrict__ dst) {
     const cplx* s = src + (size_t)blockIdx.x * 1024;
     cplx* d = dst + (size_t)blockIdx.x * 1024;
     for (int k = threadIdx.x; k < 1024; k += 256) {
         const int hh = k >> 9, r = (k >> 6) & 7, L = k & 63;
-        const int idx = 512 * hh + 16 * (L >> 1) + 2 * r + (L & 1);
+        const int u = 16 * ((L >> 2) & 1) + 8 * ((L >> 1) & 1) + 4 * ((L >> 5) & 1) + 2 * ((L >> 4) & 1) + ((L >> 3) & 1);
+        const int idx = 512 * hh + 16 * u + 2 * r + (L & 1);
         const int q = idx & 3, Lp = (idx >> 2) & 63, v = idx >> 8;
         d[k] = s[(4 * v + q) * 64 + Lp];
     }
