@@ -104,14 +104,30 @@ FHE_DEV double dpp_swap1(double v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), 0xB1, 0xF, 0xF, false);
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-FHE_DEV double flip_if(double v, uint32_t signbit) {
-    return __longlong_as_double((long long)((uint64_t)__double_as_longlong(v) ^ ((uint64_t)signbit << 32)));
+// partner + sgn * x with sgn = +1 (L0 = 0) or -1 (L0 = 1): one exact-product fma, identical to the
+// add of +-x.  sgn is rebuilt from the lane id at each use (volatile: not hoisted and kept live
+// across the CMUX loop, where the kernel has no register left for it).
+FHE_DEV double q_sgn9() {
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const uint32_t hi = 0x3FF00000u | (lane << 31);
+    return __longlong_as_double((long long)((uint64_t)hi << 32));
 }
-FHE_DEV void q_stage9(cplx (&x)[8], uint32_t signbit) {
+// The accumulator (and the rotation region) hold the torus representatives times 2^-41: every
+// operation on them is an exact power-of-two rescaling of device_math.h's tor_red / tor_digit<23>
+// (no value comes near the subnormal range), so results are bit-identical, and the digit needs no
+// scaling multiply.  The untwist factors carry the 2^-41 (context.cpp:quad_tables).
+FHE_DEV double tor_red_s(double v) { return __fma_rn(-0x1p23, __builtin_rint(v * 0x1p-23), v); }
+FHE_DEV double tor_digit_s(double v) {
+    const double g = __builtin_rint(v);
+    return __fma_rn(-0x1p23, __builtin_rint(g * 0x1p-23), g);
+}
+FHE_DEV void q_stage9(cplx (&x)[8]) {
+    const double sgn = q_sgn9();
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         const cplx p = make_double2(dpp_swap1(x[r].x), dpp_swap1(x[r].y));
-        x[r] = make_double2(p.x + flip_if(x[r].x, signbit), p.y + flip_if(x[r].y, signbit));
+        x[r] = make_double2(__fma_rn(sgn, x[r].x, p.x), __fma_rn(sgn, x[r].y, p.y));
     }
 }
 // ---- B <-> C as register transposes (no LDS): register bits (2,1,0) <-> lane bits (5,4,3)
@@ -169,7 +185,8 @@ FHE_DEV void q_xpose_bc(cplx (&x)[8]) {
 }  // namespace
 
 // One workgroup (4 waves) per ciphertext.  W = twiddles W[0..512), ps = [2][8][128]: twist factors
-// psi, then the untwist factors (psi.x 2^-10, -psi.y 2^-10) -- exact scalings, as the oracle's.
+// psi, then the untwist factors (psi.x 2^-51, -psi.y 2^-51): the oracle's 2^-10 and the accumulator's
+// 2^-41, exact scalings.
 __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
                                                               const uint32_t* __restrict__ lut_idx,
@@ -192,7 +209,6 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
     const cplx* other = s_x[p ^ 1];
     double* rot = reinterpret_cast<double*>(reg);
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
-    const uint32_t sign9 = (uint32_t)(L & 1) << 31;
     // lane bits of phases B and C (see the layout table above): L5 L4 L3 = (b3 b2 b1) in B, (b6 b5 b4)
     // in C; L2 L1 = b8 b7 and L0 = b0 in both
     const int l0 = L & 1, l1 = (L >> 1) & 1, l2 = (L >> 2) & 1, l3 = (L >> 3) & 1, l4 = (L >> 4) & 1, l5 = (L >> 5) & 1;
@@ -218,7 +234,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
                 const uint32_t u = (uint32_t)(128 * r + t - rotb) & 4095u;
                 v = neg_if((double)(int64_t)lut[u & 2047u], (u >> 11) << 31);
             }
-            acc[r] = v;
+            acc[r] = v * 0x1p-41;  // accumulator kept in units of 2^41 (exact scaling, see tor_*_s)
         }
     }
 
@@ -242,7 +258,12 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t u = (uint32_t)(128 * r + t - (int)a) & 4095u;
-            dg[r] = tor_digit<23>(neg_if(rot[u & 2047u], (u >> 11) << 31) - acc[r]);
+            // negate by u's bit 11: adding it at bit 31 of the high word is the sign flip (2 ops)
+            const uint64_t vb = (uint64_t)__double_as_longlong(rot[u & 2047u]);
+            uint32_t vh;
+            asm("v_lshl_add_u32 %0, %1, 20, %2" : "=v"(vh) : "v"(u & 2048u), "v"((uint32_t)(vb >> 32)));
+            const double v = __longlong_as_double((long long)(((uint64_t)vh << 32) | (uint32_t)vb));
+            dg[r] = tor_digit_s(v - acc[r]);
         }
         __syncthreads();  // every rotation read done before the region is reused
         cplx x[8];
@@ -285,7 +306,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
             x[2 * r2] = cmul(x[2 * r2], s_z[ia]);
             x[2 * r2 + 1] = cmul(x[2 * r2 + 1], mul_i(s_z[ib]));
         }
-        q_stage9(x, sign9);
+        q_stage9(x);
 
         // ---- swap Fourier digits with the other polynomial's wave of the same half, MAC with BSK
         wave_sync();
@@ -304,7 +325,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         }
 
         // ---- inverse FFT: stage 9 and phase C in registers, then the region again
-        q_stage9(x, sign9);
+        q_stage9(x);
         q_dit<0>(x, s_w, tpos(256 * (L & 1)));
         q_dit<1>(x, s_w, tpos(128 * (L & 1)));
         q_dit<2>(x, s_w, tpos(64 * (L & 1)));
@@ -320,7 +341,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bA + fq(128 * r)];
         __syncthreads();  // every B->A read done before the next rotation overwrites the region
-        cplx pst[8];  // untwist factors conj(psi) 2^-10
+        cplx pst[8];  // untwist factors conj(psi) 2^-51
 #pragma unroll
         for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
         q_dit<0>(x, s_w, tpos(4 * t));
@@ -331,8 +352,8 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const cplx y = cmul(x[r], pst[r]);
-            acc[r] = tor_red(acc[r] + y.x);
-            acc[r + 8] = tor_red(acc[r + 8] + y.y);
+            acc[r] = tor_red_s(acc[r] + y.x);
+            acc[r + 8] = tor_red_s(acc[r + 8] + y.y);
         }
     }
 
@@ -342,12 +363,12 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int j = 128 * r + t;
-            const uint64_t v = f64_to_torus(acc[r]);
+            const uint64_t v = f64_to_torus(acc[r] * 0x1p41);
             if (j == 0) o[0] = v;
             else o[2048 - j] = 0ull - v;
         }
     } else if (t == 0) {
-        o[2048] = f64_to_torus(acc[0]);
+        o[2048] = f64_to_torus(acc[0] * 0x1p41);
     }
 }
 

@@ -108,7 +108,8 @@ void quad_tables(const std::vector<double2>& W, const std::vector<double2>& psi,
         for (int r = 0; r < 8; ++r) {
             const double2 q = psi[128 * r + t];
             (*ps)[r * 128 + t] = q;
-            (*ps)[1024 + r * 128 + t] = make_double2(q.x * 0.0009765625, -q.y * 0.0009765625);
+            // untwist conj(psi) 2^-10, times the quad accumulator's 2^-41 scale (br_quad.hip: tor_red_s)
+            (*ps)[1024 + r * 128 + t] = make_double2(std::ldexp(q.x, -51), -std::ldexp(q.y, -51));
         }
 }
 
