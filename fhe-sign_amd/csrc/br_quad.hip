@@ -113,15 +113,7 @@ FHE_DEV double q_sgn9() {
     const uint32_t hi = 0x3FF00000u | (lane << 31);
     return __longlong_as_double((long long)((uint64_t)hi << 32));
 }
-// The accumulator (and the rotation region) hold the torus representatives times 2^-41: every
-// operation on them is an exact power-of-two rescaling of device_math.h's tor_red / tor_digit<23>
-// (no value comes near the subnormal range), so results are bit-identical, and the digit needs no
-// scaling multiply.  The untwist factors carry the 2^-41 (context.cpp:quad_tables).
-FHE_DEV double tor_red_s(double v) { return __fma_rn(-0x1p23, __builtin_rint(v * 0x1p-23), v); }
-FHE_DEV double tor_digit_s(double v) {
-    const double g = __builtin_rint(v);
-    return __fma_rn(-0x1p23, __builtin_rint(g * 0x1p-23), g);
-}
+// The accumulator is kept in units of 2^41 (device_math.h: tor_red_s, tor_digit_s).
 FHE_DEV void q_stage9(cplx (&x)[8]) {
     const double sgn = q_sgn9();
 #pragma unroll
@@ -258,12 +250,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t u = (uint32_t)(128 * r + t - (int)a) & 4095u;
-            // negate by u's bit 11: adding it at bit 31 of the high word is the sign flip (2 ops)
-            const uint64_t vb = (uint64_t)__double_as_longlong(rot[u & 2047u]);
-            uint32_t vh;
-            asm("v_lshl_add_u32 %0, %1, 20, %2" : "=v"(vh) : "v"(u & 2048u), "v"((uint32_t)(vb >> 32)));
-            const double v = __longlong_as_double((long long)(((uint64_t)vh << 32) | (uint32_t)vb));
-            dg[r] = tor_digit_s(v - acc[r]);
+            dg[r] = tor_digit_s(neg_bit11(rot[u & 2047u], u) - acc[r]);
         }
         __syncthreads();  // every rotation read done before the region is reused
         cplx x[8];

@@ -177,10 +177,10 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
     for (int s = 0; s < 10; ++s) ZT[s] = zw[s * 256 + t];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) PS[r] = psiw[r * 256 + t];
+    for (int r = 0; r < 4; ++r) PS[r] = make_double2(psiw[r * 256 + t].x * 0x1p-51, -psiw[r * 256 + t].y * 0x1p-51);
 
     // accumulator: coefficient c = 256 r' + 4 L + q, r' = 0..7
-    double acc[8];  // f64 torus representatives
+    double acc[8];  // f64 torus representatives times 2^-41 (tor_red_s / tor_digit_s)
     {
         const uint32_t bt = modswitch_2n(a_ct[n]);
         const int rot = (int)((4096u - bt) & 4095u);
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 const uint32_t u = (uint32_t)(256 * r + 4 * L + q - rot) & 4095u;
                 v = neg_if((double)(int64_t)lut[u & 2047u], (u >> 11) << 31);
             }
-            acc[r] = v;
+            acc[r] = v * 0x1p-41;
         }
     }
     double* rot_me = s_rot[p];
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 const int rr = r + 4 * hh;
                 const uint32_t u = (uint32_t)(256 * rr + 4 * L + q - (int)a) & 4095u;
                 const uint32_t c = u & 2047u;
-                d2[hh] = tor_digit<23>(neg_if(rot_me[c + (c >> 2)], (u >> 11) << 31) - acc[rr]);
+                d2[hh] = tor_digit_s(neg_bit11(rot_me[c + (c >> 2)], u) - acc[rr]);
             }
             x[r] = make_double2(d2[0], d2[1]);
         }
@@ -306,10 +306,9 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         // ---- untwist, accumulate (x[r] = idx 256 r + 4 L + q -> coefs idx, idx + 1024)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const cplx u = make_double2(PS[r].x * 0.0009765625, -PS[r].y * 0.0009765625);
-            const cplx y = cmul(x[r], u);
-            acc[r] = tor_red(acc[r] + y.x);
-            acc[r + 4] = tor_red(acc[r + 4] + y.y);
+            const cplx y = cmul(x[r], PS[r]);  // conj(psi) 2^-10, times the accumulator's 2^-41
+            acc[r] = tor_red_s(acc[r] + y.x);
+            acc[r + 4] = tor_red_s(acc[r + 4] + y.y);
         }
     }
 
@@ -319,12 +318,12 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int j = 256 * r + 4 * L + q;
-            const uint64_t v = f64_to_torus(acc[r]);
+            const uint64_t v = f64_to_torus(acc[r] * 0x1p41);
             if (j == 0) o[0] = v;
             else o[2048 - j] = 0ull - v;
         }
     } else if (t == 0) {
-        o[2048] = f64_to_torus(acc[0]);
+        o[2048] = f64_to_torus(acc[0] * 0x1p41);
     }
 }
 

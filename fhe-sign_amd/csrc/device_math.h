@@ -92,6 +92,23 @@ FHE_DEV double tor_digit(double v) {
     const double g = __builtin_rint(v * down);
     return __fma_rn(-base, __builtin_rint(g * ibase), g);
 }
+// The blind-rotation kernels keep the accumulator (and the rotation region) in units of 2^41: every
+// operation on it is then an exact power-of-two rescaling of tor_red / tor_digit<23> above (no value
+// comes near the subnormal range), so results are bit-identical while the digit needs no scaling
+// multiply.  The untwist factors carry the 2^-41; sample extraction multiplies by 2^41.
+FHE_DEV double tor_red_s(double v) { return __fma_rn(-0x1p23, __builtin_rint(v * 0x1p-23), v); }
+FHE_DEV double tor_digit_s(double v) {
+    const double g = __builtin_rint(v);
+    return __fma_rn(-0x1p23, __builtin_rint(g * 0x1p-23), g);
+}
+// -v if bit 11 of u is set (negacyclic wrap of a rotation index): bit 11 added at bit 31 of the high
+// word flips the sign (v_and + v_lshl_add; the compiler's own form of the xor takes three ops)
+FHE_DEV double neg_bit11(double v, uint32_t u) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    uint32_t hi;
+    asm("v_lshl_add_u32 %0, %1, 20, %2" : "=v"(hi) : "v"(u & 2048u), "v"((uint32_t)(b >> 32)));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint32_t)b));
+}
 // v or -v by a lane bit (negbit = 0 or 1 << 31 applied to the high word): exact, one VALU op
 FHE_DEV double neg_if(double v, uint32_t negbit) {
     const uint64_t b = (uint64_t)__double_as_longlong(v) ^ ((uint64_t)negbit << 32);
