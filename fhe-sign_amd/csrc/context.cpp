@@ -4,8 +4,10 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 
 #include "kernels.h"
+#include "keygen.h"
 #include "radix.h"
 
 namespace fhe {
@@ -300,6 +302,66 @@ int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** 
         set_error(std::string("keygen failed: ") + e.what());
         return FHE_ERR_ALLOC;
     }
+    return FHE_OK;
+}
+
+int fhe_generate_keys_device(fhe_ctx* c, const fhe_params* params, uint64_t seed, fhe_client_key** ck,
+                             fhe_server_key** sk) {
+    if (!c || !params || !ck || !sk) {
+        set_error("null argument");
+        return FHE_ERR_INVALID;
+    }
+    Params p;
+    const char* why = nullptr;
+    if (!Params::from_c(*params, &p, &why)) {
+        set_error(why);
+        return FHE_ERR_UNSUPPORTED;
+    }
+    std::unique_ptr<fhe_client_key> cko;
+    std::unique_ptr<fhe_server_key> sko;
+    try {
+        cko.reset(new fhe_client_key());
+        sko.reset(new fhe_server_key());
+        generate_secret_keys(p, seed, cko.get());
+        sko->params = p;
+        sko->ksk.resize((size_t)kPolySize * p.ks_level * (p.n + 1));
+        sko->bsk.resize((size_t)p.n * 4 * kPolySize);
+    } catch (const std::exception& e) {
+        set_error(std::string("keygen failed: ") + e.what());
+        return FHE_ERR_ALLOC;
+    }
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    const size_t kw = sko->ksk.size(), bw = sko->bsk.size();
+    uint64_t *d_ksk = nullptr, *d_bsk = nullptr, *d_lwe = nullptr, *d_glwe = nullptr;
+    auto release = [&] {
+        for (uint64_t* q : {d_ksk, d_bsk, d_lwe, d_glwe})
+            if (q) (void)hipFree(q);
+    };
+    hipError_t e = hipSuccess;
+    auto step = [&](hipError_t r) {
+        if (e == hipSuccess && r != hipSuccess) e = r;
+        return e == hipSuccess;
+    };
+    step(hipMalloc(&d_ksk, kw * 8)) && step(hipMalloc(&d_bsk, bw * 8)) && step(hipMalloc(&d_lwe, p.n * 8)) &&
+        step(hipMalloc(&d_glwe, kPolySize * 8)) &&
+        step(hipMemcpyAsync(d_lwe, cko->lwe_sk.data(), p.n * 8, hipMemcpyHostToDevice, c->stream)) &&
+        step(hipMemcpyAsync(d_glwe, cko->glwe_sk.data(), kPolySize * 8, hipMemcpyHostToDevice, c->stream)) &&
+        step(launch_chacha_u64(chacha_stream_key(seed, kStreamKsk), d_ksk, kw, c->stream)) &&
+        step(launch_ksk_bodies(d_ksk, d_lwe, d_glwe, (int)p.n, (int)(kPolySize * p.ks_level), (int)p.ks_level,
+                               (int)p.ks_base_log, (int)p.lwe_noise_log2, c->stream)) &&
+        step(launch_chacha_u64(chacha_stream_key(seed, kStreamBsk), d_bsk, bw, c->stream)) &&
+        step(launch_bsk_bodies(d_bsk, d_lwe, d_glwe, (int)p.n, (int)p.pbs_base_log, (int)p.glwe_noise_log2,
+                               c->stream)) &&
+        step(hipMemcpyAsync(sko->ksk.data(), d_ksk, kw * 8, hipMemcpyDeviceToHost, c->stream)) &&
+        step(hipMemcpyAsync(sko->bsk.data(), d_bsk, bw * 8, hipMemcpyDeviceToHost, c->stream)) &&
+        step(hipStreamSynchronize(c->stream));
+    release();
+    if (e != hipSuccess) {
+        set_error(std::string("device keygen: ") + hipGetErrorString(e));
+        return FHE_ERR_HIP;
+    }
+    *ck = cko.release();
+    *sk = sko.release();
     return FHE_OK;
 }
 

@@ -167,18 +167,22 @@ static void negacyclic_binary_mac(uint64_t* r, const uint64_t* a, const uint64_t
     }
 }
 
-void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_server_key* sk) {
-    const uint32_t n = p.n, N = kPolySize, L = p.ks_level;
+void generate_secret_keys(const Params& p, uint64_t seed, fhe_client_key* ck) {
     ck->params = p;
-    sk->params = p;
-    ck->lwe_sk.assign(n, 0);
-    ck->glwe_sk.assign(N, 0);
+    ck->lwe_sk.assign(p.n, 0);
+    ck->glwe_sk.assign(kPolySize, 0);
     {
         ChaChaStream r(seed, kStreamSecret);
         for (auto& v : ck->lwe_sk) v = r.next_u64() & 1ull;
         for (auto& v : ck->glwe_sk) v = r.next_u64() & 1ull;
     }
     ck->enc_rng.reset(seed, kStreamEncrypt);
+}
+
+void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_server_key* sk) {
+    const uint32_t n = p.n, N = kPolySize, L = p.ks_level;
+    sk->params = p;
+    generate_secret_keys(p, seed, ck);
 
     // KSK[j][l] = LWE_{lwe_sk}( S_j * 2^(64 - base_log*(l+1)) )
     sk->ksk.assign((size_t)N * L * (n + 1), 0);

@@ -80,6 +80,9 @@ struct fhe_server_key {
 
 namespace fhe {
 void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_server_key* sk);
+// the client-key half of generate_keys (secret keys, encryption stream); the device keygen
+// (context.cpp: fhe_generate_keys_device) uses it and derives the server key on the GPU
+void generate_secret_keys(const Params& p, uint64_t seed, fhe_client_key* ck);
 void encrypt_big(fhe_client_key* ck, uint64_t plaintext, uint64_t* ct);
 // n encryptions (plaintexts already scaled), outputs and stream state identical to n encrypt_big
 // calls; large batches run on several host threads over seeked copies of the stream

@@ -30,6 +30,8 @@ _SIGNATURES = [
     ("fhe_last_error", C.c_char_p, []),
     ("fhe_params_default", C.c_int, [C.POINTER(FheParams)]),
     ("fhe_generate_keys", C.c_int, [C.POINTER(FheParams), C.c_uint64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    ("fhe_generate_keys_device", C.c_int,
+     [C.c_void_p, C.POINTER(FheParams), C.c_uint64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     ("fhe_client_key_destroy", None, [C.c_void_p]),
     ("fhe_server_key_destroy", None, [C.c_void_p]),
     ("fhe_client_key_export", C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),

@@ -112,11 +112,16 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
-def generate_keys(params: FheParams | None = None, seed: int = 0):
-    """tfhe::generate_keys(ConfigBuilder::default().build()) -- src/schnorr.rs:441-442."""
+def generate_keys(params: FheParams | None = None, seed: int = 0, device: "Context | None" = None):
+    """tfhe::generate_keys(ConfigBuilder::default().build()) -- src/schnorr.rs:441-442.
+    With `device` (a Context), the server key is generated on that GPU: identical key words
+    (fhe_generate_keys_device); the key is returned, not installed."""
     p = params or default_params()
     ck, sk = C.c_void_p(), C.c_void_p()
-    check(load().fhe_generate_keys(C.byref(p), seed, C.byref(ck), C.byref(sk)))
+    if device is None:
+        check(load().fhe_generate_keys(C.byref(p), seed, C.byref(ck), C.byref(sk)))
+    else:
+        check(load().fhe_generate_keys_device(device.handle, C.byref(p), seed, C.byref(ck), C.byref(sk)))
     return ClientKey(ck, p), ServerKey(sk, p)
 
 

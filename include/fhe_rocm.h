@@ -62,6 +62,12 @@ int fhe_params_default(fhe_params* out);
  * src/perf_test.rs:12).  Deterministic in `seed` (ChaCha20 streams). */
 int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** client_key,
                       fhe_server_key** server_key);
+/* The same keys (identical words) generated on the GPU of `ctx` (keygen
+ * dominates setup).  The ChaCha streams are counter-indexed, so the host's sequential draws become
+ * one stream block per thread; the key is downloaded into the returned handle and not installed
+ * (call fhe_set_server_key as after fhe_generate_keys).  ctx needs no server key. */
+int fhe_generate_keys_device(fhe_ctx* ctx, const fhe_params* params, uint64_t seed,
+                             fhe_client_key** client_key, fhe_server_key** server_key);
 void fhe_client_key_destroy(fhe_client_key* ck);
 void fhe_server_key_destroy(fhe_server_key* sk);
 /* The parameter set a key was generated for (e.g. after deserialization). */
