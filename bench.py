@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import threading
 import os
 import sys
 import time
@@ -174,6 +175,26 @@ def ops_legs(ck, ctx, seed):
     return out
 
 
+FANOUT_DEADLINE_S = 180.0
+
+
+def with_deadline(fn, seconds):
+    """fn() on a daemon thread: (result, timed_out).  The fan-out legs are the only part of the N > 1
+    run that depends on RCCL between GPUs; if they hang, the measured line is still printed."""
+    box = {}
+
+    def run():
+        try:
+            box["r"] = fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the line
+            box["r"] = {"error": str(e)}
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(seconds)
+    return box.get("r"), th.is_alive()
+
+
 def fanout_legs(ck, ctx, dist, rank, world, seed):
     """config 5 / SURVEY.md 8e: ONE 256-bit mul and ONE sign fanned across all ranks (levels of at
     least FANOUT_MIN bootstraps split over the GPUs, outputs all-gathered with RCCL).  Identical
@@ -304,7 +325,11 @@ def main():
         # every rank signs its own batch of 8 (config 5b): whole-job signatures per second
         b8 = ops["sign_fhe_with_k0_batch8_compat"]
         b8["signs_per_s"] = world * 8 / b8["seconds"]
-    fan = fanout_legs(ck, ctx, dist, rank, world, a.seed) if (world > 1 and not a.no_ops) else None
+    fan, fan_hung = None, False
+    if world > 1 and not a.no_ops:
+        fan, fan_hung = with_deadline(lambda: fanout_legs(ck, ctx, dist, rank, world, a.seed), FANOUT_DEADLINE_S)
+        if fan_hung:
+            fan = {"ranks": world, "error": f"fan-out legs exceeded {FANOUT_DEADLINE_S:.0f} s; abandoned"}
 
     total = world * B * a.steps
     br_ms = float(np.mean(br_t))
@@ -369,6 +394,9 @@ def main():
         res["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
+    if fan_hung:  # a collective of the abandoned legs may still hold the stream: no orderly teardown
+        sys.stdout.flush()
+        os._exit(0)
     ctx.free(d_in)
     ctx.free(d_out)
     ctx.free(d_lut)

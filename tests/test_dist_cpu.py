@@ -150,3 +150,21 @@ def test_server_key_replication_world2():
     one, no rank enters the collective and all report failure (nobody waits alone)."""
     assert _run_replicate(True) == [(0, True, [0]), (1, True, [0])]
     assert [(r, ok, b) for r, ok, b in _run_replicate(False)] == [(0, False, []), (1, False, [])]
+
+
+def test_fanout_deadline_guard():
+    """bench.py's N > 1 fan-out legs run under a deadline: a hung leg is abandoned, not waited on."""
+    import importlib.util
+    import threading
+    import time
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.with_deadline(lambda: {"ok": 1}, 5.0) == ({"ok": 1}, False)
+    r, hung = bench.with_deadline(lambda: 1 / 0, 5.0)
+    assert not hung and "error" in r
+    stop = threading.Event()
+    t = time.perf_counter()
+    r, hung = bench.with_deadline(lambda: stop.wait(30), 0.2)
+    assert hung and r is None and time.perf_counter() - t < 5
+    stop.set()
