@@ -246,12 +246,16 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) rot[128 * r + t] = acc[r];
         __syncthreads();
-        double dg[16];  // digits of X^a acc - acc, decomposed as the rotated words arrive
+        double dg[16];  // digits of X^a acc - acc (all 16 rotated reads issued before the first use)
+        double rv[16];
+        uint32_t uu[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const uint32_t u = (uint32_t)(128 * r + t - (int)a) & 4095u;
-            dg[r] = tor_digit_s(neg_bit11(rot[u & 2047u], u) - acc[r]);
+            uu[r] = (uint32_t)(128 * r + t - (int)a) & 4095u;
+            rv[r] = rot[uu[r] & 2047u];
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dg[r] = tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]);
         __syncthreads();  // every rotation read done before the region is reused
         cplx x[8];
 #pragma unroll
