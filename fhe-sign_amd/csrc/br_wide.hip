@@ -228,18 +228,18 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         }
         __syncthreads();
         cplx x[4];
+        double rv[8];  // all 8 rotated reads issued before the first use
+        uint32_t uu[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            double d2[2];
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int rr = r + 4 * hh;
-                const uint32_t u = (uint32_t)(256 * rr + 4 * L + q - (int)a) & 4095u;
-                const uint32_t c = u & 2047u;
-                d2[hh] = tor_digit_s(neg_bit11(rot_me[c + (c >> 2)], u) - acc[rr]);
-            }
-            x[r] = make_double2(d2[0], d2[1]);
+        for (int rr = 0; rr < 8; ++rr) {
+            uu[rr] = (uint32_t)(256 * rr + 4 * L + q - (int)a) & 4095u;
+            const uint32_t c = uu[rr] & 2047u;
+            rv[rr] = rot_me[c + (c >> 2)];
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            x[r] = make_double2(tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]),
+                                tor_digit_s(neg_bit11(rv[r + 4], uu[r + 4]) - acc[r + 4]));
 
         // ---- forward transform (twisted: no twist multiply): A (stages 0,1) -> B -> C -> D
         // (wave-private) -> E (cross-wave)
