@@ -29,6 +29,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds @1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6        # MI355X dense FP64 peak (matrix = vector on gfx950), spec
+FP64_PEAK_MEASURED_TFLOPS = 65.0  # dependent-free v_fma_f64 stream on the GPU box (tools/fp64_peak.hip)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "r1w_pmc_summary.json")  # tools/profile_round.sh
 FANOUT_MIN = 257  # levels with at least this many bootstraps are split over the GPUs (fan-out legs)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -71,10 +72,26 @@ def allmax(dist, x: float) -> float:
     return float(t.item())
 
 
+def host_cores():
+    """(threads to use, description): every CPU this process may run on (sched_getaffinity), capped by
+    the cgroup CPU quota when one is set (on the GPU box the affinity mask can show the whole
+    machine while the container's share is smaller); nproc reported beside it."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(round(quota))))
+    return threads, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(seed, target_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, info = host_cores()
     ok = oracle.OracleKeys(seed)
     lut = ok.make_lut([(m + 1) % 16 for m in range(16)])[None, :]
     r = ok.rng(3)
@@ -89,9 +106,10 @@ def cpu_baseline(seed, target_s):
     t0 = time.perf_counter()
     ok.pbs_batch(cts, lut, np.zeros(count, np.uint32), threads)
     dt = time.perf_counter() - t0
-    return {"value": count / dt, "unit": "PBS/s", "cores": threads, "kind": "port",
-            "sample": f"{count} PBS (KS+BR+SE, same params/keys shape) with the C oracle, "
-                      f"OpenMP {threads} threads, {dt:.1f} s"}
+    return {"value": count / dt, "unit": "PBS/s", "cores": threads, "kind": "port", **info,
+            "sample": f"{count} PBS (KS+BR+SE, same params/keys shape) with the C oracle (bit-exact "
+                      f"restatement, not a tuned CPU path), OpenMP {threads} threads = every CPU of "
+                      f"this process's affinity/cgroup share, {dt:.1f} s"}
 
 
 def pmc_traffic(batch):
@@ -106,16 +124,24 @@ def pmc_traffic(batch):
         return None, None
 
 
+def golden_mul():
+    """(a, b, compat limbs) of the first committed 8x8-limb vector (tests/golden/biguint_vectors.json,
+    seeded 256-bit operands; `out` = the reference's limb loop src/biguint.rs:194-265, lost carries
+    included): the legs check results against committed data, never against oracle code."""
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "biguint_vectors.json")))["mul"][0]
+    val = lambda limbs: sum(int(x) << (32 * i) for i, x in enumerate(limbs))  # noqa: E731
+    return val(g["a"]), val(g["b"]), [int(x) for x in g["out"]]
+
+
 def ops_legs(ck, ctx, seed):
     """configs 2 and 4: BigUintFHE 256-bit mul wall-clock and sign_fhe_with_k0 seconds (every rank
     runs its own replica: the N-GPU line is the 'one sign per GPU' batch of configs[4])."""
     import random
-    from fhe_sign import (COMPAT, FAST, PUBLIC, BigUintFHE, FheUint32, FheUint256, Schnorr, compute_nonce, set_server_key,
-                          stats)
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from fhe_sign import (COMPAT, FAST, PUBLIC, BigUintFHE, FheUint8, FheUint32, FheUint256, Schnorr, compute_nonce,
+                          set_server_key, stats)
     set_server_key(ctx)
     rng = random.Random(seed)
-    a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(256) | 1 << 255
+    a, b, compat_limbs = golden_mul()
     A, B = BigUintFHE.new(a, ck), BigUintFHE.new(b, ck)
     out = {}
 
@@ -132,9 +158,7 @@ def ops_legs(ck, ctx, seed):
 
     A.add(B, FAST)  # warm-up (LUT registration, pools)
     A.mul(B, COMPAT).decrypt_limbs(ck)  # grows the block pool / staging buffers to their steady-state size
-    import ref_semantics as R
-    leg("biguint256_mul_compat", lambda: A.mul(B, COMPAT),
-        lambda r: r.decrypt_limbs(ck) == R.biguint_mul(R.to_u32_digits(a), R.to_u32_digits(b)))
+    leg("biguint256_mul_compat", lambda: A.mul(B, COMPAT), lambda r: r.decrypt_limbs(ck) == compat_limbs)
     leg("biguint256_mul_fast", lambda: A.mul(B, FAST), lambda r: r.to_biguint(ck) == a * b)
     leg("biguint256_add_fast", lambda: A.add(B, FAST), lambda r: r.to_biguint(ck) == a + b)
     # config 3: 256-bit radix / clear divisor (src/perf_test.rs:54 at 256 bits)
@@ -151,6 +175,21 @@ def ops_legs(ck, ctx, seed):
     leg("fheuint32_div5", lambda: X32 / 5, lambda r: r.decrypt(ck) == 268)
     leg("fheuint32_add", lambda: X32 + FheUint32.try_encrypt(5, ck), lambda r: r.decrypt(ck) == 1349)
     leg("fheuint32_mul", lambda: X32 * FheUint32.try_encrypt(5, ck), lambda r: r.decrypt(ck) == 6720)
+    # the rest of src/perf_test.rs:36-48 (README.md:110-113): 1344 >> Enc(5) = 42, cast to u8, min with
+    # Enc(7u8), & 1 -- each timed alone on its own inputs, like the reference's Instant pairs
+    B5 = FheUint32.try_encrypt(5, ck)
+    leg("fheuint32_shr_encrypted", lambda: X32 >> B5, lambda r: r.decrypt(ck) == 42)
+    # each leg's input is computed (and read back: the engine defers work until a host read) before
+    # its clock starts, so a leg times only its own operation
+    S42 = X32 >> B5
+    assert S42.decrypt(ck) == 42
+    leg("fheuint32_cast_u8", lambda: S42.cast_into(FheUint8), lambda r: r.decrypt(ck) == 42)
+    C8, C7 = S42.cast_into(FheUint8), FheUint8.try_encrypt(7, ck)
+    assert C8.decrypt(ck) == 42
+    leg("fheuint8_min", lambda: C8.min(C7), lambda r: r.decrypt(ck) == 7)
+    M7 = C8.min(C7)
+    assert M7.decrypt(ck) == 7
+    leg("fheuint8_and1", lambda: M7 & 1, lambda r: r.decrypt(ck) == 1)
     d, msg = 3, bytes(32)  # BIP-340 vector 0 (tests/golden/bip340_vectors.csv row 0)
     k0 = compute_nonce(d, msg, bytes(32))
     dF = BigUintFHE.new(d, ck)
@@ -176,6 +215,7 @@ def ops_legs(ck, ctx, seed):
 
 
 FANOUT_DEADLINE_S = 180.0
+FANOUT_HUNG_EXIT = 3
 
 
 def with_deadline(fn, seconds):
@@ -195,23 +235,28 @@ def with_deadline(fn, seconds):
     return box.get("r"), th.is_alive()
 
 
+def abandon(why):
+    """End a run whose watchdog abandoned a GPU leg: the JSON line (already printed) is kept, but the
+    process exits non-zero, so the run is recorded as failed -- never as a clean rc 0."""
+    sys.stdout.flush()
+    sys.stderr.write(f"bench: {why}; exiting with status {FANOUT_HUNG_EXIT}\n")
+    sys.stderr.flush()
+    os._exit(FANOUT_HUNG_EXIT)
+
+
 def fanout_legs(ck, ctx, dist, rank, world, seed):
     """config 5 / SURVEY.md 8e: ONE 256-bit mul and ONE sign fanned across all ranks (levels of at
     least FANOUT_MIN bootstraps split over the GPUs, outputs all-gathered with RCCL).  Identical
     inputs on every rank; a failure on any rank stops the fan-out legs on all of them."""
-    import random
     from fhe_sign import COMPAT, FAST, BigUintFHE, Schnorr, compute_nonce, set_server_key
     from fhe_sign.dist import all_ok, attach_fanout
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ref_semantics as R
     out = {"ranks": world, "min_level": FANOUT_MIN}
     ok, err = attach_fanout(ctx, dist, rank, world, min_level=FANOUT_MIN)
     if not ok:
         out["error"] = err
         return out
     set_server_key(ctx)
-    rng = random.Random(seed ^ 0xFA)
-    a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(256) | 1 << 255
+    a, b, compat_limbs = golden_mul()
     ck.seed_encryption(seed ^ 0x5EED, 100)  # every rank encrypts the same ciphertexts
     A, B = BigUintFHE.new(a, ck), BigUintFHE.new(b, ck)
     d, msg = 3, bytes(32)
@@ -222,8 +267,7 @@ def fanout_legs(ck, ctx, dist, rank, world, seed):
     legs = [
         ("warmup_add_fast", lambda: A.add(B, FAST), lambda r: r.to_biguint(ck) == a + b),
         ("biguint256_mul_fast", lambda: A.mul(B, FAST), lambda r: r.to_biguint(ck) == a * b),
-        ("biguint256_mul_compat", lambda: A.mul(B, COMPAT),
-         lambda r: r.decrypt_limbs(ck) == R.biguint_mul(R.to_u32_digits(a), R.to_u32_digits(b))),
+        ("biguint256_mul_compat", lambda: A.mul(B, COMPAT), lambda r: r.decrypt_limbs(ck) == compat_limbs),
         ("sign_fhe_with_k0_v0_compat", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT), lambda r: r == ref),
         ("sign_fhe_with_k0_v0_fast", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, FAST), lambda r: r == ref),
     ]
@@ -360,13 +404,15 @@ def main():
             "parallelism": f"replicas x{world}",
         },
         "roofline": {
-            "bound": "mfma",
+            "bound": "fp64_valu",
             "compute_pipe": "fp64 VALU (FFT butterflies; no dense contraction on the path)",
             "kernel": "k_blind_rotate_quad",
             "achieved": achieved,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS,
+            "peak_measured": FP64_PEAK_MEASURED_TFLOPS,
+            "frac_measured": achieved / FP64_PEAK_MEASURED_TFLOPS,
             "flops_per_pbs": n * FLOPS_PER_CMUX,
             "traffic": traffic,
             "traffic_source": traffic_src,
@@ -384,7 +430,8 @@ def main():
         # published reference CPU numbers for the same operations (README.md:104-114;
         # c5.24xlarge, likely a debug build) -- context only, not the headline metric
         readme = {"fheuint32_add": 25.965747001, "fheuint32_mul": 76.051254698, "fheuint32_div5": 1121.134781795,
-                  "sign_fhe_with_k0_v0_compat": 4269.0}
+                  "fheuint32_shr_encrypted": 45.566019345, "fheuint32_cast_u8": 135.023e-6,
+                  "fheuint8_min": 25.71097148, "fheuint8_and1": 6.418014644, "sign_fhe_with_k0_v0_compat": 4269.0}
         res["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
                                           "speedup": v / ops[k]["seconds"]} for k, v in readme.items() if k in ops}
     res["pcie_inclusive_pbs_per_s"] = pcie_rate * world  # per-rank host-buffer rate x ranks
@@ -395,8 +442,7 @@ def main():
     if rank == 0:
         print(json.dumps(res), flush=True)
     if fan_hung:  # a collective of the abandoned legs may still hold the stream: no orderly teardown
-        sys.stdout.flush()
-        os._exit(0)
+        abandon("fan-out legs hung")
     ctx.free(d_in)
     ctx.free(d_out)
     ctx.free(d_lut)

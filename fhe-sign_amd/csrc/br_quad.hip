@@ -37,7 +37,7 @@ FHE_DEV constexpr int fq(int i) {
 }
 
 // Twiddles W[k], k < 512, live in LDS at tpos(k) = k + k/32 (8.4 KB, <= 2-way conflicts for every
-// stage's lane pattern; tools/lds_layout_quad*.py).  Stage s of the transform uses W[lane part +
+// stage's lane pattern; the round-1 searches, tools/lds_layout_search.py method).  Stage s of the transform uses W[lane part +
 // step * (r mod 2^K)] with step 128 (K = 2) or 256 (K = 1): tpos of that is lane base + 132 / 264.
 constexpr int QTW_SZ = 512 + 16;
 // Zetas of the twisted forward transform that vary across lanes, in the order of

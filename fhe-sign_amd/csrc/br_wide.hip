@@ -151,6 +151,9 @@ FHE_DEV void dit2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
 }  // namespace
 
 // Per-thread twiddle table [12][256] (t = 64 q + L), built on the host (context.cpp:wide_twiddles).
+// Launch bounds: 512 threads, and HIP's second argument is the minimum number of WAVES PER SIMD
+// (amdgpu-waves-per-eu), not workgroups per CU: the 8 waves of the one workgroup a CU holds (144 KB
+// of LDS) are 2 per SIMD, which caps the kernel at 256 VGPRs.
 __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
                                                               const uint32_t* __restrict__ lut_idx,

@@ -6,7 +6,9 @@
 // boundaries (the carry-propagation rounds), never inside a bootstrap.
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "context.h"
 #include "radix.h"
@@ -19,6 +21,27 @@ int nccl_check(ncclResult_t r, const char* what) {
     if (r == ncclSuccess) return FHE_OK;
     set_error(std::string(what) + ": " + ncclGetErrorString(r));
     return FHE_ERR_HIP;
+}
+
+// The communicator is non-blocking (ncclConfig_t::blocking = 0): a call may return ncclInProgress
+// and completes in the background.  Poll its state until it settles or the deadline passes; on a
+// timeout the communicator is aborted, so a rank whose peer never arrived returns an error
+// instead of waiting forever inside the library.
+int nccl_settle(ncclComm_t comm, ncclResult_t r, const char* what, uint32_t timeout_ms, bool abort_on_timeout) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+            if (abort_on_timeout) (void)ncclCommAbort(comm);
+            set_error(std::string(what) + ": timed out after " + std::to_string(timeout_ms) +
+                      " ms (a peer rank never joined)");
+            return FHE_ERR_TIMEOUT;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t q = ncclCommGetAsyncError(comm, &st);
+        r = q != ncclSuccess ? q : st;
+    }
+    return nccl_check(r, what);
 }
 }  // namespace
 
@@ -34,8 +57,9 @@ int fhe_ctx::ensure_gather(size_t n) {
 
 int fhe_ctx::allgather(uint64_t* buf, size_t words) {
     if (!comm) return FHE_OK;  // emulated ranks already wrote every segment
-    return nccl_check(ncclAllGather(buf + (size_t)rank * words, buf, words, ncclUint64, (ncclComm_t)comm, stream),
-                      "ncclAllGather");
+    ncclComm_t cm = (ncclComm_t)comm;
+    return nccl_settle(cm, ncclAllGather(buf + (size_t)rank * words, buf, words, ncclUint64, cm, stream),
+                       "ncclAllGather", comm_timeout_ms, false);
 }
 
 void fhe_ctx::release_comm() {
@@ -60,19 +84,35 @@ int fhe_comm_unique_id(uint8_t id[FHE_COMM_ID_BYTES]) {
     return FHE_OK;
 }
 
-int fhe_ctx_attach_comm(fhe_ctx* c, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank) {
-    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return FHE_ERR_INVALID;
+int fhe_ctx_attach_comm_timeout(fhe_ctx* c, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank,
+                                uint32_t timeout_ms) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks || timeout_ms == 0) return FHE_ERR_INVALID;
     FHE_HIP_CHECK(hipSetDevice(c->device));
     c->release_comm();
     ncclUniqueId u;
     std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
     ncclComm_t comm = nullptr;
-    int rc = nccl_check(ncclCommInitRank(&comm, nranks, u, rank), "ncclCommInitRank");
-    if (rc) return rc;
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;  // the init returns at once; nccl_settle waits for it against the deadline
+    const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        if (comm) (void)ncclCommAbort(comm);
+        return nccl_check(r, "ncclCommInitRankConfig");
+    }
+    const int rc = nccl_settle(comm, r, "ncclCommInitRankConfig", timeout_ms, true);
+    if (rc) {
+        if (rc != FHE_ERR_TIMEOUT && comm) (void)ncclCommAbort(comm);
+        return rc;
+    }
     c->comm = comm;
     c->nranks = nranks;
     c->rank = rank;
+    c->comm_timeout_ms = timeout_ms;
     return FHE_OK;
+}
+
+int fhe_ctx_attach_comm(fhe_ctx* c, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank) {
+    return fhe_ctx_attach_comm_timeout(c, id, nranks, rank, FHE_COMM_DEFAULT_TIMEOUT_MS);
 }
 
 int fhe_ctx_detach_comm(fhe_ctx* c) {
@@ -107,12 +147,15 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
             return FHE_ERR_HIP;
         }
     }
+    const uint32_t tmo = c->comm_timeout_ms;
     // parameters (a few words; also tells the receivers the buffer sizes)
     fhe_params hp = c->p.to_c();
     fhe_params* dp = nullptr;
     FHE_HIP_CHECK(hipMalloc(&dp, sizeof(fhe_params)));
-    FHE_HIP_CHECK(hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, c->stream));
-    int rc = nccl_check(ncclBroadcast(dp, dp, sizeof(fhe_params), ncclUint8, root, comm, c->stream), "ncclBroadcast");
+    int rc = hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc)
+        rc = nccl_settle(comm, ncclBroadcast(dp, dp, sizeof(fhe_params), ncclUint8, root, comm, c->stream),
+                         "ncclBroadcast", tmo, false);
     if (!rc) rc = hipMemcpyAsync(&hp, dp, sizeof hp, hipMemcpyDeviceToHost, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     (void)hipFree(dp);
@@ -126,43 +169,71 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     const size_t ksk_words = (size_t)kBigDim * p.ks_level * (p.n + 1);
     const int npoly = (int)(p.n * 4);
     const size_t bsk_doubles = (size_t)npoly * 1024 * 2;
-    if (!is_root) {
-        if (c->has_key) {
-            FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
-            FHE_HIP_CHECK(hipFree(c->d_ksk));
-            FHE_HIP_CHECK(hipFree(c->d_bsk));
-            FHE_HIP_CHECK(hipFree(c->d_bsk_quad));
-            FHE_HIP_CHECK(hipFree(c->d_ksk_planes));
-            c->has_key = false;
-        }
-        FHE_HIP_CHECK(hipMalloc(&c->d_ksk, ksk_words * 8));
-        FHE_HIP_CHECK(hipMalloc(&c->d_ksk_planes, fhe::ks_planes_bytes((int)p.n)));
-        FHE_HIP_CHECK(hipMalloc(&c->d_bsk, bsk_doubles * 8));
-        FHE_HIP_CHECK(hipMalloc(&c->d_bsk_quad, bsk_doubles * 8));
+    if (is_root) {
+        rc = nccl_settle(comm, ncclBroadcast(c->d_ksk, c->d_ksk, ksk_words, ncclUint64, root, comm, c->stream),
+                         "ncclBroadcast", tmo, false);
+        if (!rc)
+            rc = nccl_settle(comm, ncclBroadcast(c->d_bsk, c->d_bsk, bsk_doubles, ncclFloat64, root, comm, c->stream),
+                             "ncclBroadcast", tmo, false);
+        if (rc) return rc;
+        FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+        return FHE_OK;
     }
-    rc = nccl_check(ncclBroadcast(c->d_ksk, c->d_ksk, ksk_words, ncclUint64, root, comm, c->stream), "ncclBroadcast");
-    if (!rc) rc = nccl_check(ncclBroadcast(c->d_bsk, c->d_bsk, bsk_doubles, ncclFloat64, root, comm, c->stream), "ncclBroadcast");
-    if (rc) return rc;
-    if (!is_root) {
-        FHE_HIP_CHECK(launch_ksk_to_planes(c->d_ksk, (int)p.n, c->d_ksk_planes, c->stream));
-        FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, c->d_bsk_quad, c->stream));
-        if (!(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
-            c->lut_ids.clear();
-            c->h_luts.clear();
-            c->luts_dirty = true;
-        }
-        c->p = p;
-        c->has_key = true;
-        if (!c->engine) {
-            try {
-                c->engine = new fhe::Engine(c);
-            } catch (const std::exception& ex) {
-                set_error(ex.what());
-                return FHE_ERR_HIP;
-            }
+    // Receivers: the new key lands in fresh buffers; the installed key (if any) stays in place and
+    // usable until every collective and conversion has succeeded, then the two are swapped.
+    uint64_t* n_ksk = nullptr;
+    int8_t* n_planes = nullptr;
+    double2 *n_bsk = nullptr, *n_quad = nullptr;
+    auto drop_new = [&] {
+        (void)hipStreamSynchronize(c->stream);
+        if (n_ksk) (void)hipFree(n_ksk);
+        if (n_planes) (void)hipFree(n_planes);
+        if (n_bsk) (void)hipFree(n_bsk);
+        if (n_quad) (void)hipFree(n_quad);
+    };
+    hipError_t he = hipMalloc(&n_ksk, ksk_words * 8);
+    if (he == hipSuccess) he = hipMalloc(&n_planes, fhe::ks_planes_bytes((int)p.n));
+    if (he == hipSuccess) he = hipMalloc(&n_bsk, bsk_doubles * 8);
+    if (he == hipSuccess) he = hipMalloc(&n_quad, bsk_doubles * 8);
+    if (he != hipSuccess) {
+        drop_new();
+        set_error(std::string("broadcast_server_key: ") + hipGetErrorString(he));
+        return FHE_ERR_ALLOC;
+    }
+    rc = nccl_settle(comm, ncclBroadcast(n_ksk, n_ksk, ksk_words, ncclUint64, root, comm, c->stream), "ncclBroadcast",
+                     tmo, false);
+    if (!rc)
+        rc = nccl_settle(comm, ncclBroadcast(n_bsk, n_bsk, bsk_doubles, ncclFloat64, root, comm, c->stream),
+                         "ncclBroadcast", tmo, false);
+    if (!rc) rc = launch_ksk_to_planes(n_ksk, (int)p.n, n_planes, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = launch_bsk_to_quad(n_bsk, npoly, n_quad, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (rc) {
+        drop_new();
+        return rc;
+    }
+    if (!c->engine) {
+        try {
+            c->engine = new fhe::Engine(c);
+        } catch (const std::exception& ex) {
+            drop_new();
+            set_error(ex.what());
+            return FHE_ERR_HIP;
         }
     }
-    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    // commit: swap in the new key, release the old one
+    std::swap(c->d_ksk, n_ksk);
+    std::swap(c->d_ksk_planes, n_planes);
+    std::swap(c->d_bsk, n_bsk);
+    std::swap(c->d_bsk_quad, n_quad);
+    drop_new();  // frees the previous key's buffers (null when there was none)
+    if (!(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
+        c->lut_ids.clear();
+        c->h_luts.clear();
+        c->luts_dirty = true;
+    }
+    c->p = p;
+    c->has_key = true;
     return FHE_OK;
 }
 

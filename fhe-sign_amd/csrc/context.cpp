@@ -281,7 +281,8 @@ int fhe_params_default(fhe_params* out) {
     return FHE_OK;
 }
 
-int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** ck, fhe_server_key** sk) {
+namespace {
+int generate_host(const fhe_params* params, const KeyWords& key, fhe_client_key** ck, fhe_server_key** sk) {
     if (!params || !ck || !sk) {
         set_error("null argument");
         return FHE_ERR_INVALID;
@@ -293,20 +294,51 @@ int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** 
         return FHE_ERR_UNSUPPORTED;
     }
     try {
-        auto* c = new fhe_client_key();
-        auto* s = new fhe_server_key();
-        generate_keys(p, seed, c, s);
-        *ck = c;
-        *sk = s;
+        std::unique_ptr<fhe_client_key> c(new fhe_client_key());
+        std::unique_ptr<fhe_server_key> s(new fhe_server_key());
+        generate_keys(p, key, c.get(), s.get());
+        *ck = c.release();
+        *sk = s.release();
     } catch (const std::exception& e) {
         set_error(std::string("keygen failed: ") + e.what());
         return FHE_ERR_ALLOC;
     }
     return FHE_OK;
 }
+int generate_device(fhe_ctx* c, const fhe_params* params, const KeyWords& key, fhe_client_key** ck,
+                    fhe_server_key** sk);
+}  // namespace
+
+int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** ck, fhe_server_key** sk) {
+    return generate_host(params, seed_key(seed), ck, sk);
+}
+
+int fhe_generate_keys_keyed(const fhe_params* params, const uint8_t key[32], fhe_client_key** ck,
+                            fhe_server_key** sk) {
+    if (!key) {
+        set_error("null key");
+        return FHE_ERR_INVALID;
+    }
+    return generate_host(params, bytes_key(key), ck, sk);
+}
 
 int fhe_generate_keys_device(fhe_ctx* c, const fhe_params* params, uint64_t seed, fhe_client_key** ck,
                              fhe_server_key** sk) {
+    return generate_device(c, params, seed_key(seed), ck, sk);
+}
+
+int fhe_generate_keys_device_keyed(fhe_ctx* c, const fhe_params* params, const uint8_t key[32],
+                                   fhe_client_key** ck, fhe_server_key** sk) {
+    if (!key) {
+        set_error("null key");
+        return FHE_ERR_INVALID;
+    }
+    return generate_device(c, params, bytes_key(key), ck, sk);
+}
+
+namespace {
+int generate_device(fhe_ctx* c, const fhe_params* params, const KeyWords& seed, fhe_client_key** ck,
+                    fhe_server_key** sk) {
     if (!c || !params || !ck || !sk) {
         set_error("null argument");
         return FHE_ERR_INVALID;
@@ -346,15 +378,19 @@ int fhe_generate_keys_device(fhe_ctx* c, const fhe_params* params, uint64_t seed
         step(hipMalloc(&d_glwe, kPolySize * 8)) &&
         step(hipMemcpyAsync(d_lwe, cko->lwe_sk.data(), p.n * 8, hipMemcpyHostToDevice, c->stream)) &&
         step(hipMemcpyAsync(d_glwe, cko->glwe_sk.data(), kPolySize * 8, hipMemcpyHostToDevice, c->stream)) &&
-        step(launch_chacha_u64(chacha_stream_key(seed, kStreamKsk), d_ksk, kw, c->stream)) &&
+        step(launch_chacha_u64(chacha_stream_key(seed.data(), kStreamKsk), d_ksk, kw, c->stream)) &&
         step(launch_ksk_bodies(d_ksk, d_lwe, d_glwe, (int)p.n, (int)(kPolySize * p.ks_level), (int)p.ks_level,
                                (int)p.ks_base_log, (int)p.lwe_noise_log2, c->stream)) &&
-        step(launch_chacha_u64(chacha_stream_key(seed, kStreamBsk), d_bsk, bw, c->stream)) &&
+        step(launch_chacha_u64(chacha_stream_key(seed.data(), kStreamBsk), d_bsk, bw, c->stream)) &&
         step(launch_bsk_bodies(d_bsk, d_lwe, d_glwe, (int)p.n, (int)p.pbs_base_log, (int)p.glwe_noise_log2,
                                c->stream)) &&
         step(hipMemcpyAsync(sko->ksk.data(), d_ksk, kw * 8, hipMemcpyDeviceToHost, c->stream)) &&
-        step(hipMemcpyAsync(sko->bsk.data(), d_bsk, bw * 8, hipMemcpyDeviceToHost, c->stream)) &&
-        step(hipStreamSynchronize(c->stream));
+        step(hipMemcpyAsync(sko->bsk.data(), d_bsk, bw * 8, hipMemcpyDeviceToHost, c->stream));
+    // the secret keys must not survive in freed device memory (a later allocation, possibly of
+    // another process, could read them): clear them on the stream before the buffers are released
+    if (d_lwe) (void)hipMemsetAsync(d_lwe, 0, p.n * 8, c->stream);
+    if (d_glwe) (void)hipMemsetAsync(d_glwe, 0, kPolySize * 8, c->stream);
+    step(hipStreamSynchronize(c->stream));
     release();
     if (e != hipSuccess) {
         set_error(std::string("device keygen: ") + hipGetErrorString(e));
@@ -364,6 +400,7 @@ int fhe_generate_keys_device(fhe_ctx* c, const fhe_params* params, uint64_t seed
     *sk = sko.release();
     return FHE_OK;
 }
+}  // namespace
 
 void fhe_client_key_destroy(fhe_client_key* ck) { delete ck; }
 void fhe_server_key_destroy(fhe_server_key* sk) { delete sk; }

@@ -60,7 +60,8 @@ struct fhe_ctx {
     uint64_t* d_ks_body = nullptr;
     size_t ks_cap = 0;              // ciphertexts
     // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU)
-    int wide_threshold = 512;  // wide up to two ciphertexts per CU; quad above (profiles/r1/latency_sweep_r1p.txt)
+    // (one ciphertext per CU at a time -- 144 KB LDS -- so up to two rounds over the 256 CUs); quad above
+    int wide_threshold = 512;  // profiles/r1/latency_sweep_r1p.txt
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;
@@ -87,6 +88,7 @@ struct fhe_ctx {
     // one ciphertext per CU is already their latency floor.
     void* comm = nullptr;       // ncclComm_t
     int rank = 0, nranks = 1;
+    uint32_t comm_timeout_ms = FHE_COMM_DEFAULT_TIMEOUT_MS;  // deadline of every collective's enqueue
     int fanout_emulate = 0;     // test hook: split levels over this many virtual ranks on one GPU
     size_t fanout_min = 257;  // above one ciphertext per CU (256 CUs) a level costs 2x the floor
     uint64_t* d_gather = nullptr;        // [nranks * chunk][2049]

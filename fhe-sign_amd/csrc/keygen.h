@@ -10,7 +10,7 @@ struct ChaChaKey {
     uint32_t key[8];
     uint32_t nonce[3];
 };
-ChaChaKey chacha_stream_key(uint64_t seed, uint32_t stream);
+ChaChaKey chacha_stream_key(const uint32_t key[8], uint32_t stream);
 
 // out[q] = u64 word q of the stream (q < count; count / 8 blocks must stay below 2^32)
 hipError_t launch_chacha_u64(const ChaChaKey& k, uint64_t* out, uint64_t count, hipStream_t s);

@@ -122,11 +122,9 @@ __global__ __launch_bounds__(256) void k_bsk_bodies(uint64_t* __restrict__ bsk, 
 
 }  // namespace
 
-ChaChaKey chacha_stream_key(uint64_t seed, uint32_t stream) {
+ChaChaKey chacha_stream_key(const uint32_t key[8], uint32_t stream) {
     ChaChaKey k{};  // keys.cpp ChaChaStream::reset
-    k.key[0] = (uint32_t)seed;
-    k.key[1] = (uint32_t)(seed >> 32);
-    k.key[2] = 0x46484553u;
+    for (int i = 0; i < 8; ++i) k.key[i] = key[i];
     k.nonce[0] = stream;
     k.nonce[1] = 0x524f434du;
     k.nonce[2] = 0;

@@ -74,11 +74,24 @@ static inline void qround(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
     c += d; b ^= c; b = rotl(b, 7);
 }
 
-void ChaChaStream::reset(uint64_t seed, uint32_t stream) {
-    key_.fill(0);
-    key_[0] = (uint32_t)seed;
-    key_[1] = (uint32_t)(seed >> 32);
-    key_[2] = 0x46484553u;  // "FHES"
+KeyWords seed_key(uint64_t seed) {
+    KeyWords k{};
+    k[0] = (uint32_t)seed;
+    k[1] = (uint32_t)(seed >> 32);
+    k[2] = 0x46484553u;  // "FHES"
+    return k;
+}
+
+KeyWords bytes_key(const uint8_t* b) {
+    KeyWords k{};
+    for (int i = 0; i < 8; ++i)
+        k[i] = (uint32_t)b[4 * i] | (uint32_t)b[4 * i + 1] << 8 | (uint32_t)b[4 * i + 2] << 16 |
+               (uint32_t)b[4 * i + 3] << 24;
+    return k;
+}
+
+void ChaChaStream::reset(const KeyWords& key, uint32_t stream) {
+    key_ = key;
     nonce_ = {stream, 0x524f434du /* "ROCM" */, 0};
     counter_ = 0;
     pos_ = 16;
@@ -167,7 +180,7 @@ static void negacyclic_binary_mac(uint64_t* r, const uint64_t* a, const uint64_t
     }
 }
 
-void generate_secret_keys(const Params& p, uint64_t seed, fhe_client_key* ck) {
+void generate_secret_keys(const Params& p, const KeyWords& seed, fhe_client_key* ck) {
     ck->params = p;
     ck->lwe_sk.assign(p.n, 0);
     ck->glwe_sk.assign(kPolySize, 0);
@@ -179,7 +192,7 @@ void generate_secret_keys(const Params& p, uint64_t seed, fhe_client_key* ck) {
     ck->enc_rng.reset(seed, kStreamEncrypt);
 }
 
-void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_server_key* sk) {
+void generate_keys(const Params& p, const KeyWords& seed, fhe_client_key* ck, fhe_server_key* sk) {
     const uint32_t n = p.n, N = kPolySize, L = p.ks_level;
     sk->params = p;
     generate_secret_keys(p, seed, ck);

@@ -33,12 +33,22 @@ struct Params {
     uint32_t msg_carry() const { return message_modulus * carry_modulus; }
 };
 
+// The 256-bit ChaCha20 key every key-generation stream is derived from (stream id = nonce word 0).
+// Production keys come from 32 bytes of OS entropy (fhe_generate_keys_keyed, generate_keys(seed=None)
+// in the Python mirror); `seed_key` expands a 64-bit test seed into {seed, "FHES", 0, ...} -- a
+// deterministic, publicly reproducible key meant for tests only.
+using KeyWords = std::array<uint32_t, 8>;
+KeyWords seed_key(uint64_t seed);
+KeyWords bytes_key(const uint8_t* key32);  // little-endian words
+
 // ChaCha20 block function (RFC 8439) as a deterministic stream of 64-bit words.
 class ChaChaStream {
 public:
     ChaChaStream() = default;
     ChaChaStream(uint64_t seed, uint32_t stream) { reset(seed, stream); }
-    void reset(uint64_t seed, uint32_t stream);
+    ChaChaStream(const KeyWords& key, uint32_t stream) { reset(key, stream); }
+    void reset(uint64_t seed, uint32_t stream) { reset(seed_key(seed), stream); }
+    void reset(const KeyWords& key, uint32_t stream);
     uint64_t next_u64();
     int64_t tuniform(uint32_t log2_bound);
     // absolute position (32-bit words) of the next output within the current nonce epoch, and a
@@ -79,10 +89,10 @@ struct fhe_server_key {
 };
 
 namespace fhe {
-void generate_keys(const Params& p, uint64_t seed, fhe_client_key* ck, fhe_server_key* sk);
+void generate_keys(const Params& p, const KeyWords& key, fhe_client_key* ck, fhe_server_key* sk);
 // the client-key half of generate_keys (secret keys, encryption stream); the device keygen
 // (context.cpp: fhe_generate_keys_device) uses it and derives the server key on the GPU
-void generate_secret_keys(const Params& p, uint64_t seed, fhe_client_key* ck);
+void generate_secret_keys(const Params& p, const KeyWords& key, fhe_client_key* ck);
 void encrypt_big(fhe_client_key* ck, uint64_t plaintext, uint64_t* ct);
 // n encryptions (plaintexts already scaled), outputs and stream state identical to n encrypt_big
 // calls; large batches run on several host threads over seeked copies of the stream

@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libfhe_rocm.so")
+# FHE_ROCM_LIB selects another build of the same library (the host-sanitizer build of
+# `make -C fhe-sign_amd asan`, tools/sanitize_host.sh); by default the in-tree product build.
+LIB_PATH = os.environ.get("FHE_ROCM_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libfhe_rocm.so")
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
@@ -32,6 +34,10 @@ _SIGNATURES = [
     ("fhe_generate_keys", C.c_int, [C.POINTER(FheParams), C.c_uint64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     ("fhe_generate_keys_device", C.c_int,
      [C.c_void_p, C.POINTER(FheParams), C.c_uint64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    ("fhe_generate_keys_keyed", C.c_int,
+     [C.POINTER(FheParams), C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    ("fhe_generate_keys_device_keyed", C.c_int,
+     [C.c_void_p, C.POINTER(FheParams), C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     ("fhe_client_key_destroy", None, [C.c_void_p]),
     ("fhe_server_key_destroy", None, [C.c_void_p]),
     ("fhe_client_key_export", C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
@@ -59,6 +65,7 @@ _SIGNATURES = [
     ("fhe_ctx_set_ks_kernel", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("fhe_ctx_attach_comm", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+    ("fhe_ctx_attach_comm_timeout", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_uint32]),
     ("fhe_ctx_broadcast_server_key", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_ctx_params", C.c_int, [C.c_void_p, C.POINTER(FheParams)]),
     ("fhe_ctx_detach_comm", C.c_int, [C.c_void_p]),

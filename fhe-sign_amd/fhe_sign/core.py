@@ -112,16 +112,30 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
-def generate_keys(params: FheParams | None = None, seed: int = 0, device: "Context | None" = None):
+def generate_keys(params: FheParams | None = None, seed: int | None = None, device: "Context | None" = None):
     """tfhe::generate_keys(ConfigBuilder::default().build()) -- src/schnorr.rs:441-442.
+
+    seed=None (the default) keys every ChaCha20 stream with 32 bytes from os.urandom, as tfhe-rs
+    draws from the OS CSPRNG.  An integer seed gives DETERMINISTIC, INSECURE keys (a public
+    expansion of 64 bits) for tests and golden vectors only.
     With `device` (a Context), the server key is generated on that GPU: identical key words
-    (fhe_generate_keys_device); the key is returned, not installed."""
+    (fhe_generate_keys_device*); the key is returned, not installed."""
+    import os
+
     p = params or default_params()
     ck, sk = C.c_void_p(), C.c_void_p()
-    if device is None:
-        check(load().fhe_generate_keys(C.byref(p), seed, C.byref(ck), C.byref(sk)))
+    lib = load()
+    if seed is None:
+        key = (C.c_uint8 * 32).from_buffer_copy(os.urandom(32))
+        if device is None:
+            check(lib.fhe_generate_keys_keyed(C.byref(p), key, C.byref(ck), C.byref(sk)))
+        else:
+            check(lib.fhe_generate_keys_device_keyed(device.handle, C.byref(p), key, C.byref(ck), C.byref(sk)))
+        C.memset(key, 0, 32)
+    elif device is None:
+        check(lib.fhe_generate_keys(C.byref(p), seed, C.byref(ck), C.byref(sk)))
     else:
-        check(load().fhe_generate_keys_device(device.handle, C.byref(p), seed, C.byref(ck), C.byref(sk)))
+        check(lib.fhe_generate_keys_device(device.handle, C.byref(p), seed, C.byref(ck), C.byref(sk)))
     return ClientKey(ck, p), ServerKey(sk, p)
 
 
@@ -203,9 +217,15 @@ class Context:
         check(load().fhe_ctx_set_wide_threshold(self._h, int(threshold)))
 
     # ---- multi-GPU fan-out (one process per GPU)
-    def attach_comm(self, unique_id: bytes, nranks: int, rank: int) -> None:
+    def attach_comm(self, unique_id: bytes, nranks: int, rank: int, timeout_ms: int = 120000) -> None:
+        """non-blocking RCCL init polled against `timeout_ms`: a peer that never joins gives an error
+        (FHE_ERR_TIMEOUT), not a hang"""
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
-        check(load().fhe_ctx_attach_comm(self._h, buf, nranks, rank))
+        check(load().fhe_ctx_attach_comm_timeout(self._h, buf, nranks, rank, int(timeout_ms)))
+
+    def ready(self) -> bool:
+        """the context exists and its device is usable (checked before any collective is entered)"""
+        return bool(getattr(self, "_h", None)) and load().fhe_ctx_sync(self._h) == 0
 
     def broadcast_server_key(self, root: int = 0) -> None:
         """collective: replicate rank `root`'s installed server key to every rank (RCCL)"""

@@ -3,9 +3,10 @@
 The data path is the engine's own RCCL communicator (comm.cpp: in-place all-gather of each split
 level on the engine stream).  This module only does the out-of-band part over an already
 initialised torch.distributed process group (gloo is enough): rank 0 creates the RCCL id, every
-rank receives it and attaches, and the ranks agree that all of them succeeded before any
-collective is issued -- a rank that failed alone would otherwise leave the others waiting in an
-all-gather.
+rank receives it, the ranks agree that every one of them is ready BEFORE anyone enters the
+communicator init (itself a collective), attach with a non-blocking init polled against a deadline
+(comm.cpp: a peer that dies inside the init gives FHE_ERR_TIMEOUT, not a hang), and agree again that
+all of them succeeded before any data-path collective is issued.
 """
 from __future__ import annotations
 
@@ -34,20 +35,36 @@ def share_id(dist, rank: int, make_id=comm_unique_id) -> bytes | None:
     return bytes(buf[:128].tolist()) if int(buf[128]) else None
 
 
-def attach_fanout(ctx, dist, rank: int, world: int, min_level: int = 257, make_id=comm_unique_id):
+def attach_fanout(ctx, dist, rank: int, world: int, min_level: int = 257, make_id=comm_unique_id,
+                  timeout_ms: int = 120000):
     """Attach `ctx` to a world-size RCCL communicator and enable level fan-out.
-    Returns (ok, error): ok is identical on all ranks."""
-    err = None
+    Returns (ok, error): ok is identical on all ranks.
+
+    1. rank 0's id is shared (None everywhere if it could not make one);
+    2. every rank reports readiness (id received, context alive, device usable) and the ranks agree
+       on it before the init: a rank that fails here makes nobody enter the collective;
+    3. the init itself runs under `timeout_ms` (a peer dying inside it -> error on the others);
+    4. the ranks agree that every attach succeeded, else all detach."""
     uid = share_id(dist, rank, make_id)
-    ok = uid is not None
-    if not ok:
+    ready, err = uid is not None, None
+    if not ready:
         err = "rank 0 could not create an RCCL id"
     else:
         try:
-            ctx.attach_comm(uid, world, rank)
-            ctx.set_fanout(min_level)
+            check_ready = getattr(ctx, "ready", None)
+            ready = bool(check_ready()) if check_ready else True
+            if not ready:
+                err = f"rank {rank}: context/device not ready"
         except Exception as e:  # noqa: BLE001
-            ok, err = False, str(e)
+            ready, err = False, f"rank {rank}: {e}"
+    if not all_ok(dist, ready):
+        return False, err or "another rank was not ready to attach"
+    ok = True
+    try:
+        ctx.attach_comm(uid, world, rank, timeout_ms)
+        ctx.set_fanout(min_level)
+    except Exception as e:  # noqa: BLE001
+        ok, err = False, str(e)
     if not all_ok(dist, ok):
         try:
             ctx.detach_comm()

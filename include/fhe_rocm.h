@@ -29,6 +29,7 @@ extern "C" {
 #define FHE_ERR_NO_KEY (-3)
 #define FHE_ERR_ALLOC (-4)
 #define FHE_ERR_UNSUPPORTED (-5)
+#define FHE_ERR_TIMEOUT (-6) /* a collective's peers did not arrive before the deadline */
 
 #define FHE_LWE_BIG_SIZE 2049u /* big LWE ciphertext words (k*N + 1) */
 
@@ -58,14 +59,24 @@ const char* fhe_last_error(void);
 int fhe_params_default(fhe_params* out);
 
 /* ---------------------------------------------------------------------------------- keys */
-/* Replaces tfhe::generate_keys(config) (src/schnorr.rs:442, src/biguint.rs:277,
- * src/perf_test.rs:12).  Deterministic in `seed` (ChaCha20 streams). */
+/* Replaces tfhe::generate_keys(config) (src/schnorr.rs:441-442, src/biguint.rs:277,
+ * src/perf_test.rs:12), which draws from the OS CSPRNG.  Every key stream (secret keys, KSK, BSK,
+ * encryption) is ChaCha20 under one 256-bit key: pass 32 bytes of OS entropy (getrandom /
+ * /dev/urandom) as `key`.  The key bytes are the client's secret -- whoever holds them can rebuild
+ * the client key. */
+int fhe_generate_keys_keyed(const fhe_params* params, const uint8_t key[32],
+                            fhe_client_key** client_key, fhe_server_key** server_key);
+/* DETERMINISTIC, INSECURE -- tests and golden vectors only: the 256-bit key is the public
+ * expansion {seed, "FHES", 0...} of a 64-bit `seed`, so anyone can rebuild the client key. */
 int fhe_generate_keys(const fhe_params* params, uint64_t seed, fhe_client_key** client_key,
                       fhe_server_key** server_key);
 /* The same keys (identical words) generated on the GPU of `ctx` (keygen
  * dominates setup).  The ChaCha streams are counter-indexed, so the host's sequential draws become
  * one stream block per thread; the key is downloaded into the returned handle and not installed
  * (call fhe_set_server_key as after fhe_generate_keys).  ctx needs no server key. */
+int fhe_generate_keys_device_keyed(fhe_ctx* ctx, const fhe_params* params, const uint8_t key[32],
+                                   fhe_client_key** client_key, fhe_server_key** server_key);
+/* the deterministic test-seed form (INSECURE, as fhe_generate_keys) */
 int fhe_generate_keys_device(fhe_ctx* ctx, const fhe_params* params, uint64_t seed,
                              fhe_client_key** client_key, fhe_server_key** server_key);
 void fhe_client_key_destroy(fhe_client_key* ck);
@@ -149,12 +160,22 @@ int fhe_ctx_set_ks_kernel(fhe_ctx* ctx, int kind);
  * over the ranks and its outputs all-gathered with RCCL on the engine stream.  Smaller levels are
  * computed redundantly on every rank.  Rank 0 creates the id and shares it out of band. */
 #define FHE_COMM_ID_BYTES 128
+#define FHE_COMM_DEFAULT_TIMEOUT_MS 120000u
 int fhe_comm_unique_id(uint8_t id[FHE_COMM_ID_BYTES]);
+/* Non-blocking communicator init (RCCL ncclCommInitRankConfig, blocking = 0) polled against a
+ * deadline: if a peer never joins, the communicator is aborted and FHE_ERR_TIMEOUT returned on the
+ * ranks that did -- no rank is left waiting inside the library.  The same deadline bounds the
+ * enqueue of every later collective (all-gather, key broadcast).  Callers should still agree out of
+ * band that every rank is ready before attaching (fhe_sign/dist.py: attach_fanout). */
+int fhe_ctx_attach_comm_timeout(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank,
+                                uint32_t timeout_ms);
+/* the same with FHE_COMM_DEFAULT_TIMEOUT_MS */
 int fhe_ctx_attach_comm(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank);
 /* Collective over the attached communicator: rank `root` (which has a server key installed)
  * replicates it to every rank device-to-device (RCCL broadcast over xGMI: parameters, KSK, Fourier
  * BSK; each receiver derives the kernels' layouts itself).  Afterwards every rank's context is as if
- * fhe_set_server_key had been called with the root's key. */
+ * fhe_set_server_key had been called with the root's key.  A receiver keeps its previously installed
+ * key (if any) until the collectives and conversions have succeeded: on any error it is unchanged. */
 int fhe_ctx_broadcast_server_key(fhe_ctx* ctx, int root);
 /* parameters of the server key installed in a context */
 int fhe_ctx_params(const fhe_ctx* ctx, fhe_params* out);

@@ -412,6 +412,16 @@ void fho_keyswitch(const fho_keys* k, const uint64_t* in, uint64_t* out) {
     }
 }
 
+void fho_keyswitch_batch(const fho_keys* k, const uint64_t* in, size_t count, uint64_t* out, int threads) {
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (long i = 0; i < (long)count; ++i)
+        fho_keyswitch(k, in + (size_t)i * (FHO_N + 1), out + (size_t)i * (k->p.n + 1));
+    (void)threads;
+}
+
 uint32_t fho_modswitch(uint64_t x) {
     return (uint32_t)((((x >> 51) + 1) >> 1) & (2 * FHO_N - 1));
 }

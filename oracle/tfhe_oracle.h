@@ -113,6 +113,8 @@ uint64_t fho_delta(const fho_params* p);
 
 /* --- PBS pipeline --- */
 void fho_keyswitch(const fho_keys* k, const uint64_t* ct_big, uint64_t* ct_small /* n+1 */);
+/* count keyswitches, OpenMP over ciphertexts (out: count x (n+1)) */
+void fho_keyswitch_batch(const fho_keys* k, const uint64_t* in, size_t count, uint64_t* out, int threads);
 uint32_t fho_modswitch(uint64_t x); /* -> [0, 2N) */
 /* lut: N coefficients (GLWE body of the accumulator) */
 void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_t* lut,

@@ -54,10 +54,15 @@ def test_single_rank_needs_no_process_group():
 class _FakeCtx:
     """Stands in for fhe_sign.Context: records what the fan-out control plane asks of it."""
 
-    def __init__(self, fail=False):
-        self.fail, self.calls = fail, []
+    def __init__(self, fail=False, not_ready=False):
+        self.fail, self.not_ready, self.calls = fail, not_ready, []
 
-    def attach_comm(self, uid, world, rank):
+    def ready(self):
+        if self.not_ready:
+            raise RuntimeError("hipSetDevice failed")
+        return True
+
+    def attach_comm(self, uid, world, rank, timeout_ms=None):
         if self.fail:
             raise RuntimeError("attach refused")
         self.calls.append(("attach", uid, world, rank))
@@ -69,23 +74,23 @@ class _FakeCtx:
         self.calls.append(("detach",))
 
 
-def _fanout_rank(rank, world, port, fail_rank, q):
+def _fanout_rank(rank, world, port, fail_rank, q, unready_rank=-1):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
     import torch.distributed as dist
     from fhe_sign.dist import attach_fanout
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    ctx = _FakeCtx(fail=rank == fail_rank)
+    ctx = _FakeCtx(fail=rank == fail_rank, not_ready=rank == unready_rank)
     ok, err = attach_fanout(ctx, dist, rank, world, min_level=300, make_id=lambda: bytes(range(128)))
     q.put((rank, ok, ctx.calls))
     dist.destroy_process_group()
 
 
-def _run_fanout(fail_rank):
+def _run_fanout(fail_rank, unready_rank=-1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_fanout_rank, args=(r, 2, port, fail_rank, q)) for r in range(2)]
+    procs = [ctx.Process(target=_fanout_rank, args=(r, 2, port, fail_rank, q, unready_rank)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -100,6 +105,14 @@ def test_fanout_attach_world2_shares_rank0_id():
     for rank, ok, calls in got:
         assert ok
         assert calls == [("attach", bytes(range(128)), 2, rank), ("fanout", 300)]
+
+
+def test_fanout_unready_rank_stops_everyone_before_the_init():
+    """A rank that fails BEFORE the (collective) communicator init -- e.g. its device is unusable --
+    is agreed on first: no rank calls attach_comm at all, so nobody waits in ncclCommInitRank for a
+    peer that will never come (comm.cpp additionally bounds the init with a deadline)."""
+    got = _run_fanout(fail_rank=-1, unready_rank=1)
+    assert [(ok, calls) for _, ok, calls in got] == [(False, []), (False, [])]
 
 
 def test_fanout_attach_failure_is_agreed():
@@ -168,3 +181,20 @@ def test_fanout_deadline_guard():
     r, hung = bench.with_deadline(lambda: stop.wait(30), 0.2)
     assert hung and r is None and time.perf_counter() - t < 5
     stop.set()
+
+
+def test_fanout_hang_exits_nonzero():
+    """A hung fan-out leg is abandoned AND the process exits with a non-zero status (3): the driver
+    must record the run as failed, not as rc 0 with an 'error' buried in the JSON."""
+    import subprocess
+    code = (
+        "import importlib.util, threading, json\n"
+        f"spec = importlib.util.spec_from_file_location('b', {os.path.join(ROOT, 'bench.py')!r})\n"
+        "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+        "r, hung = b.with_deadline(lambda: threading.Event().wait(60), 0.2)\n"
+        "print(json.dumps({'value': 1.0}), flush=True)\n"
+        "if hung: b.abandon('test hang')\n"
+    )
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3, (p.returncode, p.stderr)
+    assert '"value": 1.0' in p.stdout and "status 3" in p.stderr

@@ -7,10 +7,15 @@ the unsplit run, which pins the partition / gather / scatter indexing -- and (b)
 RCCL communicator of world 1 (the all-gather path with the library).  Multi-rank RCCL on distinct
 GPUs is exercised by bench.py's fan-out leg at N > 1; the out-of-band id exchange is covered on
 CPU by tests/test_dist_cpu.py."""
+import csv
+import json
+import os
 import random
 
 import numpy as np
 import pytest
+
+from conftest import ROOT
 
 from fhe_sign import (COMPAT, FAST, BigUintFHE, Context, FheUint64, FheUint256, Schnorr, comm_unique_id, compute_nonce,
                       generate_keys, set_server_key)
@@ -106,3 +111,84 @@ def test_rccl_world1_server_key_broadcast(keys):
     set_server_key(None)
     ctx.close()
     ref_ctx.close()
+
+
+# ---------------------------------------------------------------- config 5 at the production split
+CSV = {r["index"]: r for r in csv.DictReader(open(os.path.join(ROOT, "tests", "golden", "bip340_vectors.csv")))}
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _limbs(x):
+    return [int(v) for v in x]
+
+
+def _config5(ctx, ck):
+    """What config 5 runs: sign_fhe_with_k0 (compat, fast) on vector 0, its FHE block k + e*d' for
+    vector 1 (8x8 limbs) as ciphertexts, the compat 256-bit mul, and the 8-sign batch of SURVEY 8d
+    (vectors 0, 1, 2, 15, 16, 17, 18, 0).  Returns (ciphertext words, decrypted values)."""
+    set_server_key(ctx)
+    ck.seed_encryption(0xC5, 100)  # identical ciphertext inputs for every configuration
+    s = Schnorr()
+    g = json.load(open(os.path.join(GOLD, "biguint_vectors.json")))["mul"][0]
+    v1 = json.load(open(os.path.join(GOLD, "sign_vectors.json")))["vectors"][1]
+    val = lambda limbs: sum(int(x) << (32 * i) for i, x in enumerate(limbs))  # noqa: E731
+    A, B = BigUintFHE.new(val(g["a"]), ck), BigUintFHE.new(val(g["b"]), ck)
+    E, D, K = (BigUintFHE.new(val(v1[k]), ck) for k in ("e", "d", "k"))
+    mul = A.mul(B, COMPAT)
+    block = E.mul_add(D, K, COMPAT)
+    cts = {"mul_compat": [x.export() for x in mul.digits], "sign_block_v1": [x.export() for x in block.digits]}
+    vals = {"mul_compat": mul.decrypt_limbs(ck), "sign_block_v1": block.decrypt_limbs(ck)}
+    d, msg = 3, bytes(32)
+    k0 = compute_nonce(d, msg, bytes(32))
+    dF = BigUintFHE.new(d, ck)
+    vals["sign_v0_compat"] = s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT)
+    vals["sign_v0_fast"] = s.sign_fhe_with_k0(msg, k0, d, dF, ck, FAST)
+    jobs = []
+    for idx in ("0", "1", "2", "15", "16", "17", "18", "0"):
+        row = CSV[idx]
+        dd = int(row["secret key"], 16)
+        mm, aux = bytes.fromhex(row["message"]), bytes.fromhex(row["aux_rand"])
+        jobs.append((mm, compute_nonce(dd, mm, aux), dd, BigUintFHE.new(dd, ck)))
+    vals["batch8"] = s.sign_fhe_with_k0_batch(jobs, ck, COMPAT)
+    return cts, vals, (g, v1)
+
+
+@pytest.fixture(scope="module")
+def config5_ref(keys):
+    ck, sk = keys
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    cts, vals, (g, v1) = _config5(ctx, ck)
+    # the unsplit run itself against the reference's data
+    assert vals["mul_compat"] == _limbs(g["out"])
+    assert vals["sign_block_v1"] == _limbs(v1["sum"])
+    assert vals["sign_v0_compat"].hex().upper() == CSV["0"]["signature"].upper()
+    assert vals["sign_v0_fast"].hex().upper() == CSV["0"]["signature"].upper()
+    for idx, sig in zip(("0", "1", "2", "15", "16", "17", "18", "0"), vals["batch8"]):
+        assert sig.hex().upper() == CSV[idx]["signature"].upper(), idx
+    set_server_key(None)
+    ctx.close()
+    return cts, vals
+
+
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+def test_config5_emulated_ranks_production_split(keys, config5_ref, ranks):
+    """config 5 (one sign / one 256-bit mul fanned over N GPUs, src/schnorr.rs:270-277) at the
+    production split threshold (levels of >= 257 bootstraps, fhe_ctx_set_fanout's default): emulated
+    ranks compute every slice on this GPU, so each ciphertext word must equal the unsplit run's, and
+    every signature the CSV's (the 8-sign batch of SURVEY 8d included)."""
+    ck, sk = keys
+    ref_cts, ref_vals = config5_ref
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    ctx.set_fanout(min_level=257, emulate_ranks=ranks)
+    cts, vals, _ = _config5(ctx, ck)
+    assert vals == ref_vals
+    for k in ref_cts:
+        assert len(cts[k]) == len(ref_cts[k])
+        for x, y in zip(cts[k], ref_cts[k]):
+            assert np.array_equal(x, y), (ranks, k)
+    _, world, split = ctx.fanout_info()
+    assert world == ranks and split > 0  # the compat mul's wide product levels were split
+    set_server_key(None)
+    ctx.close()

@@ -79,3 +79,36 @@ def test_batch_encryption_equals_sequential():
         assert np.array_equal(seq, bat), n
         assert np.array_equal(ck.encrypt_block(5), ck2.encrypt_block(5))  # same stream position after
         assert [ck2.decrypt_block(c) for c in bat[:20]] == vals[:20]
+
+
+def test_default_keys_are_drawn_from_os_entropy():
+    """generate_keys() with no seed keys every stream with 32 bytes of os.urandom (tfhe-rs draws from
+    the OS CSPRNG, src/schnorr.rs:441-442): two calls give unrelated secret keys, and the keyed C
+    entry with the bytes of a test seed's public expansion {seed, "FHES", 0...} rebuilds exactly the
+    seeded (deterministic, insecure) keys -- the seed path is only a fixed key, not a weaker cipher."""
+    import ctypes as C
+    import struct
+
+    from fhe_sign._lib import check, load
+    from fhe_sign.core import ClientKey, ServerKey, default_params
+
+    a, _ = generate_keys()
+    b, _ = generate_keys()
+    la, ga = a.export()
+    lb, gb = b.export()
+    assert not np.array_equal(la, lb) and not np.array_equal(ga, gb)
+    assert 300 < la.sum() < 534
+
+    seed = 0xB1
+    key = struct.pack("<8I", seed & 0xFFFFFFFF, seed >> 32, 0x46484553, 0, 0, 0, 0, 0)
+    p = default_params()
+    ck, sk = C.c_void_p(), C.c_void_p()
+    check(load().fhe_generate_keys_keyed(C.byref(p), (C.c_uint8 * 32).from_buffer_copy(key), C.byref(ck),
+                                         C.byref(sk)))
+    ck, sk = ClientKey(ck, p), ServerKey(sk, p)
+    ref_ck, ref_sk = generate_keys(seed=seed)
+    for x, y in zip(ck.export(), ref_ck.export()):
+        assert np.array_equal(x, y)
+    for x, y in zip(sk.export(), ref_sk.export()):
+        assert np.array_equal(x, y)
+    assert load().fhe_generate_keys_keyed(C.byref(p), None, C.byref(ck.handle), C.byref(sk.handle)) != 0

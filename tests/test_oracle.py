@@ -124,3 +124,44 @@ def test_noise_budget_at_radix_limit_oracle(okeys):
     assert np.abs(errs).max() < 64
     print(f"modulus-switched sigma at 22 units: {errs.std():.2f} (half step 64)")
     assert errs.std() * 8 < 64, f"modulus-switched sigma {errs.std():.2f}"
+
+
+def test_noise_failure_sample_oracle_10k(okeys):
+    """CPU mirror of tests/test_noise_gpu.py on the oracle: 10^4 PBS inputs at the radix
+    layer's noise limit -- 5000 of the carry prefix's 22-unit shape 4 s0 + 2 s1 + s2 + c and 5000 of
+    the 25-unit shape 4 s + 3 c -- built from a pool of 384 oracle bootstrap outputs (distinct index
+    tuples; tuples share pool blocks, so the samples are correlated, not independent), keyswitched
+    (batched) and modulus-switched: the blind rotation's input error in the 4096-domain must stay
+    below the half step (64) for every one of them -- zero decode failures -- and its sigma must
+    match the modulus-switch model sqrt((n/2 + 1) / 12) (the dominant term) within 15 %."""
+    rs = np.random.default_rng(0x10_000)
+    ns, nc = 256, 128
+    sv, cv = rs.integers(0, 3, ns), rs.integers(0, 2, nc)
+    r = okeys.rng(79)
+    fresh = np.stack([okeys.encrypt(r, int(v)) for v in np.concatenate([sv, cv])])
+    ident = okeys.make_lut(list(range(16)))[None, :]
+    unit = okeys.pbs_batch(fresh, ident, np.zeros(len(fresh), np.uint32)).astype(np.uint64)
+    us, uc = unit[:ns], unit[ns:]
+    K = 5000
+    ia = np.stack([rs.choice(ns, 3, replace=False) for _ in range(K)])
+    ic = rs.integers(0, nc, K)
+    ib = rs.integers(0, ns, K)
+    jc = rs.integers(0, nc, K)
+    with np.errstate(over="ignore"):
+        comb_a = np.uint64(4) * us[ia[:, 0]] + np.uint64(2) * us[ia[:, 1]] + us[ia[:, 2]] + uc[ic]
+        comb_b = np.uint64(4) * us[ib] + np.uint64(3) * uc[jc]
+    m = np.concatenate([4 * sv[ia[:, 0]] + 2 * sv[ia[:, 1]] + sv[ia[:, 2]] + cv[ic], 4 * sv[ib] + 3 * cv[jc]])
+    assert m.max() <= 15
+    small = okeys.keyswitch_batch(np.concatenate([comb_a, comb_b]))
+    n = okeys.params.n
+    ms = ((small.astype(object) + (1 << 51)) >> 52) % 4096
+    ms = ms.astype(np.int64)
+    phase = (ms[:, n] - ms[:, :n] @ okeys.lwe_sk.astype(np.int64)) % 4096
+    err = (phase - 128 * m + 2048) % 4096 - 2048
+    fails = int((np.abs(err) >= 64).sum())
+    model = np.sqrt((n / 2 + 1) / 12)
+    print(f"\noracle: {2 * K} inputs at 22/25 units, {fails} failures; MS-domain sigma 22u {err[:K].std():.2f}, "
+          f"25u {err[K:].std():.2f} (modulus-switch model {model:.2f}; half step 64); max |err| {np.abs(err).max()}")
+    assert fails == 0
+    for e in (err[:K], err[K:]):
+        assert abs(e.std() / model - 1) < 0.15

@@ -147,6 +147,29 @@ def test_biguint_mul_256_compat(keys):
     assert p1 > p0 and l1 > l0
 
 
+def test_biguint_mul_256_config2_breadth(keys):
+    """config 2 breadth on the HIP path: every committed seeded 8x8 pair, BIP-340 vector 1's e*d'
+    and the all-ones (F7) pair, each in compat (the reference's limbs, src/biguint.rs:194-265, lost
+    carries included) and fast (true product) mode.  All 20 products are issued before the first
+    host read, so the deferred engine runs them as ONE schedule (throughput-bound, not 20 x the
+    latency floor)."""
+    ck, _ = keys
+    g = json.load(open(os.path.join(G, "biguint_vectors.json")))
+    v1 = json.load(open(os.path.join(G, "sign_vectors.json")))["vectors"][1]
+    q = g["quirk_mul"][0]
+    pairs = [(v["a"], v["b"], v["out"]) for v in g["mul"]] + [(v1["e"], v1["d"], v1["prod"]),
+                                                              (q["a"], q["b"], q["out"])]
+    assert len(pairs) == 10
+    outs = []
+    for a, b, want in pairs:
+        A, B = _big(ck, a), _big(ck, b)
+        outs.append((A.mul(B, COMPAT), A.mul(B, FAST), a, b, want))
+    for i, (oc, of, a, b, want) in enumerate(outs):
+        assert oc.decrypt_limbs(ck) == want, i
+        assert R.from_limbs(of.decrypt_limbs(ck)) == R.from_limbs(a) * R.from_limbs(b), i
+    assert outs[-1][0].decrypt_limbs(ck) == q["out"] != q["true_product"]
+
+
 def test_biguint_mul_quirk_compat_vs_fast(keys):
     """F7: (2^256-1)^2 -- compat reproduces the reference's lost carry, fast gives the true product."""
     ck, _ = keys
