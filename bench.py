@@ -34,6 +34,10 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "r1w_pmc_summary.json")  # to
 FANOUT_MIN = 257  # levels with at least this many bootstraps are split over the GPUs (fan-out legs)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FLOPS_PER_CMUX = 4 * 51200 + 4 * 6144 + 32768   # 4 FFT-1024 (5 N log N), 4 twist/untwist, MAC
+# multi-bit (grouping 2), per pair of key bits: the same transforms and MAC, plus the key bundle --
+# per Fourier point 3 monomials minus 1 (3) and 3 patterns x 4 polynomials of complex multiply-add (96)
+FLOPS_PER_GROUP_MB = FLOPS_PER_CMUX + 1024 * (3 + 96)
+L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 ~34.5 TB/s aggregate
 
 
 def parse():
@@ -46,6 +50,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0xF11E51)
     ap.add_argument("--no-ops", action="store_true", help="skip the 256-bit mul / sign wall-clock legs")
+    ap.add_argument("--no-multibit", action="store_true", help="skip the multi-bit (grouping 2) measurement")
     return ap.parse_args()
 
 
@@ -298,16 +303,14 @@ def fanout_legs(ck, ctx, dist, rank, world, seed):
     return out
 
 
-def main():
-    a = parse()
-    dist, rank, world, local = dist_setup(a.gpus)
-    from fhe_sign import Context, generate_keys
+def pbs_leg(a, kind, dist, rank, world, device):
+    """one parameter set: keys, the timed batch of `a.batch` PBS per GPU (barrier + sync around exactly
+    a.steps steps, max over ranks), the live HIP-event kernel timing and a decryption spot check.
+    Returns (ck, ctx, result dict); the caller frees nothing (ctx.close() at exit)."""
+    from fhe_sign import Context, default_params, generate_keys, multi_bit_params
 
-    ck, sk = generate_keys(seed=a.seed)
-    device = local
-    if dist is not None:  # more ranks than visible GPUs (rehearsals): ranks share devices round-robin
-        import torch
-        device = local % max(1, torch.cuda.device_count())
+    P = multi_bit_params() if kind == "multibit" else default_params()
+    ck, sk = generate_keys(P, seed=a.seed)
     ctx = Context(device)
     ctx.set_server_key(sk)
     n = sk.params.lwe_dimension
@@ -360,8 +363,60 @@ def main():
     ctx.d2h(out, d_out)
     ok = all(ck.decrypt_block(out[i]) == (i % 256 % 16 + 1) % 16 for i in range(0, B, max(1, B // 64)))
     if not ok:
-        raise SystemExit("bench: decryption check failed")
+        raise SystemExit(f"bench: decryption check failed ({kind})")
+    for d in (d_in, d_out, d_lut):
+        ctx.free(d)
 
+    br_ms = float(np.mean(br_t))
+    ks_ms = float(np.mean(ks_t))
+    flops_pbs = n * FLOPS_PER_CMUX if kind == "classic" else n // 2 * FLOPS_PER_GROUP_MB
+    achieved = B * flops_pbs / (br_ms * 1e-3) / 1e12
+    ggsw = n if kind == "classic" else n // 2 * 3
+    bsk_bytes = ggsw * 4 * 1024 * 16
+    hbm_bytes = bsk_bytes + B * ((n + 1) * 2 + 2049 * 8 + 4)
+    # every workgroup streams the whole Fourier BSK from L2 (one ciphertext per workgroup): the bytes
+    # the blind rotate moves L2 -> CU per launch, and their rate against the L2 peak
+    l2_bytes = B * bsk_bytes
+    res = {
+        "value": world * B * a.steps / dt,
+        "ms_per_step": dt / a.steps * 1e3,
+        "params": f"n={n},N=2048,k=1,pbs=2^23x1,ks=2^3x5,msg=4,carry=4,grouping={1 if kind == 'classic' else 2}",
+        "roofline": {
+            "bound": "fp64_valu",
+            "compute_pipe": "fp64 VALU (FFT butterflies; no dense contraction on the path)",
+            "kernel": "k_blind_rotate_quad" + ("<1>" if kind == "classic" else "<2>"),
+            "achieved": achieved,
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS,
+            "peak_measured": FP64_PEAK_MEASURED_TFLOPS,
+            "frac_measured": achieved / FP64_PEAK_MEASURED_TFLOPS,
+            "flops_per_pbs": flops_pbs,
+            "kernel_ms": br_ms,
+            "keyswitch_ms": ks_ms,
+            "hbm": {"bound": "hbm", "achieved": hbm_bytes / (br_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": hbm_bytes / (br_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "l2": {"bound": "l2_to_cu", "achieved": l2_bytes / (br_ms * 1e-3) / 1e9, "peak": L2_PEAK_GBS,
+                   "unit": "GB/s", "frac": l2_bytes / (br_ms * 1e-3) / 1e9 / L2_PEAK_GBS,
+                   "bytes_per_launch": l2_bytes},
+        },
+        "pcie_inclusive_pbs_per_s": pcie_rate * world,  # per-rank host-buffer rate x ranks
+    }
+    return ck, ctx, res
+
+
+def main():
+    a = parse()
+    dist, rank, world, local = dist_setup(a.gpus)
+
+    device = local
+    if dist is not None:  # more ranks than visible GPUs (rehearsals): ranks share devices round-robin
+        import torch
+        device = local % max(1, torch.cuda.device_count())
+    B = a.batch
+    # headline: the default (classic) parameters of configs[1]; the multi-bit blind rotation (same
+    # client key, grouping 2) is measured beside it with the same protocol
+    ck, ctx, cl = pbs_leg(a, "classic", dist, rank, world, device)
     ops = None if a.no_ops else ops_legs(ck, ctx, a.seed)
     if ops is not None and dist is not None:
         for k in ops:
@@ -374,23 +429,33 @@ def main():
         fan, fan_hung = with_deadline(lambda: fanout_legs(ck, ctx, dist, rank, world, a.seed), FANOUT_DEADLINE_S)
         if fan_hung:
             fan = {"ranks": world, "error": f"fan-out legs exceeded {FANOUT_DEADLINE_S:.0f} s; abandoned"}
+    mb = None
+    if not a.no_multibit and not fan_hung:
+        ck_mb, ctx_mb, mb = pbs_leg(a, "multibit", dist, rank, world, device)
+        if not a.no_ops:
+            mb_ops = ops_legs(ck_mb, ctx_mb, a.seed)
+            if dist is not None:
+                for k in mb_ops:
+                    mb_ops[k]["seconds"] = allmax(dist, mb_ops[k]["seconds"])
+                mb_ops["sign_fhe_with_k0_batch8_compat"]["signs_per_s"] = (
+                    world * 8 / mb_ops["sign_fhe_with_k0_batch8_compat"]["seconds"])
+            mb["ops"] = mb_ops
+            mb["biguint256_mul_seconds"] = mb_ops["biguint256_mul_compat"]["seconds"]
+            mb["sign_fhe_with_k0_seconds"] = mb_ops["sign_fhe_with_k0_v0_compat"]["seconds"]
+        ctx_mb.close()
 
-    total = world * B * a.steps
-    br_ms = float(np.mean(br_t))
-    ks_ms = float(np.mean(ks_t))
-    flops = B * n * FLOPS_PER_CMUX
-    achieved = flops / (br_ms * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(B)
-    bsk_bytes = n * 4 * 1024 * 16
-    hbm_bytes = bsk_bytes + B * ((n + 1) * 2 + 2049 * 8 + 4)
+    roof = dict(cl["roofline"])
+    roof["traffic"] = traffic
+    roof["traffic_source"] = traffic_src
     res = {
         "metric": METRIC,
-        "value": total / dt,
+        "value": cl["value"],
         "unit": "PBS/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": dt / a.steps * 1e3,
+        "ms_per_step": cl["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -400,27 +465,10 @@ def main():
             "workload": f"batched programmable bootstrap (KS+MS+BR+SE) of {B} 2_2 radix blocks per GPU "
                         "= one PBS level of BigUintFHE 256-bit mul (configs[1])",
             "batch_pbs_per_gpu": B,
-            "params": f"n={n},N=2048,k=1,pbs=2^23x1,ks=2^3x5,msg=4,carry=4",
+            "params": cl["params"],
             "parallelism": f"replicas x{world}",
         },
-        "roofline": {
-            "bound": "fp64_valu",
-            "compute_pipe": "fp64 VALU (FFT butterflies; no dense contraction on the path)",
-            "kernel": "k_blind_rotate_quad",
-            "achieved": achieved,
-            "peak": FP64_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved / FP64_PEAK_TFLOPS,
-            "peak_measured": FP64_PEAK_MEASURED_TFLOPS,
-            "frac_measured": achieved / FP64_PEAK_MEASURED_TFLOPS,
-            "flops_per_pbs": n * FLOPS_PER_CMUX,
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "kernel_ms": br_ms,
-            "keyswitch_ms": ks_ms,
-            "hbm": {"bound": "hbm", "achieved": hbm_bytes / (br_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": hbm_bytes / (br_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
-        },
+        "roofline": roof,
     }
     if ops is not None:
         res["ops"] = ops
@@ -434,7 +482,10 @@ def main():
                   "fheuint8_min": 25.71097148, "fheuint8_and1": 6.418014644, "sign_fhe_with_k0_v0_compat": 4269.0}
         res["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
                                           "speedup": v / ops[k]["seconds"]} for k, v in readme.items() if k in ops}
-    res["pcie_inclusive_pbs_per_s"] = pcie_rate * world  # per-rank host-buffer rate x ranks
+    res["pcie_inclusive_pbs_per_s"] = cl["pcie_inclusive_pbs_per_s"]
+    if mb is not None:
+        # tfhe-rs' MultiBitPBS shape (grouping factor 2) on the same client key: same decrypted results
+        res["multibit"] = mb
     if fan is not None:
         res["fanout"] = fan
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -443,9 +494,6 @@ def main():
         print(json.dumps(res), flush=True)
     if fan_hung:  # a collective of the abandoned legs may still hold the stream: no orderly teardown
         abandon("fan-out legs hung")
-    ctx.free(d_in)
-    ctx.free(d_out)
-    ctx.free(d_lut)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

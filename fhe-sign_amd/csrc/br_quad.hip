@@ -24,6 +24,22 @@
 #include "device_math.h"
 #include "kernels.h"
 
+// G = 2 tuning (A/B): waves per SIMD the kernel is compiled for, and how many registers ahead the
+// key-bundle slice streams in
+#ifndef QMB_W
+#define QMB_W 2
+#endif
+#ifndef QMB_D
+#define QMB_D 3
+#endif
+// the same for the classic (G = 1) kernel
+#ifndef QCL_W
+#define QCL_W 3
+#endif
+#ifndef QCL_D
+#define QCL_D 4
+#endif
+
 namespace fhe {
 
 namespace {
@@ -179,7 +195,14 @@ FHE_DEV void q_xpose_bc(cplx (&x)[8]) {
 // One workgroup (4 waves) per ciphertext.  W = twiddles W[0..512), ps = [2][8][128]: twist factors
 // psi, then the untwist factors (psi.x 2^-51, -psi.y 2^-51): the oracle's 2^-10 and the accumulator's
 // 2^-41, exact scalings.
-__global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __restrict__ ms, int ms_stride,
+//
+// G = blind-rotation grouping (as br_wide.hip): G = 1 classic; G = 2 multi-bit -- the digits of acc
+// itself (no rotation through LDS: two barriers less per step), and at the MAC the key bundle
+// K_rc = sum_B (E[(4j+1) m_B] - 1) G_B,rc per point.  A lane's phase-C points r are
+// j0 + 256 (r & 1) + 128 ((r >> 1) & 1) + 64 (r >> 2): registers r and r + 1 differ by i^m exactly,
+// so each pattern needs one monomial gather per register pair.
+template <int G>
+__global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_quad(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
                                                               const uint32_t* __restrict__ lut_idx,
                                                               const uint64_t* __restrict__ luts,
@@ -187,6 +210,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
                                                               const cplx* __restrict__ W,
                                                               const cplx* __restrict__ ps,
                                                               const cplx* __restrict__ zq,  // quad_zetas
+                                                              const cplx* __restrict__ mono,  // E[4096] (G = 2)
                                                               uint64_t* __restrict__ out, int n) {
     __shared__ __attribute__((aligned(16))) cplx s_x[2][QX_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_w[QTW_SZ];
@@ -230,18 +254,37 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         }
     }
 
+    // G = 2: c4 = 4 j0 + 1 of this lane's phase-C point r = 0 (idx 512 h + 16 u + L0), natural j0 = bitrev
+    const uint32_t c4 = 4u * (__builtin_bitreverse32((uint32_t)(512 * h + 16 * u + l0)) >> 22) + 1u;
     uint32_t a_next = modswitch_2n(a_ct[0]);
-    for (int i = 0; i < n; ++i) {
-        const uint32_t a = a_next;
-        a_next = modswitch_2n(a_ct[i + 1]);
-        if (a == 0) continue;  // X^0 - 1 = 0 (uniform over the workgroup)
+    uint32_t a_next1 = G == 2 ? modswitch_2n(a_ct[1]) : 0u;
+    for (int i = 0; i < n / G; ++i) {
+        uint32_t a = 0, mB[3] = {0u, 0u, 0u};
+        if constexpr (G == 1) {
+            a = a_next;
+            a_next = modswitch_2n(a_ct[i + 1]);
+            if (a == 0) continue;  // X^0 - 1 = 0 (uniform over the workgroup)
+        } else {
+            mB[0] = a_next;
+            mB[1] = a_next1;
+            mB[2] = (a_next + a_next1) & 4095u;
+            if (2 * i + 2 < n) {
+                a_next = modswitch_2n(a_ct[2 * i + 2]);
+                a_next1 = modswitch_2n(a_ct[2 * i + 3]);
+            }
+            if ((mB[0] | mB[1]) == 0) continue;  // X^0 = 1: acc unchanged (uniform)
+        }
         const cplx* Pg = ps;
         asm volatile("" : "+s"(Pg));
         const gcptr P = as_global(Pg) + t;
         // BSK rows for this wave's own digit (row p) and the other polynomial's digit (row 1 - p)
-        const gcptr bm = as_global(bsk) + ((size_t)((i * 2 + p) * 2 + p) * 16 + 8 * h) * 64 + L;
-        const gcptr bo = as_global(bsk) + ((size_t)((i * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 64 + L;
+        // (G = 2: pattern B = 1 of the group; patterns 2, 3 follow at +4 and +8 polynomials)
+        const size_t g0 = G == 1 ? (size_t)i : (size_t)3 * i;
+        const gcptr bm = as_global(bsk) + ((size_t)((g0 * 2 + p) * 2 + p) * 16 + 8 * h) * 64 + L;
+        const gcptr bo = as_global(bsk) + ((size_t)((g0 * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 64 + L;
 
+        cplx x[8];
+        if constexpr (G == 1) {
         // ---- rotate (X^a acc - acc) through the polynomial's region, decompose
 #pragma unroll
         for (int r = 0; r < 16; ++r) rot[128 * r + t] = acc[r];
@@ -257,9 +300,13 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) dg[r] = tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]);
         __syncthreads();  // every rotation read done before the region is reused
-        cplx x[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = make_double2(dg[r], dg[r + 8]);
+        } else {
+        // digits of acc itself: no rotation (the previous step's last barrier guards the region)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 8]));
+        }
 
         // ---- forward transform: twisted Cooley-Tukey (the negacyclic twist is in the zetas)
         {
@@ -278,12 +325,26 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         q_ct<0>(x, s_z[16 + B3], s_z[24 + B3]);
         q_xpose_bc(x);
         // BSK ring head, in flight across phase C and the digit swap
-        constexpr int QR = 4;
-        cplx Bq0[QR], Bq1[QR];
+        constexpr int QR = G == 1 ? QCL_D : QMB_D;
+        cplx Bq0[G == 1 ? QR : 3 * QR], Bq1[G == 1 ? QR : 3 * QR];
+        cplx em[G == 2 ? 3 : 1];  // G = 2: monomials of the current register pair, per pattern
+        const gcptr E = as_global(mono);
+        if constexpr (G == 1) {
 #pragma unroll
         for (int r = 0; r < QR; ++r) {
             Bq0[r] = bm[r * 64];
             Bq1[r] = bo[r * 64];
+        }
+        } else {
+#pragma unroll
+        for (int B = 0; B < 3; ++B) {
+            em[B] = E[(c4 * mB[B]) & 4095u];
+#pragma unroll
+            for (int d = 0; d < QR; ++d) {
+                Bq0[3 * d + B] = bm[B * 4 * 1024 + d * 64];
+                Bq1[3 * d + B] = bo[B * 4 * 1024 + d * 64];
+            }
+        }
         }
         q_ct<2>(x, s_z[32 + B6], s_z[32 + B6]);
         q_ct<1>(x, s_z[96 + B6], s_z[96 + B6]);
@@ -305,6 +366,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
         for (int r = 0; r < 8; ++r) reg[bC + fq(2 * r)] = x[r];
         __syncthreads();
         // mac2 is symmetric in its two rows: own digit x BSK row p, other digit x row 1 - p
+        if constexpr (G == 1) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const cplx Bm = Bq0[r % QR], Bo = Bq1[r % QR];
@@ -313,6 +375,33 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_quad(const uint64_t* __
                 Bq1[r % QR] = bo[(r + QR) * 64];
             }
             x[r] = mac2(x[r], Bm, other[bC + fq(2 * r)], Bo);
+        }
+        } else {
+        // key bundle per point (oracle cmul_acc, patterns in order), then the MAC; the slice of the
+        // next registers stream in behind (QR registers ahead), the monomials per register pair
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            cplx Ko = make_double2(0.0, 0.0), Kt = make_double2(0.0, 0.0);
+            if (r > 0 && !(r & 1)) {  // monomials of this register pair (r, r + 1)
+                const uint32_t cr = c4 + 512u * ((r >> 1) & 1) + 256u * (r >> 2);
+#pragma unroll
+                for (int B = 0; B < 3; ++B) em[B] = E[(cr * mB[B]) & 4095u];
+            }
+#pragma unroll
+            for (int B = 0; B < 3; ++B) {
+                const cplx z = (r & 1) ? qturn(em[B], mB[B] & 3u) : em[B];
+                const cplx w = make_double2(z.x - 1.0, z.y);
+                const int sl = 3 * (r % QR) + B;
+                const cplx Bm = Bq0[sl], Bo = Bq1[sl];
+                if (r + QR < 8) {
+                    Bq0[sl] = bm[B * 4 * 1024 + (r + QR) * 64];
+                    Bq1[sl] = bo[B * 4 * 1024 + (r + QR) * 64];
+                }
+                Ko = cmul_acc(Ko, Bm, w);
+                Kt = cmul_acc(Kt, Bo, w);
+            }
+            x[r] = mac2(x[r], Ko, other[bC + fq(2 * r)], Kt);
+        }
         }
 
         // ---- inverse FFT: stage 9 and phase C in registers, then the region again
@@ -380,10 +469,15 @@ __global__ __launch_bounds__(256) void k_bsk_to_quad(const cplx* __restrict__ sr
 
 hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const cplx* bsk_quad, const cplx* tw, const cplx* ps,
-                                    const cplx* zq, uint64_t* out, int count, int n, hipStream_t s) {
+                                    const cplx* zq, const cplx* mono, int grouping, uint64_t* out, int count, int n,
+                                    hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blind_rotate_quad, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk_quad,
-                       tw, ps, zq, out, n);
+    if (grouping == 2)
+        hipLaunchKernelGGL(k_blind_rotate_quad<2>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
+                           bsk_quad, tw, ps, zq, mono, out, n);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_quad<1>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
+                           bsk_quad, tw, ps, zq, mono, out, n);
     return hipGetLastError();
 }
 

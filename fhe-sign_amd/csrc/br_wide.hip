@@ -154,6 +154,14 @@ FHE_DEV void dit2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
 // Launch bounds: 512 threads, and HIP's second argument is the minimum number of WAVES PER SIMD
 // (amdgpu-waves-per-eu), not workgroups per CU: the 8 waves of the one workgroup a CU holds (144 KB
 // of LDS) are 2 per SIMD, which caps the kernel at 256 VGPRs.
+//
+// G = blind-rotation grouping.  G = 1: one CMUX per key bit (rotation X^a acc - acc through LDS).
+// G = 2 (multi-bit, oracle fho_blind_rotate grouping 2): per pair of key bits the digits of acc
+// itself (no rotation, no rotation barrier) and the key bundle K_rc = sum_B (E[(4j+1) m_B] - 1) G_B,rc
+// (B = 1..3) built per Fourier point before the MAC.  In phase E a lane's four points are
+// j0 + 256 bitrev2(r), so their monomials are E[(4 j0 + 1) m] times i^(bitrev2(r) m): one table gather
+// per pattern, the rest exact quarter turns (wave-uniform).
+template <int G>
 __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
                                                               const uint32_t* __restrict__ lut_idx,
@@ -162,8 +170,9 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                                                               const cplx* __restrict__ tw,   // [12][256]
                                                               const cplx* __restrict__ psiw, // [4][256]
                                                               const cplx* __restrict__ zw,   // [10][256]
+                                                              const cplx* __restrict__ mono, // E[4096] (G = 2)
                                                               uint64_t* __restrict__ out, int n) {
-    __shared__ __attribute__((aligned(16))) double s_rot[2][ROT_SZ];
+    __shared__ __attribute__((aligned(16))) double s_rot[G == 1 ? 2 : 1][G == 1 ? ROT_SZ : 2];
     __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_inv[2][CROSS_SZ];  // inverse E -> D exchange
     __shared__ __attribute__((aligned(16))) cplx s_cd[8][CD_SZ];      // C <-> D, one region per wave
@@ -198,28 +207,36 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             acc[r] = v * 0x1p-41;
         }
     }
-    double* rot_me = s_rot[p];
+    double* rot_me = s_rot[G == 1 ? p : 0];
     cplx* cd = s_cd[w];
     const int gL = L >> 2, aL = L & 3;
     cplx* cross = s_cross[p];
     // lane parts of the linear LDS maps
     const int xD = fx(16 * L + q), xE = fx(256 * q + 4 * L);
 
+    // G = 2: c4 = 4 j0 + 1 of this lane's phase-E point r = 0 (idx 256 q + 4 L, natural j0 = bitrev)
+    const uint32_t c4 = 4u * (__builtin_bitreverse32((uint32_t)(256 * q + 4 * L)) >> 22) + 1u;
+    const gcptr E = as_global(mono);
+
     uint32_t a_next = modswitch_2n(a_ct[0]);
-    for (int i = 0; i < n; ++i) {
+    uint32_t a_next1 = G == 2 ? modswitch_2n(a_ct[1]) : 0u;
+    for (int i = 0; i < n / G; ++i) {
+        cplx x[4];
+        cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
+        uint32_t mB[3] = {0u, 0u, 0u};
+        if constexpr (G == 1) {
         const uint32_t a = a_next;
         a_next = modswitch_2n(a_ct[i + 1]);
         if (a == 0) continue;
 
         // BSK slice for this iteration (issued early; consumed after the forward FFT)
-        cplx B0[4], B1[4];
         {
             const cplx* b0 = bsk + ((size_t)((i * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;        // own digit's row
             const cplx* b1 = bsk + ((size_t)((i * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;  // other digit's row
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                B0[r] = b0[r * 64];
-                B1[r] = b1[r * 64];
+                Kown[r] = b0[r * 64];
+                Koth[r] = b1[r * 64];
             }
         }
 
@@ -230,7 +247,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             rot_me[c + (c >> 2)] = acc[r];
         }
         __syncthreads();
-        cplx x[4];
         double rv[8];  // all 8 rotated reads issued before the first use
         uint32_t uu[8];
 #pragma unroll
@@ -243,6 +259,41 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         for (int r = 0; r < 4; ++r)
             x[r] = make_double2(tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]),
                                 tor_digit_s(neg_bit11(rv[r + 4], uu[r + 4]) - acc[r + 4]));
+        } else {
+        mB[0] = a_next;
+        mB[1] = a_next1;
+        mB[2] = (a_next + a_next1) & 4095u;
+        if (2 * i + 2 < n) {
+            a_next = modswitch_2n(a_ct[2 * i + 2]);
+            a_next1 = modswitch_2n(a_ct[2 * i + 3]);
+        }
+        if ((mB[0] | mB[1]) == 0) continue;  // X^0 = 1: the group leaves acc unchanged (uniform)
+        // key bundle K_rc = sum_B (E[(4j+1) m_B] - 1) G_B,rc (rows p and 1 - p of column p), patterns
+        // in order (oracle cmul_acc); a lane's points r are j0 + 256 bitrev2(r), so their monomials
+        // are i^(bitrev2(r) m_B) E[(4 j0 + 1) m_B]: one gather per pattern, exact quarter turns
+        {
+            cplx e[3];
+#pragma unroll
+            for (int B = 0; B < 3; ++B) e[B] = E[(c4 * mB[B]) & 4095u];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Kown[r] = Koth[r] = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int B = 0; B < 3; ++B) {
+                const gcptr b0 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;
+                const gcptr b1 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const cplx z = qturn(e[B], ((2 * (r & 1) + (r >> 1)) * mB[B]) & 3u);
+                    const cplx wv = make_double2(z.x - 1.0, z.y);
+                    Kown[r] = cmul_acc(Kown[r], b0[r * 64], wv);
+                    Koth[r] = cmul_acc(Koth[r], b1[r * 64], wv);
+                }
+            }
+        }
+        // digits of acc itself (no rotation)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 4]));
+        }
 
         // ---- forward transform (twisted: no twist multiply): A (stages 0,1) -> B -> C -> D
         // (wave-private) -> E (cross-wave)
@@ -277,7 +328,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 
         // ---- pointwise MAC (symmetric: own digit x row p, other digit x row 1 - p)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], B0[r], y[r], B1[r]);
+        for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], Kown[r], y[r], Koth[r]);
 
         // ---- inverse FFT: E -> D (cross-wave) -> C -> B -> A (wave-private)
         {
@@ -332,10 +383,15 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 
 hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const double2* bsk, const double2* tw, const double2* psiw,
-                                    const double2* zw, uint64_t* out, int count, int n, hipStream_t s) {
+                                    const double2* zw, const double2* mono, int grouping, uint64_t* out, int count,
+                                    int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blind_rotate_wide, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk, tw,
-                       psiw, zw, out, n);
+    if (grouping == 2)
+        hipLaunchKernelGGL(k_blind_rotate_wide<2>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts,
+                           bsk, tw, psiw, zw, mono, out, n);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_wide<1>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts,
+                           bsk, tw, psiw, zw, mono, out, n);
     return hipGetLastError();
 }
 

@@ -167,7 +167,7 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
         return FHE_ERR_UNSUPPORTED;
     }
     const size_t ksk_words = (size_t)kBigDim * p.ks_level * (p.n + 1);
-    const int npoly = (int)(p.n * 4);
+    const int npoly = (int)(p.ggsw_count() * 4);
     const size_t bsk_doubles = (size_t)npoly * 1024 * 2;
     if (is_root) {
         rc = nccl_settle(comm, ncclBroadcast(c->d_ksk, c->d_ksk, ksk_words, ncclUint64, root, comm, c->stream),

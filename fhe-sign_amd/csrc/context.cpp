@@ -34,6 +34,19 @@ void fft_tables(std::vector<double2>* W, std::vector<double2>* psi) {
     (*psi)[0] = make_double2(1.0, 0.0);
 }
 
+void mono_table(const std::vector<double2>& psi, std::vector<double2>* E) {
+    E->resize(4096);
+    for (int k = 0; k < 4096; ++k) {  // oracle fho_tables_init: i^(k >> 10) psi[k & 1023], moves only
+        const double2 z = psi[k & 1023];
+        switch (k >> 10) {
+            case 0: (*E)[k] = z; break;
+            case 1: (*E)[k] = make_double2(-z.y, z.x); break;
+            case 2: (*E)[k] = make_double2(-z.x, -z.y); break;
+            default: (*E)[k] = make_double2(z.y, -z.x); break;
+        }
+    }
+}
+
 // zeta(s, b) at [2^s + b] of the twisted forward transform: same expressions and order as
 // oracle/tfhe_oracle.c:fho_tables_init (exp(i pi (4 bitrev_s(b) + 1) / 2^(s+2)), odd b = i * even)
 void zeta_table(std::vector<double2>* Z) {
@@ -264,10 +277,10 @@ hipError_t fhe_ctx::keyswitch(const uint64_t* in, const fhe::PbsDesc* desc, size
 
 hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_idx, uint64_t* out, size_t count) {
     if ((int)count <= wide_threshold)
-        return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide, d_zeta_wide, out,
-                                        (int)count, (int)p.n, stream);
+        return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
+                                        d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
     return launch_blind_rotate_quad(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_quad, d_tw_quad, d_psi_quad,
-                                    d_zeta_quad, out, (int)count, (int)p.n, stream);
+                                    d_zeta_quad, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
 }
 
 // =========================================================================== C ABI (core)
@@ -278,6 +291,14 @@ const char* fhe_last_error(void) { return fhe::last_error(); }
 int fhe_params_default(fhe_params* out) {
     if (!out) return FHE_ERR_INVALID;
     *out = Params().to_c();
+    return FHE_OK;
+}
+
+int fhe_params_multi_bit(fhe_params* out) {
+    if (!out) return FHE_ERR_INVALID;
+    Params p;
+    p.grouping = 2;
+    *out = p.to_c();
     return FHE_OK;
 }
 
@@ -357,32 +378,36 @@ int generate_device(fhe_ctx* c, const fhe_params* params, const KeyWords& seed, 
         generate_secret_keys(p, seed, cko.get());
         sko->params = p;
         sko->ksk.resize((size_t)kPolySize * p.ks_level * (p.n + 1));
-        sko->bsk.resize((size_t)p.n * 4 * kPolySize);
+        sko->bsk.resize((size_t)p.ggsw_count() * 4 * kPolySize);
     } catch (const std::exception& e) {
         set_error(std::string("keygen failed: ") + e.what());
         return FHE_ERR_ALLOC;
     }
     FHE_HIP_CHECK(hipSetDevice(c->device));
     const size_t kw = sko->ksk.size(), bw = sko->bsk.size();
-    uint64_t *d_ksk = nullptr, *d_bsk = nullptr, *d_lwe = nullptr, *d_glwe = nullptr;
+    uint64_t *d_ksk = nullptr, *d_bsk = nullptr, *d_lwe = nullptr, *d_glwe = nullptr, *d_msg = nullptr;
     auto release = [&] {
-        for (uint64_t* q : {d_ksk, d_bsk, d_lwe, d_glwe})
+        for (uint64_t* q : {d_ksk, d_bsk, d_lwe, d_glwe, d_msg})
             if (q) (void)hipFree(q);
     };
+    const uint32_t ngg = p.ggsw_count();
+    std::vector<uint64_t> msgs(ngg);  // per-GGSW messages (key bits or multi-bit pattern indicators)
+    for (uint32_t q = 0; q < ngg; ++q) msgs[q] = p.ggsw_message(cko->lwe_sk.data(), q);
     hipError_t e = hipSuccess;
     auto step = [&](hipError_t r) {
         if (e == hipSuccess && r != hipSuccess) e = r;
         return e == hipSuccess;
     };
     step(hipMalloc(&d_ksk, kw * 8)) && step(hipMalloc(&d_bsk, bw * 8)) && step(hipMalloc(&d_lwe, p.n * 8)) &&
-        step(hipMalloc(&d_glwe, kPolySize * 8)) &&
+        step(hipMalloc(&d_glwe, kPolySize * 8)) && step(hipMalloc(&d_msg, ngg * 8)) &&
+        step(hipMemcpyAsync(d_msg, msgs.data(), ngg * 8, hipMemcpyHostToDevice, c->stream)) &&
         step(hipMemcpyAsync(d_lwe, cko->lwe_sk.data(), p.n * 8, hipMemcpyHostToDevice, c->stream)) &&
         step(hipMemcpyAsync(d_glwe, cko->glwe_sk.data(), kPolySize * 8, hipMemcpyHostToDevice, c->stream)) &&
         step(launch_chacha_u64(chacha_stream_key(seed.data(), kStreamKsk), d_ksk, kw, c->stream)) &&
         step(launch_ksk_bodies(d_ksk, d_lwe, d_glwe, (int)p.n, (int)(kPolySize * p.ks_level), (int)p.ks_level,
                                (int)p.ks_base_log, (int)p.lwe_noise_log2, c->stream)) &&
         step(launch_chacha_u64(chacha_stream_key(seed.data(), kStreamBsk), d_bsk, bw, c->stream)) &&
-        step(launch_bsk_bodies(d_bsk, d_lwe, d_glwe, (int)p.n, (int)p.pbs_base_log, (int)p.glwe_noise_log2,
+        step(launch_bsk_bodies(d_bsk, d_msg, d_glwe, (int)ngg, (int)p.pbs_base_log, (int)p.glwe_noise_log2,
                                c->stream)) &&
         step(hipMemcpyAsync(sko->ksk.data(), d_ksk, kw * 8, hipMemcpyDeviceToHost, c->stream)) &&
         step(hipMemcpyAsync(sko->bsk.data(), d_bsk, bw * 8, hipMemcpyDeviceToHost, c->stream));
@@ -390,6 +415,7 @@ int generate_device(fhe_ctx* c, const fhe_params* params, const KeyWords& seed, 
     // another process, could read them): clear them on the stream before the buffers are released
     if (d_lwe) (void)hipMemsetAsync(d_lwe, 0, p.n * 8, c->stream);
     if (d_glwe) (void)hipMemsetAsync(d_glwe, 0, kPolySize * 8, c->stream);
+    if (d_msg) (void)hipMemsetAsync(d_msg, 0, ngg * 8, c->stream);
     step(hipStreamSynchronize(c->stream));
     release();
     if (e != hipSuccess) {
@@ -514,6 +540,10 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
     FHE_HIP_CHECK(hipMemcpy(c->d_tw_wide, tww.data(), tww.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMemcpy(c->d_psi_wide, psiw.data(), psiw.size() * sizeof(double2), hipMemcpyHostToDevice));
     if (const char* e = getenv("FHE_WIDE_THRESHOLD")) c->wide_threshold = atoi(e);
+    std::vector<double2> mono;
+    mono_table(psi, &mono);
+    FHE_HIP_CHECK(hipMalloc(&c->d_mono, mono.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMemcpy(c->d_mono, mono.data(), mono.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMalloc(&c->d_W, W.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMalloc(&c->d_psi, psi.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_W, W.data(), W.size() * sizeof(double2), hipMemcpyHostToDevice));
@@ -530,7 +560,7 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     c->engine = nullptr;
     c->release_comm();
     void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
-                    c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
+                    c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_mono, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)
@@ -559,7 +589,7 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     FHE_HIP_CHECK(hipMemcpyAsync(c->d_ksk, sk->ksk.data(), sk->ksk.size() * 8, hipMemcpyHostToDevice, c->stream));
     FHE_HIP_CHECK(hipMalloc(&c->d_ksk_planes, fhe::ks_planes_bytes((int)p.n)));
     FHE_HIP_CHECK(launch_ksk_to_planes(c->d_ksk, (int)p.n, c->d_ksk_planes, c->stream));
-    const int npoly = (int)(p.n * 4);
+    const int npoly = (int)(p.ggsw_count() * 4);
     uint64_t* d_std = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d_std, sk->bsk.size() * 8));
     FHE_HIP_CHECK(hipMalloc(&c->d_bsk, (size_t)npoly * 1024 * sizeof(double2)));
@@ -589,7 +619,7 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
 
 int fhe_ctx_export_fourier_bsk(fhe_ctx* c, double* out, size_t len) {
     if (!c || !c->has_key) return FHE_ERR_NO_KEY;
-    const size_t need = (size_t)c->p.n * 4 * 1024 * 2;
+    const size_t need = (size_t)c->p.ggsw_count() * 4 * 1024 * 2;
     if (len < need) {
         set_error("buffer too small");
         return FHE_ERR_INVALID;

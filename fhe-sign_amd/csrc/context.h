@@ -34,6 +34,8 @@ void wide_tables(const std::vector<double2>& W, const std::vector<double2>& psi,
                  std::vector<double2>* psiw);
 // Accumulator polynomial of a univariate LUT (tfhe shortint box encoding, padding bit).
 void make_lut_poly(const Params& p, const uint32_t* f, std::vector<uint64_t>* lut);
+// E[k] = exp(i pi k / 2048), k < 4096, as i^(k >> 10) psi[k & 1023] exactly (oracle fho_monomials)
+void mono_table(const std::vector<double2>& psi, std::vector<double2>* E);
 
 }  // namespace fhe
 
@@ -53,6 +55,7 @@ struct fhe_ctx {
     double2* d_psi_quad = nullptr;  // [2][8][128]: twist (unused since the twisted forward), untwist
     double2* d_zeta_quad = nullptr; // br_quad.hip zeta layout (context.cpp:quad_zetas)
     double2* d_zeta_wide = nullptr; // [10][256] (context.cpp:wide_zetas)
+    double2* d_mono = nullptr;      // monomial table E[4096] of the multi-bit blind rotation (mono_table)
     int br_kernel = FHE_BR_QUAD;    // throughput kernel for levels above wide_threshold
     int8_t* d_ksk_planes = nullptr; // KSK as balanced signed-byte planes (ks_mfma.hip)
     int ks_kernel = FHE_KS_MFMA;

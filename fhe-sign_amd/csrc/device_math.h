@@ -61,6 +61,16 @@ FHE_DEV cplx mac2(cplx d0, cplx b0, cplx d1, cplx b1) {
     o.y = __fma_rn(d0.x, b0.y, d0.y * b0.x) + __fma_rn(d1.x, b1.y, d1.y * b1.x);
     return o;
 }
+// key-bundle accumulation of the multi-bit blind rotation (oracle fho_blind_rotate, grouping 2):
+// k + g w with the product's rounding fused into the accumulation, k starting at +0
+FHE_DEV cplx cmul_acc(cplx k, cplx g, cplx w) {
+    return make_double2(__fma_rn(g.x, w.x, __fma_rn(-g.y, w.y, k.x)), __fma_rn(g.x, w.y, __fma_rn(g.y, w.x, k.y)));
+}
+// i^t z for t = 0..3 (exact: moves and sign flips; t is wave-uniform at every call site)
+FHE_DEV cplx qturn(cplx z, uint32_t t) {
+    const cplx a = (t & 1) ? make_double2(-z.y, z.x) : z;
+    return (t & 2) ? make_double2(-a.x, -a.y) : a;
+}
 FHE_DEV cplx cadd(cplx a, cplx b) { return make_double2(a.x + b.x, a.y + b.y); }
 FHE_DEV cplx csub(cplx a, cplx b) { return make_double2(a.x - b.x, a.y - b.y); }
 FHE_DEV cplx conj_(cplx a) { return make_double2(a.x, -a.y); }

@@ -44,14 +44,17 @@ hipError_t launch_keyswitch(const uint64_t* in, int count, const uint64_t* ksk, 
 hipError_t launch_keyswitch_desc(const PbsDesc* desc, int count, const uint64_t* ksk, uint64_t* small,
                                  int ks_stride, int n, hipStream_t s);
 // latency kernel: one ciphertext per 512-thread workgroup (br_wide.hip); desc or lut_idx/out mode
+// grouping 1 (classic) or 2 (multi-bit: bsk holds 3 GGSWs per pair of key bits, mono = E[4096])
 hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const double2* bsk, const double2* tw, const double2* psiw,
-                                    const double2* zw, uint64_t* out, int count, int n, hipStream_t s);
+                                    const double2* zw, const double2* mono, int grouping, uint64_t* out, int count,
+                                    int n, hipStream_t s);
 // dst_i = sum_t coef * src + cst, no bootstrap (linear radix ops)
 hipError_t launch_lincomb(const PbsDesc* desc, int count, hipStream_t s);
 hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const double2* bsk_quad, const double2* tw, const double2* ps,
-                                    const double2* zq, uint64_t* out, int count, int n, hipStream_t s);
+                                    const double2* zq, const double2* mono, int grouping, uint64_t* out, int count,
+                                    int n, hipStream_t s);
 hipError_t launch_bsk_to_quad(const double2* bsk, int npoly, double2* out, hipStream_t s);
 // dst[i][0..2049) = src[i * 2049 ..] for i < count (all-gathered level outputs -> block slots)
 hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s);

@@ -17,8 +17,8 @@ hipError_t launch_chacha_u64(const ChaChaKey& k, uint64_t* out, uint64_t count, 
 // ksk holds the KSK stream words ([rows][n + 1], rows = N * levels): bodies computed in place
 hipError_t launch_ksk_bodies(uint64_t* ksk, const uint64_t* lwe_sk, const uint64_t* glwe_sk, int n, int rows,
                              int levels, int base_log, int noise_log2, hipStream_t s);
-// bsk holds the BSK stream words ([n][2][2][N]): bodies, then gadgets, in place
-hipError_t launch_bsk_bodies(uint64_t* bsk, const uint64_t* lwe_sk, const uint64_t* glwe_sk, int n, int pbs_base_log,
+// bsk holds the BSK stream words ([nggsw][2][2][N]): bodies, then gadgets (msgs[i] << ...), in place
+hipError_t launch_bsk_bodies(uint64_t* bsk, const uint64_t* msgs, const uint64_t* glwe_sk, int nggsw, int pbs_base_log,
                              int noise_log2, hipStream_t s);
 
 }  // namespace fhe

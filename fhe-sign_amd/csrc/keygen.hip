@@ -81,9 +81,10 @@ __global__ __launch_bounds__(256) void k_ksk_bodies(uint64_t* __restrict__ ksk, 
 }
 
 // One workgroup per BSK row (i, row): B = e + A * S mod (X^N + 1) (S binary), then the gadget
-// s_i << (64 - pbs_base_log) on A[0] (row 0) or B[0] (row 1).  A and S staged in LDS; each thread
+// m_i << (64 - pbs_base_log) on A[0] (row 0) or B[0] (row 1); m_i = the GGSW's message (s_i, or the
+// multi-bit pattern indicator: Params::ggsw_message).  A and S staged in LDS; each thread
 // owns 8 output coefficients and runs over all N terms (selects, no divergence).
-__global__ __launch_bounds__(256) void k_bsk_bodies(uint64_t* __restrict__ bsk, const uint64_t* __restrict__ lwe_sk,
+__global__ __launch_bounds__(256) void k_bsk_bodies(uint64_t* __restrict__ bsk, const uint64_t* __restrict__ msgs,
                                                     const uint64_t* __restrict__ glwe_sk, int pbs_base_log,
                                                     int noise_log2) {
     constexpr int N = 2048;
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void k_bsk_bodies(uint64_t* __restrict__ bsk, 
             acc[k] += (d >= 0 ? a : 0ull - a) & s;
         }
     }
-    const uint64_t g = lwe_sk[i] << (64 - pbs_base_log);
+    const uint64_t g = msgs[i] << (64 - pbs_base_log);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int m = threadIdx.x + 256 * k;
@@ -144,9 +145,9 @@ hipError_t launch_ksk_bodies(uint64_t* ksk, const uint64_t* lwe_sk, const uint64
     return hipGetLastError();
 }
 
-hipError_t launch_bsk_bodies(uint64_t* bsk, const uint64_t* lwe_sk, const uint64_t* glwe_sk, int n, int pbs_base_log,
+hipError_t launch_bsk_bodies(uint64_t* bsk, const uint64_t* msgs, const uint64_t* glwe_sk, int nggsw, int pbs_base_log,
                              int noise_log2, hipStream_t s) {
-    k_bsk_bodies<<<2 * n, 256, 0, s>>>(bsk, lwe_sk, glwe_sk, pbs_base_log, noise_log2);
+    k_bsk_bodies<<<2 * nggsw, 256, 0, s>>>(bsk, msgs, glwe_sk, pbs_base_log, noise_log2);
     return hipGetLastError();
 }
 

@@ -38,6 +38,12 @@ bool Params::from_c(const fhe_params& c, Params* out, const char** why) {
         *why = "noise bound too large";
         return false;
     }
+    const uint32_t g = c.grouping == 0 ? 1 : c.grouping;  // 0 (a zero-initialised struct) = classic
+    if (g > 2 || c.lwe_dimension % g) {
+        *why = "grouping must be 1 (classic) or 2 (multi-bit) and divide lwe_dimension";
+        return false;
+    }
+    out->grouping = g;
     out->n = c.lwe_dimension;
     out->pbs_base_log = c.pbs_base_log;
     out->ks_base_log = c.ks_base_log;
@@ -62,6 +68,7 @@ fhe_params Params::to_c() const {
     c.glwe_noise_log2 = glwe_noise_log2;
     c.message_modulus = message_modulus;
     c.carry_modulus = carry_modulus;
+    c.grouping = grouping;
     return c;
 }
 
@@ -214,13 +221,14 @@ void generate_keys(const Params& p, const KeyWords& seed, fhe_client_key* ck, fh
             }
     }
 
-    // BSK[i] = GGSW_{S}(s_i): rows r = 0 (mask gadget), 1 (body gadget), one level.
-    // Masks and noises are drawn sequentially (deterministic stream), the exact A*S products are
-    // then computed in parallel on the host.
-    sk->bsk.assign((size_t)n * 4 * N, 0);
+    // BSK[q] = GGSW_{S}(m_q): rows r = 0 (mask gadget), 1 (body gadget), one level; m_q = s_q
+    // (classic) or the multi-bit pattern indicator (Params::ggsw_message).  Masks and noises are drawn
+    // sequentially (deterministic stream), the exact A*S products are then computed in parallel.
+    const uint32_t ngg = p.ggsw_count();
+    sk->bsk.assign((size_t)ngg * 4 * N, 0);
     {
         ChaChaStream r(seed, kStreamBsk);
-        for (uint32_t i = 0; i < n; ++i)
+        for (uint32_t i = 0; i < ngg; ++i)
             for (int row = 0; row < 2; ++row) {
                 uint64_t* A = sk->bsk.data() + (((size_t)i * 2 + row) * 2 + 0) * N;
                 uint64_t* B = sk->bsk.data() + (((size_t)i * 2 + row) * 2 + 1) * N;
@@ -228,7 +236,7 @@ void generate_keys(const Params& p, const KeyWords& seed, fhe_client_key* ck, fh
                 for (uint32_t j = 0; j < N; ++j) B[j] = (uint64_t)r.tuniform(p.glwe_noise_log2);
             }
     }
-    const uint32_t rows = n * 2;
+    const uint32_t rows = ngg * 2;
     unsigned nth = std::thread::hardware_concurrency();
     if (nth == 0) nth = 4;
     if (nth > 16) nth = 16;
@@ -240,7 +248,7 @@ void generate_keys(const Params& p, const KeyWords& seed, fhe_client_key* ck, fh
                 uint64_t* B = sk->bsk.data() + ((size_t)q * 2 + 1) * N;
                 negacyclic_binary_mac(B, A, ck->glwe_sk.data());
                 const uint32_t i = q / 2, row = q % 2;
-                const uint64_t g = ck->lwe_sk[i] << (64 - p.pbs_base_log);
+                const uint64_t g = p.ggsw_message(ck->lwe_sk.data(), i) << (64 - p.pbs_base_log);
                 if (row == 0) A[0] += g; else B[0] += g;
             }
         });

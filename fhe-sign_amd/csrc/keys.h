@@ -26,11 +26,24 @@ struct Params {
     uint32_t glwe_noise_log2 = 17;
     uint32_t message_modulus = 4;
     uint32_t carry_modulus = 4;
+    // blind-rotation grouping factor: 1 = one CMUX per key bit (tfhe-rs' classic PBS), 2 = multi-bit
+    // (tfhe-rs' MultiBitPBS shape: two key bits per external product, 3 GGSWs per pair of bits)
+    uint32_t grouping = 1;
 
     static bool from_c(const fhe_params& c, Params* out, const char** why);
     fhe_params to_c() const;
     uint64_t delta() const { return (1ull << 63) / ((uint64_t)message_modulus * carry_modulus); }
     uint32_t msg_carry() const { return message_modulus * carry_modulus; }
+    // GGSWs in the bootstrapping key: n (classic) or (n / g)(2^g - 1) (multi-bit)
+    uint32_t ggsw_count() const { return grouping == 1 ? n : n / grouping * ((1u << grouping) - 1); }
+    // the message of GGSW q: s_q (classic); multi-bit group i = q / 3, pattern B = q % 3 + 1 of
+    // (s_2i, s_2i+1): f_B = [s_2i = B bit 0][s_2i+1 = B bit 1] (oracle fho_keygen)
+    uint64_t ggsw_message(const uint64_t* lwe_sk, uint32_t q) const {
+        if (grouping == 1) return lwe_sk[q];
+        const uint32_t i = q / 3, B = q % 3 + 1;
+        const uint64_t s0 = lwe_sk[2 * i] & 1, s1 = lwe_sk[2 * i + 1] & 1;
+        return ((B & 1) ? s0 : 1 - s0) & ((B & 2) ? s1 : 1 - s1);
+    }
 };
 
 // The 256-bit ChaCha20 key every key-generation stream is derived from (stream id = nonce word 0).

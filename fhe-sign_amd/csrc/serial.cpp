@@ -13,7 +13,7 @@ static const char kMagic[8] = {'F', 'H', 'E', 'R', 'O', 'C', 'M', '\0'};
 
 void Writer::params(const Params& p) {
     for (uint32_t v : {p.n, p.pbs_base_log, p.ks_base_log, p.ks_level, p.lwe_noise_log2, p.glwe_noise_log2,
-                       p.message_modulus, p.carry_modulus})
+                       p.message_modulus, p.carry_modulus, p.grouping})
         u32(v);
 }
 
@@ -27,6 +27,7 @@ bool Reader::params(Params* out, std::string* why) {
     p.glwe_noise_log2 = u32();
     p.message_modulus = u32();
     p.carry_modulus = u32();
+    p.grouping = version >= 2 ? u32() : 1;
     if (!ok) {
         *why = "truncated parameters";
         return false;
@@ -75,7 +76,7 @@ bool unframe(const uint8_t* buf, size_t len, Kind kind, Reader* payload, std::st
     Reader h{buf + 8, kHeaderBytes - 8};
     const uint32_t version = h.u32(), k = h.u32();
     const uint64_t plen = h.u64(), sum = h.u64();
-    if (version != kVersion) {
+    if (version < 1 || version > kVersion) {
         *why = "unsupported format version";
         return false;
     }
@@ -92,6 +93,7 @@ bool unframe(const uint8_t* buf, size_t len, Kind kind, Reader* payload, std::st
         return false;
     }
     *payload = Reader{buf + kHeaderBytes, (size_t)plen};
+    payload->version = version;
     return true;
 }
 
@@ -114,7 +116,7 @@ using namespace fhe::ser;
 
 namespace {
 size_t ksk_words(const Params& p) { return (size_t)kPolySize * p.ks_level * (p.n + 1); }
-size_t bsk_words(const Params& p) { return (size_t)p.n * 2 * 2 * kPolySize; }
+size_t bsk_words(const Params& p) { return (size_t)p.ggsw_count() * 2 * 2 * kPolySize; }
 bool binary(const std::vector<uint64_t>& v) {
     for (uint64_t x : v)
         if (x > 1) return false;

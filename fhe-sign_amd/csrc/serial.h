@@ -3,10 +3,11 @@
 // The reference never serializes (keys are regenerated per run; `grep serial` hits only a doc
 // comment, src/schnorr.rs:47); tfhe-rs's bincode + tfhe-versionable wire format cannot be pinned
 // here (no tfhe-rs fixture, crate absent), so this is this engine's own format, little-endian:
-//   header  magic "FHEROCM\0" | u32 version (1) | u32 kind | u64 payload bytes | u64 checksum
+//   header  magic "FHEROCM\0" | u32 version (2; 1 still read) | u32 kind | u64 payload bytes | u64 checksum
 //           (FNV-1a over the payload's little-endian u64 words, tail zero-padded)
-//   payload params (8 x u32: n, pbs_base_log, ks_base_log, ks_level, lwe/glwe noise log2, msg,
-//           carry) then the kind's fields (serial.cpp / capi_radix.cpp).
+//   payload params (9 x u32: n, pbs_base_log, ks_base_log, ks_level, lwe/glwe noise log2, msg,
+//           carry, grouping -- version 1 has no grouping word: classic) then the kind's fields
+//           (serial.cpp / capi_radix.cpp).
 // Readers check magic, version, kind, length, checksum, parameter ranges and every count before
 // touching memory, and refuse block metadata (degree, noise) outside the radix layer's budget, so a
 // corrupted or hostile buffer fails with FHE_ERR_INVALID instead of poisoning the scheduler.
@@ -22,7 +23,7 @@
 namespace fhe::ser {
 
 enum Kind : uint32_t { kClientKey = 1, kServerKey = 2, kRadix = 3, kBigUint = 4 };
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;  // 2: params carry the blind-rotation grouping (9th word); 1 still read
 constexpr size_t kHeaderBytes = 32;
 
 struct Writer {
@@ -42,6 +43,7 @@ struct Reader {
     const uint8_t* p = nullptr;
     size_t n = 0, off = 0;
     bool ok = true;
+    uint32_t version = kVersion;  // of the frame (unframe sets it)
     bool take(void* dst, size_t k) {
         if (!ok || n - off < k) return ok = false;
         memcpy(dst, p + off, k);

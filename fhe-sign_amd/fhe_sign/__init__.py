@@ -8,7 +8,8 @@ Mirrors the reference crate's surface (coset-io/fhe-sign):
 All ciphertext arithmetic runs on the GPU through lib/libfhe_rocm.so; this package only marshals.
 """
 from ._lib import FheError, FheParams, load  # noqa: F401
-from .core import ClientKey, Context, ServerKey, comm_unique_id, default_params, generate_keys  # noqa: F401
+from .core import (ClientKey, Context, ServerKey, comm_unique_id, default_params, generate_keys,  # noqa: F401
+                   multi_bit_params)
 from .integer import (  # noqa: F401,E402
     COMPAT, FAST, PUBLIC, BigUintFHE, FheBool, FheUint, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, set_server_key,
     stats, to_u32_digits)

@@ -24,13 +24,19 @@ class FheParams(C.Structure):
     _fields_ = [(name, C.c_uint32) for name in (
         "lwe_dimension", "glwe_dimension", "polynomial_size", "pbs_base_log", "pbs_level",
         "ks_base_log", "ks_level", "lwe_noise_log2", "glwe_noise_log2", "message_modulus",
-        "carry_modulus")]
+        "carry_modulus", "grouping")]
+
+    def ggsw_count(self) -> int:
+        """GGSWs in the bootstrapping key: n (classic) or (n / g)(2^g - 1) (multi-bit)"""
+        g = self.grouping or 1
+        return self.lwe_dimension if g == 1 else self.lwe_dimension // g * ((1 << g) - 1)
 
 
 # (name, restype, argtypes) -- every symbol include/fhe_rocm.h declares
 _SIGNATURES = [
     ("fhe_last_error", C.c_char_p, []),
     ("fhe_params_default", C.c_int, [C.POINTER(FheParams)]),
+    ("fhe_params_multi_bit", C.c_int, [C.POINTER(FheParams)]),
     ("fhe_generate_keys", C.c_int, [C.POINTER(FheParams), C.c_uint64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     ("fhe_generate_keys_device", C.c_int,
      [C.c_void_p, C.POINTER(FheParams), C.c_uint64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),

@@ -16,6 +16,13 @@ def default_params() -> FheParams:
     return p
 
 
+def multi_bit_params() -> FheParams:
+    """default parameters with the multi-bit blind rotation (grouping 2; fhe_params.grouping)"""
+    p = FheParams()
+    check(load().fhe_params_multi_bit(C.byref(p)))
+    return p
+
+
 class ClientKey:
     def __init__(self, handle, params: FheParams):
         self._h = handle
@@ -100,7 +107,7 @@ class ServerKey:
         p = self.params
         n, N, L = p.lwe_dimension, p.polynomial_size, p.ks_level
         ksk = np.zeros(N * L * (n + 1), np.uint64)
-        bsk = np.zeros(n * 4 * N, np.uint64)
+        bsk = np.zeros(p.ggsw_count() * 4 * N, np.uint64)
         check(load().fhe_server_key_export(self._h, ptr(ksk), ksk.size, ptr(bsk), bsk.size))
         return ksk, bsk
 
@@ -165,8 +172,7 @@ class Context:
         self.params = sk.params
 
     def export_fourier_bsk(self) -> np.ndarray:
-        n = self.params.lwe_dimension
-        out = np.zeros(n * 4 * 1024 * 2, np.float64)
+        out = np.zeros(self.params.ggsw_count() * 4 * 1024 * 2, np.float64)
         check(load().fhe_ctx_export_fourier_bsk(self._h, ptr(out, C.c_double), out.size))
         return out
 

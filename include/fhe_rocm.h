@@ -49,6 +49,10 @@ typedef struct fhe_params {
     uint32_t glwe_noise_log2; /* TUniform bound, big/GLWE key (17) */
     uint32_t message_modulus; /* 4 */
     uint32_t carry_modulus;   /* 4 */
+    uint32_t grouping;        /* blind rotation: 1 = classic (one CMUX per key bit, tfhe-rs'
+                                 ClassicPBS, the default), 2 = multi-bit (tfhe-rs' MultiBitPBS shape:
+                                 two key bits per external product, 3 GGSWs per pair; the client key
+                                 and every decrypted result are unchanged).  0 is read as 1. */
 } fhe_params;
 
 typedef struct fhe_client_key fhe_client_key;
@@ -57,6 +61,9 @@ typedef struct fhe_ctx fhe_ctx;
 
 const char* fhe_last_error(void);
 int fhe_params_default(fhe_params* out);
+/* The default parameters with the multi-bit blind rotation (grouping 2): same client key shape, same
+ * keyswitch, 1.5x the bootstrapping-key size, half the serial CMUX chain (see fhe_params.grouping). */
+int fhe_params_multi_bit(fhe_params* out);
 
 /* ---------------------------------------------------------------------------------- keys */
 /* Replaces tfhe::generate_keys(config) (src/schnorr.rs:441-442, src/biguint.rs:277,

@@ -34,6 +34,12 @@ void fho_default_params(fho_params* p) {
     p->glwe_noise_log2 = 17;
     p->message_modulus = 4;
     p->carry_modulus = 4;
+    p->grouping = 1;
+}
+
+uint32_t fho_ggsw_count(const fho_params* p) {
+    const uint32_t g = p->grouping ? p->grouping : 1;
+    return g == 1 ? p->n : p->n / g * ((1u << g) - 1);
 }
 
 /* ------------------------------------------------------------------ ChaCha20 (RFC 8439) */
@@ -94,6 +100,7 @@ int64_t fho_rng_tuniform(fho_rng* r, uint32_t b) {
 static double g_tw[512 * 2];
 static double g_psi[1024 * 2];
 static double g_zeta[1024 * 2];
+static double g_mono[4096 * 2];
 static int g_tables_ready = 0;
 
 static uint32_t bitrev(uint32_t b, int bits) {
@@ -139,12 +146,23 @@ void fho_tables_init(void) {
             }
         }
     }
+    for (int k = 0; k < 4096; ++k) { /* E[k] = i^(k >> 10) psi[k & 1023], exact moves */
+        const double re = g_psi[2 * (k & 1023)], im = g_psi[2 * (k & 1023) + 1];
+        double* e = g_mono + 2 * k;
+        switch (k >> 10) {
+            case 0: e[0] = re; e[1] = im; break;
+            case 1: e[0] = -im; e[1] = re; break;
+            case 2: e[0] = -re; e[1] = -im; break;
+            default: e[0] = im; e[1] = -re; break;
+        }
+    }
     g_tables_ready = 1;
 }
 
 const double* fho_twiddles(void) { fho_tables_init(); return g_tw; }
 const double* fho_twist(void) { fho_tables_init(); return g_psi; }
 const double* fho_zetas(void) { fho_tables_init(); return g_zeta; }
+const double* fho_monomials(void) { fho_tables_init(); return g_mono; }
 
 /* (x) * (w): the single complex-multiply formula used everywhere (GPU identical) */
 static inline void cmul(double xr, double xi, double wr, double wi, double* yr, double* yi) {
@@ -310,8 +328,10 @@ int fho_keygen(fho_keys* k, const fho_params* p, uint64_t seed) {
     k->lwe_sk = (uint64_t*)calloc(n, 8);
     k->glwe_sk = (uint64_t*)calloc(FHO_N, 8);
     k->ksk = (uint64_t*)calloc((size_t)FHO_N * L * (n + 1), 8);
-    k->bsk = (uint64_t*)calloc((size_t)n * 4 * FHO_N, 8);
-    k->bsk_f = (double*)calloc((size_t)n * 4 * FHO_HALF * 2, 8);
+    const uint32_t ngg = fho_ggsw_count(p);
+    if (p->grouping < 1 || p->grouping > 2 || n % p->grouping) return -1;
+    k->bsk = (uint64_t*)calloc((size_t)ngg * 4 * FHO_N, 8);
+    k->bsk_f = (double*)calloc((size_t)ngg * 4 * FHO_HALF * 2, 8);
     if (!k->lwe_sk || !k->glwe_sk || !k->ksk || !k->bsk || !k->bsk_f) return -1;
 
     fho_rng r;
@@ -334,22 +354,34 @@ int fho_keygen(fho_keys* k, const fho_params* p, uint64_t seed) {
         }
     }
 
-    fho_rng_init(&r, seed, 3); /* BSK: GGSW_S(s_i), one level, base 2^pbs_base_log */
+    /* BSK: GGSW_S(m_q), one level, base 2^pbs_base_log.  Classic: m_q = s_q.  Multi-bit (grouping
+     * 2): group i holds q = 3 i + B - 1 for the patterns B = 1, 2, 3 of (s_2i, s_2i+1) (bit t of B
+     * <-> s_2i+t), m_q = f_B = [s_2i = B_0][s_2i+1 = B_1]; then X^(a_2i s_2i + a_2i+1 s_2i+1) =
+     * 1 + sum_B f_B (X^(m_B) - 1) with m_B = sum_t B_t a_2i+t. */
+    fho_rng_init(&r, seed, 3);
     uint64_t* e = (uint64_t*)malloc(FHO_N * 8);
-    for (uint32_t i = 0; i < n; ++i) {
+    for (uint32_t q = 0; q < ngg; ++q) {
+        uint64_t msg;
+        if (p->grouping == 1) {
+            msg = k->lwe_sk[q];
+        } else {
+            const uint32_t i = q / 3, B = q % 3 + 1;
+            const uint64_t s0 = k->lwe_sk[2 * i], s1 = k->lwe_sk[2 * i + 1];
+            msg = ((B & 1) ? s0 : 1 - s0) & ((B & 2) ? s1 : 1 - s1);
+        }
         for (int row = 0; row < 2; ++row) {
-            uint64_t* A = k->bsk + (((size_t)i * 2 + row) * 2 + 0) * FHO_N;
-            uint64_t* B = k->bsk + (((size_t)i * 2 + row) * 2 + 1) * FHO_N;
+            uint64_t* A = k->bsk + (((size_t)q * 2 + row) * 2 + 0) * FHO_N;
+            uint64_t* B = k->bsk + (((size_t)q * 2 + row) * 2 + 1) * FHO_N;
             for (int j = 0; j < FHO_N; ++j) A[j] = fho_rng_u64(&r);
             for (int j = 0; j < FHO_N; ++j) e[j] = (uint64_t)fho_rng_tuniform(&r, p->glwe_noise_log2);
             memcpy(B, e, FHO_N * 8);
             poly_mul_binary_acc(B, A, k->glwe_sk);
-            uint64_t g = k->lwe_sk[i] << (64 - p->pbs_base_log);
+            uint64_t g = msg << (64 - p->pbs_base_log);
             if (row == 0) A[0] += g; else B[0] += g;
         }
     }
     free(e);
-    for (size_t q = 0; q < (size_t)n * 4; ++q)
+    for (size_t q = 0; q < (size_t)ngg * 4; ++q)
         fho_poly_to_fourier(k->bsk + q * FHO_N, k->bsk_f + q * FHO_HALF * 2);
     return 0;
 }
@@ -464,7 +496,47 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
     }
     poly_rotate_d(rot, (2 * FHO_N - bt) & (2 * FHO_N - 1), acc1);
 
-    for (uint32_t i = 0; i < n; ++i) {
+    if (k->p.grouping == 2) {
+        /* multi-bit (grouping 2): per group i, with m_1 = a_2i, m_2 = a_2i+1, m_3 = m_1 + m_2 (mod 2N),
+         *   acc += ExtProd(sum_B (X^(m_B) - 1) GGSW(f_B), acc)
+         * in the Fourier domain: digits of acc itself (no rotation), and per point q (natural index
+         * j = bitrev(q)) the key bundle K_rc = sum_B cmul_acc(G_B,r,c, w_B) for B = 1, 2, 3 in order,
+         * w_B = E[((4 j + 1) m_B) mod 4096] - 1 (real part minus 1.0), cmul_acc(k, g, w) =
+         * (fma(g.re, w.re, fma(-g.im, w.im, k.re)), fma(g.re, w.im, fma(g.im, w.re, k.im))) from
+         * k = (+0, +0); then O = D0 K_0c + D1 K_1c as in the classic MAC. */
+        const double* E = fho_monomials();
+        for (uint32_t i = 0; i < n / 2; ++i) {
+            const uint32_t a0 = fho_modswitch(ct_small[2 * i]), a1 = fho_modswitch(ct_small[2 * i + 1]);
+            if (a0 == 0 && a1 == 0) continue;
+            const uint32_t m[3] = {a0, a1, (a0 + a1) & (2 * FHO_N - 1)};
+            for (int mm = 0; mm < 2; ++mm) {
+                double* acc = mm ? acc1 : acc0;
+                for (int j = 0; j < FHO_N; ++j) dig[j] = tor_digit(acc[j], down, base, ibase);
+                fho_dpoly_to_fourier(dig, mm ? D1 : D0);
+            }
+            const double* gi = k->bsk_f + (size_t)(3 * i) * 4 * FHO_HALF * 2;
+            for (int w = 0; w < 2; ++w) {
+                for (int q = 0; q < FHO_HALF; ++q) {
+                    const uint32_t jn = bitrev((uint32_t)q, 10), c4 = 4 * jn + 1;
+                    double kr[2] = {0.0, 0.0}, ki[2] = {0.0, 0.0};
+                    for (int B = 0; B < 3; ++B) {
+                        const double* e = E + 2 * ((c4 * m[B]) & 4095u);
+                        const double wr = e[0] - 1.0, wi = e[1];
+                        for (int row = 0; row < 2; ++row) {
+                            const double* G = gi + (((size_t)B * 2 + row) * 2 + w) * FHO_HALF * 2 + 2 * q;
+                            kr[row] = fma(G[0], wr, fma(-G[1], wi, kr[row]));
+                            ki[row] = fma(G[0], wi, fma(G[1], wr, ki[row]));
+                        }
+                    }
+                    const double d0r = D0[2 * q], d0i = D0[2 * q + 1], d1r = D1[2 * q], d1i = D1[2 * q + 1];
+                    O[2 * q] = fma(d0r, kr[0], -(d0i * ki[0])) + fma(d1r, kr[1], -(d1i * ki[1]));
+                    O[2 * q + 1] = fma(d0r, ki[0], d0i * kr[0]) + fma(d1r, ki[1], d1i * kr[1]);
+                }
+                fho_fourier_add_to_poly(O, w ? acc1 : acc0);
+            }
+        }
+    }
+    for (uint32_t i = 0; i < (k->p.grouping == 2 ? 0 : n); ++i) {
         uint32_t a = fho_modswitch(ct_small[i]);
         if (a == 0) continue;
         for (int m = 0; m < 2; ++m) {

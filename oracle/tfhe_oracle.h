@@ -52,7 +52,13 @@ typedef struct {
     uint32_t glwe_noise_log2; /* TUniform bound for big-key / GLWE / BSK noise */
     uint32_t message_modulus; /* 4 */
     uint32_t carry_modulus;   /* 4 */
+    uint32_t grouping;        /* blind-rotation grouping factor: 1 = classic CMUX per key bit,
+                                 2 = multi-bit (two key bits per external product) */
 } fho_params;
+
+/* GGSW count of the bootstrapping key: n (grouping 1) or (n / g) (2^g - 1) (multi-bit: one GGSW
+ * of f_B(s_gi, .., s_gi+g-1) = [the group's key bits equal the nonzero pattern B] per pattern) */
+uint32_t fho_ggsw_count(const fho_params* p);
 
 void fho_default_params(fho_params* p);
 
@@ -75,8 +81,8 @@ typedef struct {
     uint64_t* lwe_sk;   /* n binary coefficients (as u64 0/1) */
     uint64_t* glwe_sk;  /* N binary coefficients = the big LWE key */
     uint64_t* ksk;      /* [N][ks_level][n+1] (mask then body) */
-    uint64_t* bsk;      /* [n][row 0..1][poly 0..1][N] standard domain */
-    double* bsk_f;      /* [n][row][poly][HALF][re,im] Fourier domain, DIF (bit-reversed) order */
+    uint64_t* bsk;      /* [ggsw][row 0..1][poly 0..1][N] standard domain (ggsw = fho_ggsw_count) */
+    double* bsk_f;      /* [ggsw][row][poly][HALF][re,im] Fourier domain, DIF (bit-reversed) order */
 } fho_keys;
 
 int fho_keygen(fho_keys* k, const fho_params* p, uint64_t seed);
@@ -86,6 +92,10 @@ void fho_keys_free(fho_keys* k);
 void fho_tables_init(void);
 const double* fho_twiddles(void); /* W[k] = exp(+2 pi i k / 1024), k < 512, (re,im) pairs */
 const double* fho_twist(void);    /* psi[j] = exp(+i pi j / 2048), j < 1024, (re,im) pairs */
+/* monomial table E[k] = exp(+i pi k / 2048), k < 4096 = the value of X^k at the Fourier point of
+ * psi, defined as i^(k >> 10) psi[k & 1023] exactly (quarter turns are moves): X^m evaluated at the
+ * point j of the folded transform is E[((4 j + 1) m) mod 4096] */
+const double* fho_monomials(void);
 
 /* --- FFT primitives (exported for unit tests) --- */
 void fho_fft_forward(double* x /* HALF complex */);

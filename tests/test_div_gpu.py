@@ -11,15 +11,17 @@ import random
 
 import pytest
 
-from fhe_sign import Context, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, generate_keys, set_server_key
+from fhe_sign import (Context, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, generate_keys, multi_bit_params,
+                      set_server_key)
 
 pytestmark = pytest.mark.gpu
 M256 = (1 << 256) - 1
 
 
-@pytest.fixture(scope="module")
-def keys():
-    ck, sk = generate_keys(seed=0xD1)
+@pytest.fixture(scope="module", params=["classic", "multibit"])
+def keys(request):
+    """classic (grouping 1) and multi-bit (grouping 2) blind rotation: the same decrypted results"""
+    ck, sk = generate_keys(multi_bit_params() if request.param == "multibit" else None, seed=0xD1)
     ctx = Context(0)
     ctx.set_server_key(sk)
     set_server_key(ctx)

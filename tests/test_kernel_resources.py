@@ -31,8 +31,10 @@ def descriptors(src, tmp_path):
 
 @pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src,kernel,lds_per_cu_ok,max_regs", [
-    ("br_wide.hip", "k_blind_rotate_wide", 1, 256),     # one 8-wave workgroup per CU
-    ("br_quad.hip", "k_blind_rotate_quad", 3, 168),     # 3 four-wave workgroups per CU, 3 waves/SIMD
+    ("br_wide.hip", "k_blind_rotate_wideILi1", 1, 256),  # one 8-wave workgroup per CU (classic)
+    ("br_wide.hip", "k_blind_rotate_wideILi2", 1, 256),  # the same, multi-bit
+    ("br_quad.hip", "k_blind_rotate_quadILi1", 3, 168),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
+    ("br_quad.hip", "k_blind_rotate_quadILi2", 2, 256),  # multi-bit: 2 per CU, 2 waves/SIMD, deeper BSK ring
 ])
 def test_blind_rotate_occupancy(tmp_path, src, kernel, lds_per_cu_ok, max_regs):
     d = descriptors(os.path.join(CSRC, src), tmp_path)

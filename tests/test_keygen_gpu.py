@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from fhe_sign import Context, generate_keys
+from fhe_sign import Context, generate_keys, multi_bit_params
 
 pytestmark = pytest.mark.gpu
 
@@ -49,3 +49,19 @@ def test_device_key_bootstraps(ctx):
     cts = np.stack([ck.encrypt_block(m) for m in range(16)])
     out = ctx.pbs(cts, lid)
     assert [ck.decrypt_block(o) for o in out] == [(3 * m + 1) % 16 for m in range(16)]
+
+
+def test_device_multibit_keys_equal_oracle(ctx):
+    """multi-bit bootstrapping key (grouping 2: GGSWs of the pattern indicators f_B of each pair of
+    key bits) generated on the GPU == the oracle's, word for word; and a fresh random (os.urandom)
+    key generated on the device equals the host keygen of the same 256-bit key"""
+    ck, sk = generate_keys(multi_bit_params(), seed=SEED, device=ctx)
+    ok = oracle.OracleKeys(SEED, oracle.multibit_params())
+    ksk, bsk = sk.export()
+    assert bsk.size == ok.bsk.size == 417 * 3 * 4 * 2048
+    assert np.array_equal(ksk, ok.ksk) and np.array_equal(bsk, ok.bsk)
+    ctx.set_server_key(sk)
+    lid = ctx.lut([(5 * m + 2) % 16 for m in range(16)])
+    cts = np.stack([ck.encrypt_block(m) for m in range(16)])
+    out = ctx.pbs(cts, lid)
+    assert [ck.decrypt_block(o) for o in out] == [(5 * m + 2) % 16 for m in range(16)]

@@ -24,7 +24,7 @@ import math
 import numpy as np
 import pytest
 
-from fhe_sign import Context, generate_keys
+from fhe_sign import Context, generate_keys, multi_bit_params
 
 pytestmark = pytest.mark.gpu
 
@@ -33,18 +33,24 @@ ROUNDS = 4           # measured rounds: 4 * 2C = 1,048,576 bootstraps at 22 / 25
 DELTA = 1 << 59      # 2^63 / (message * carry)
 
 
-def _model_sigma_log2(n):
+def _model_sigma_log2(n, multibit=False):
     var_digit = 2.0 ** 44 / 3
     var_ggsw = 2.0 ** 34 / 3
-    per_cmux = 2 * 2048 * var_digit * var_ggsw + 0.5 * (2.0 ** 80 / 3) * (1 + 1024)
-    return 0.5 * math.log2(n * per_cmux)
+    var_dec = (2.0 ** 80 / 3) * (1 + 1024)  # gadget rounding of one digit through the key polynomial
+    if not multibit:  # n CMUX: GGSW(s_i) noise, rounding when s_i = 1
+        return 0.5 * math.log2(n * (2 * 2048 * var_digit * var_ggsw + 0.5 * var_dec))
+    # n/2 groups: the key bundle sum_B (X^m_B - 1) GGSW(f_B) carries 3 GGSW noises, each through
+    # ||X^m - 1||^2 = 2; the rounding of acc's digits enters through (X^m(s) - 1) unless s = 00 (3/4)
+    return 0.5 * math.log2(n / 2 * (2 * 2048 * var_digit * var_ggsw * 3 * 2 + 0.75 * 2 * var_dec))
 
 
-def test_million_bootstraps_at_the_noise_limit():
+@pytest.mark.parametrize("kind", ["classic", "multibit"])
+def test_million_bootstraps_at_the_noise_limit(kind):
     torch = pytest.importorskip("torch")
     assert torch.cuda.is_available()
     dev = torch.device("cuda:0")
-    ck, sk = generate_keys(seed=0x7E57)
+    mb = kind == "multibit"
+    ck, sk = generate_keys(multi_bit_params() if mb else None, seed=0x7E57)
     ctx = Context(0)
     ctx.set_server_key(sk)
     n = sk.params.lwe_dimension
@@ -114,8 +120,8 @@ def test_million_bootstraps_at_the_noise_limit():
     eo = torch.cat(errs_out).numpy()
     ea, eb = torch.cat(errs_a).numpy(), torch.cat(errs_b).numpy()
     s_out, s_a, s_b = (math.log2(x.std()) for x in (eo, ea, eb))
-    model = _model_sigma_log2(n)
-    print(f"\nnoise: {total} bootstraps at 22/25 units, {fails} decode failures; output sigma 2^{s_out:.2f} "
+    model = _model_sigma_log2(n, mb)
+    print(f"\nnoise [{kind}]: {total} bootstraps at 22/25 units, {fails} decode failures; output sigma 2^{s_out:.2f} "
           f"(model without f64 rounding 2^{model:.2f}); inputs: 22-unit sigma 2^{s_a:.2f} "
           f"(22 x output: 2^{s_out + 0.5 * math.log2(22):.2f}), 25-unit 2^{s_b:.2f} "
           f"(2^{s_out + 0.5 * math.log2(25):.2f}); max |output err| = 2^{math.log2(np.abs(eo).max()):.2f}")

@@ -7,16 +7,19 @@ import numpy as np
 import pytest
 
 import oracle
-from fhe_sign import Context, generate_keys
+from fhe_sign import Context, generate_keys, multi_bit_params
 
 pytestmark = pytest.mark.gpu
 SEED = 0xC0FFEE
 
 
-@pytest.fixture(scope="module")
-def env():
-    ck, sk = generate_keys(seed=SEED)
-    ok = oracle.OracleKeys(SEED)
+@pytest.fixture(scope="module", params=["classic", "multibit"])
+def env(request):
+    """every test runs on both blind rotations: classic (grouping 1, one CMUX per key bit) and
+    multi-bit (grouping 2: oracle fho_blind_rotate's key-bundle path)"""
+    mb = request.param == "multibit"
+    ck, sk = generate_keys(multi_bit_params() if mb else None, seed=SEED)
+    ok = oracle.OracleKeys(SEED, oracle.multibit_params() if mb else None)
     ctx = Context(0)
     ctx.set_server_key(sk)
     yield ck, sk, ok, ctx
@@ -26,7 +29,7 @@ def env():
 def test_fourier_bsk_bit_exact(env):
     _, _, ok, ctx = env
     gpu = ctx.export_fourier_bsk()
-    ref = oracle.fourier_bsk_gpu_layout(ok.bsk_f, ok.params.n)
+    ref = oracle.fourier_bsk_gpu_layout(ok.bsk_f, ok.ggsw_count)
     assert gpu.shape == ref.shape
     bad = np.flatnonzero(gpu.view(np.uint64) != ref.view(np.uint64))
     assert bad.size == 0, f"{bad.size} mismatching doubles, first at {bad[:5]}"

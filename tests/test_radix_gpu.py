@@ -12,15 +12,16 @@ import pytest
 import ref_semantics as R
 from conftest import ROOT
 from fhe_sign import (COMPAT, FAST, BigUintFHE, Context, FheUint8, FheUint32, FheUint64, generate_keys,
-                      set_server_key, stats)
+                      multi_bit_params, set_server_key, stats)
 
 pytestmark = pytest.mark.gpu
 G = os.path.join(ROOT, "tests", "golden")
 
 
-@pytest.fixture(scope="module")
-def keys():
-    ck, sk = generate_keys(seed=0xB16)
+@pytest.fixture(scope="module", params=["classic", "multibit"])
+def keys(request):
+    """classic (grouping 1) and multi-bit (grouping 2) blind rotation: the same decrypted results"""
+    ck, sk = generate_keys(multi_bit_params() if request.param == "multibit" else None, seed=0xB16)
     ctx = Context(0)
     ctx.set_server_key(sk)
     set_server_key(ctx)

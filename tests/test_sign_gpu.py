@@ -7,15 +7,17 @@ import os
 import pytest
 
 from conftest import ROOT
-from fhe_sign import COMPAT, FAST, PUBLIC, BigUintFHE, Context, Schnorr, compute_nonce, generate_keys, public_key_x, set_server_key
+from fhe_sign import (COMPAT, FAST, PUBLIC, BigUintFHE, Context, Schnorr, compute_nonce, generate_keys, multi_bit_params,
+                      public_key_x, set_server_key)
 
 pytestmark = pytest.mark.gpu
 ROWS = {r["index"]: r for r in csv.DictReader(open(os.path.join(ROOT, "tests", "golden", "bip340_vectors.csv")))}
 
 
-@pytest.fixture(scope="module")
-def env():
-    ck, sk = generate_keys(seed=0x5167)
+@pytest.fixture(scope="module", params=["classic", "multibit"])
+def env(request):
+    """classic (grouping 1) and multi-bit (grouping 2) blind rotation: identical signatures"""
+    ck, sk = generate_keys(multi_bit_params() if request.param == "multibit" else None, seed=0x5167)
     ctx = Context(0)
     ctx.set_server_key(sk)
     set_server_key(ctx)
