@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 METRIC = "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds @1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6        # MI355X dense FP64 peak (matrix = vector on gfx950), spec
 FP64_PEAK_MEASURED_TFLOPS = 65.0  # dependent-free v_fma_f64 stream on the GPU box (tools/fp64_peak.hip)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "r1w_pmc_summary.json")  # tools/profile_round.sh
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2", "r2a_pmc_summary.json")  # tools/profile_round.sh
 FANOUT_MIN = 257  # levels with at least this many bootstraps are split over the GPUs (fan-out legs)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FLOPS_PER_CMUX = 4 * 51200 + 4 * 6144 + 32768   # 4 FFT-1024 (5 N log N), 4 twist/untwist, MAC
@@ -117,13 +117,13 @@ def cpu_baseline(seed, target_s):
                       f"this process's affinity/cgroup share, {dt:.1f} s"}
 
 
-def pmc_traffic(batch):
+def pmc_traffic(batch, kernel="k_blind_rotate_quad<1>"):
     """HBM-side bytes per launch of the blind-rotate kernel at this batch, from the committed PMC
     summary of the same kernel (tools/profile_round.sh; FETCH_SIZE x2 + WRITE_SIZE, gfx950
     correction of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits included)"""
     try:
         d = json.load(open(PMC_SUMMARY))["pmc"][f"B={batch}"]
-        k = next(v for k, v in d.items() if "k_blind_rotate_quad" in k)
+        k = next(v for k, v in d.items() if kernel in k)
         return k["hbm_side_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
     except (OSError, KeyError, StopIteration, ValueError):
         return None, None
@@ -485,6 +485,9 @@ def main():
     res["pcie_inclusive_pbs_per_s"] = cl["pcie_inclusive_pbs_per_s"]
     if mb is not None:
         # tfhe-rs' MultiBitPBS shape (grouping factor 2) on the same client key: same decrypted results
+        t_mb, src_mb = pmc_traffic(B, "k_blind_rotate_quad<2>")
+        mb["roofline"]["traffic"] = t_mb
+        mb["roofline"]["traffic_source"] = src_mb
         res["multibit"] = mb
     if fan is not None:
         res["fanout"] = fan

@@ -3,12 +3,14 @@ import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
 import numpy as np
+import fhe_sign
 from fhe_sign import Context, generate_keys
+MB = os.environ.get("FHE_PROBE_MB") == "1"  # multi-bit (grouping 2) keys
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 t0 = time.time()
-ck, sk = generate_keys(seed=1)
+ck, sk = generate_keys(fhe_sign.multi_bit_params() if MB else None, seed=1)
 print(f"keygen {time.time()-t0:.2f}s", flush=True)
 ctx = Context(0)
 t0 = time.time(); ctx.set_server_key(sk); print(f"set_server_key {time.time()-t0:.2f}s", flush=True)

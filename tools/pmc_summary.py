@@ -57,7 +57,7 @@ def main():
     for d in sorted(glob.glob(os.path.join(src, "pmc_*"))):
         if not os.path.isdir(d):
             continue
-        batch = d.rsplit("_", 1)[-1]
+        batch = d.rsplit("_", 1)[-1]  # pmc_<B> or pmc_<kind>_<B> (kernels of both kinds differ by name)
         for k, cs in counters(d).items():
             merged[(batch, k)].update(cs)
     for (batch, k), cs in sorted(merged.items()):
@@ -73,6 +73,8 @@ def main():
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                 if c in e:
                     e[c + "_frac"] = e[c] / e["SQ_WAVE_CYCLES"]
+        if "TA_TA_BUSY_sum" in e and e.get("GRBM_GUI_ACTIVE"):  # per CU (256) against per-XCD cycles (8)
+            e["ta_busy_frac"] = (e["TA_TA_BUSY_sum"] / 256) / (e["GRBM_GUI_ACTIVE"] / 8)
         if e.get("SQ_WAVES"):
             for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU"):
                 if c in e:
