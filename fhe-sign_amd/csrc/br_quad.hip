@@ -198,9 +198,11 @@ FHE_DEV void q_xpose_bc(cplx (&x)[8]) {
 //
 // G = blind-rotation grouping (as br_wide.hip): G = 1 classic; G = 2 multi-bit -- the digits of acc
 // itself (no rotation through LDS: two barriers less per step), and at the MAC the key bundle
-// K_rc = sum_B (E[(4j+1) m_B] - 1) G_B,rc per point.  A lane's phase-C points r are
-// j0 + 256 (r & 1) + 128 ((r >> 1) & 1) + 64 (r >> 2): registers r and r + 1 differ by i^m exactly,
-// so each pattern needs one monomial gather per register pair.
+// K_rc = sum_B (e_B(j) - 1) G_B,rc per point, e_B(j) = zeta^((4j+1) m_B) as the oracle forms it:
+// i^((j >> 8) m) cmul(E[(4 (j mod 64) + 1) m], E[256 ((j >> 6) mod 4) m]).  A lane's phase-C points
+// are j = j0 + 256 (r & 1) + 128 ((r >> 1) & 1) + 64 (r >> 2), j0 = (h + 2 u') + 512 L0: the first
+// factor is one value per lane and pattern for the whole group (its sign (-1)^(L0 m) taken out), the
+// second is wave-uniform per register pair (scalar loads), and registers r, r + 1 differ by i^m.
 template <int G>
 __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_quad(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
@@ -215,6 +217,8 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     __shared__ __attribute__((aligned(16))) cplx s_x[2][QX_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_w[QTW_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_z[QZ_LDS];
+    // G = 2: this group's monomials E[(4 j + 1) m_B] of every lane's register pairs, [pair k][B][h][lane]
+    __shared__ __attribute__((aligned(16))) cplx s_mono[G == 2 ? 3 * 2 * 64 : 1];  // [B][h][lane]
     for (int k = threadIdx.x; k < 512; k += 256) s_w[tpos(k)] = W[k];
     for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[k] = zq[k];
     __syncthreads();
@@ -254,10 +258,30 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
     }
 
-    // G = 2: c4 = 4 j0 + 1 of this lane's phase-C point r = 0 (idx 512 h + 16 u + L0), natural j0 = bitrev
-    const uint32_t c4 = 4u * (__builtin_bitreverse32((uint32_t)(512 * h + 16 * u + l0)) >> 22) + 1u;
+    // G = 2: 4 (j0 mod 64) + 1 of this lane's phase-C point r = 0 (idx 512 h + 16 u + L0, j0 = bitrev)
+    const uint32_t c4 = 4u * ((__builtin_bitreverse32((uint32_t)(512 * h + 16 * u + l0)) >> 22) & 63u) + 1u;
     uint32_t a_next = modswitch_2n(a_ct[0]);
     uint32_t a_next1 = G == 2 ? modswitch_2n(a_ct[1]) : 0u;
+    // G = 2: the lane factors E[(4 (j0 mod 64) + 1) m_B] of a group by LDS-DMA from the p = 0 wave of
+    // each half (3 per group; the per-lane gathers they replace touched a cache line per lane and
+    // were half the L1 traffic), issued one group ahead.  Single buffer: issued after the inverse's
+    // first barrier (every read of the table done), retired by the compiler's wait for the untwist
+    // factors loaded after it (VMEM loads return in order), published by the next group's barriers.
+    const uint32_t mono_base = __builtin_amdgcn_readfirstlane(lds_off(s_mono + h * 64));
+    const rsrc_t mono_rs = buffer_rsrc(mono, 4096 * 16);
+    auto mono_dma = [&](uint32_t m0, uint32_t m1) {
+        const uint32_t m[3] = {m0, m1, (m0 + m1) & 4095u};
+        if (p == 0) {
+#pragma unroll
+            for (int B = 0; B < 3; ++B)
+                dma16_buf(mono_rs, ((c4 * m[B]) & 4095u) * 16u, mono_base + (uint32_t)(B * 2 * 64 * 16));
+        }
+    };
+    if constexpr (G == 2) {
+        mono_dma(a_next, a_next1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     for (int i = 0; i < n / G; ++i) {
         uint32_t a = 0, mB[3] = {0u, 0u, 0u};
         if constexpr (G == 1) {
@@ -272,7 +296,8 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                 a_next = modswitch_2n(a_ct[2 * i + 2]);
                 a_next1 = modswitch_2n(a_ct[2 * i + 3]);
             }
-            if ((mB[0] | mB[1]) == 0) continue;  // X^0 = 1: acc unchanged (uniform)
+            // no skip of m0 = m1 = 0 (the table chain needs every group's barriers): K = 0 exactly,
+            // acc comes back unchanged up to the sign of a zero, as in the oracle's skip
         }
         const cplx* Pg = ps;
         asm volatile("" : "+s"(Pg));
@@ -328,7 +353,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         constexpr int QR = G == 1 ? QCL_D : QMB_D;
         cplx Bq0[G == 1 ? QR : 3 * QR], Bq1[G == 1 ? QR : 3 * QR];
         cplx em[G == 2 ? 3 : 1];  // G = 2: monomials of the current register pair, per pattern
-        const gcptr E = as_global(mono);
+        cplx eb[G == 2 ? 3 : 1];  // G = 2: lane factors of the group, per pattern
         if constexpr (G == 1) {
 #pragma unroll
         for (int r = 0; r < QR; ++r) {
@@ -338,7 +363,6 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         } else {
 #pragma unroll
         for (int B = 0; B < 3; ++B) {
-            em[B] = E[(c4 * mB[B]) & 4095u];
 #pragma unroll
             for (int d = 0; d < QR; ++d) {
                 Bq0[3 * d + B] = bm[B * 4 * 1024 + d * 64];
@@ -382,15 +406,29 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             cplx Ko = make_double2(0.0, 0.0), Kt = make_double2(0.0, 0.0);
-            if (r > 0 && !(r & 1)) {  // monomials of this register pair (r, r + 1)
-                const uint32_t cr = c4 + 512u * ((r >> 1) & 1) + 256u * (r >> 2);
+            if (r == 0) {  // lane factors with the sign (-1)^(L0 m) of (j >> 8) m taken out
 #pragma unroll
-                for (int B = 0; B < 3; ++B) em[B] = E[(cr * mB[B]) & 4095u];
+                for (int B = 0; B < 3; ++B) {
+                    const cplx b = s_mono[(B * 2 + h) * 64 + L];
+                    const uint32_t sg = (uint32_t)(l0 & mB[B]) << 31;
+                    eb[B] = make_double2(neg_if(b.x, sg), neg_if(b.y, sg));
+                }
+            }
+            if (!(r & 1)) {  // pair r / 2 = 2 b1 + b2: natural bits 6, 7 of j are (b2, b1)
+                const uint32_t qk = ((r >> 2) & 1) + 2u * ((r >> 1) & 1);
+#pragma unroll
+                for (int B = 0; B < 3; ++B) {
+                    if (qk == 0) {
+                        em[B] = eb[B];
+                    } else {
+                        const uint32_t fi = __builtin_amdgcn_readfirstlane((256u * qk * mB[B]) & 4095u);
+                        em[B] = cmul(eb[B], as_global(mono)[fi]);
+                    }
+                }
             }
 #pragma unroll
             for (int B = 0; B < 3; ++B) {
-                const cplx z = (r & 1) ? qturn(em[B], mB[B] & 3u) : em[B];
-                const cplx w = make_double2(z.x - 1.0, z.y);
+                const cplx w = (r & 1) ? turn_m1(em[B], make_uturn(mB[B])) : make_double2(em[B].x - 1.0, em[B].y);
                 const int sl = 3 * (r % QR) + B;
                 const cplx Bm = Bq0[sl], Bo = Bq1[sl];
                 if (r + QR < 8) {
@@ -411,6 +449,8 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         q_dit<2>(x, s_w, tpos(64 * (L & 1)));
         q_xpose_bc(x);
         __syncthreads();  // the other polynomial's waves have read this wave's digits
+        if constexpr (G == 2)
+            if (2 * i + 2 < n) mono_dma(a_next, a_next1);  // next group's table (every read done)
         q_dit<0>(x, s_w, tpos(32 * lowB));
         q_dit<1>(x, s_w, tpos(16 * lowB));
         q_dit<2>(x, s_w, tpos(8 * lowB));

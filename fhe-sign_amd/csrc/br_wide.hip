@@ -176,6 +176,12 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_inv[2][CROSS_SZ];  // inverse E -> D exchange
     __shared__ __attribute__((aligned(16))) cplx s_cd[8][CD_SZ];      // C <-> D, one region per wave
+    // G = 2: the monomial factors of each lane's j0 (oracle fho_blind_rotate, grouping 2), gathered
+    // one group ahead by LDS-DMA: E[(4 (j0 mod 64) + 1) m_B] per [group parity][B][q][lane] from the
+    // p = 0 waves (the p = 1 waves' lanes have the same j0), E[256 f m_B] per [parity][B][f] (f < 4,
+    // the lane's (j0 >> 6) mod 4; 64 entries, 4 distinct) from wave 4
+    __shared__ __attribute__((aligned(16))) cplx s_mono[G == 2 ? 2 * 3 * 4 * 64 : 1];
+    __shared__ __attribute__((aligned(16))) cplx s_monf[G == 2 ? 2 * 3 * 64 : 1];
 
     const int ct = blockIdx.x;
     const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
@@ -214,12 +220,41 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     // lane parts of the linear LDS maps
     const int xD = fx(16 * L + q), xE = fx(256 * q + 4 * L);
 
-    // G = 2: c4 = 4 j0 + 1 of this lane's phase-E point r = 0 (idx 256 q + 4 L, natural j0 = bitrev)
-    const uint32_t c4 = 4u * (__builtin_bitreverse32((uint32_t)(256 * q + 4 * L)) >> 22) + 1u;
-    const gcptr E = as_global(mono);
+    // G = 2: this lane's phase-E point r = 0 (idx 256 q + 4 L, natural j0 = bitrev): 4 (j0 mod 64) + 1
+    // and (j0 >> 6) mod 4 (lane bits 0, 1)
+    const uint32_t j0 = __builtin_bitreverse32((uint32_t)(256 * q + 4 * L)) >> 22;
+    const uint32_t c4 = 4u * (j0 & 63u) + 1u;
+    const int fsel = (int)((j0 >> 6) & 3u);
 
     uint32_t a_next = modswitch_2n(a_ct[0]);
     uint32_t a_next1 = G == 2 ? modswitch_2n(a_ct[1]) : 0u;
+    // G = 2: the monomials of group g (exponents m0, m1) for this wave's q, into parity buffer g & 1.
+    // Issued by the p = 0 waves at the top of group g - 1, before that group's key slices: the
+    // compiler's waits for those retire it (VMEM loads return in order; the explicit wait before the
+    // inverse exchange makes sure of it), and that group's barriers publish it.  The per-lane gather
+    // it replaces sat on the critical path of every group (B = 1 latency 2.00 -> 1.70 ms).
+    const uint32_t mono_base = __builtin_amdgcn_readfirstlane(lds_off(s_mono + q * 64));
+    const uint32_t monf_base = __builtin_amdgcn_readfirstlane(lds_off(s_monf));
+    const rsrc_t mono_rs = buffer_rsrc(mono, 4096 * 16);
+    auto mono_dma = [&](int g, uint32_t m0, uint32_t m1) {
+        const uint32_t m[3] = {m0, m1, (m0 + m1) & 4095u};
+        if (p == 0) {
+#pragma unroll
+            for (int B = 0; B < 3; ++B)
+                dma16_buf(mono_rs, ((c4 * m[B]) & 4095u) * 16u,
+                          mono_base + (uint32_t)(((g & 1) * 3 + B) * 4 * 64 * 16));
+        } else if (q == 0) {
+#pragma unroll
+            for (int B = 0; B < 3; ++B)
+                dma16_buf(mono_rs, ((256u * (uint32_t)(L & 3) * m[B]) & 4095u) * 16u,
+                          monf_base + (uint32_t)(((g & 1) * 3 + B) * 64 * 16));
+        }
+    };
+    if constexpr (G == 2) {
+        mono_dma(0, a_next, a_next1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     for (int i = 0; i < n / G; ++i) {
         cplx x[4];
         cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
@@ -266,25 +301,28 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         if (2 * i + 2 < n) {
             a_next = modswitch_2n(a_ct[2 * i + 2]);
             a_next1 = modswitch_2n(a_ct[2 * i + 3]);
+            mono_dma(i + 1, a_next, a_next1);
         }
-        if ((mB[0] | mB[1]) == 0) continue;  // X^0 = 1: the group leaves acc unchanged (uniform)
+        // no skip of m0 = m1 = 0 (the DMA chain needs every group's barriers): K = 0 exactly and acc
+        // comes back unchanged up to the sign of a zero (acc + (+-0), tor_red_s of a reduced value),
+        // as in the oracle's skip.
         // key bundle K_rc = sum_B (E[(4j+1) m_B] - 1) G_B,rc (rows p and 1 - p of column p), patterns
         // in order (oracle cmul_acc); a lane's points r are j0 + 256 bitrev2(r), so their monomials
-        // are i^(bitrev2(r) m_B) E[(4 j0 + 1) m_B]: one gather per pattern, exact quarter turns
+        // are i^(bitrev2(r) m_B) E[(4 j0 + 1) m_B]: one table entry per pattern, exact quarter turns
         {
-            cplx e[3];
-#pragma unroll
-            for (int B = 0; B < 3; ++B) e[B] = E[(c4 * mB[B]) & 4095u];
+            const cplx* tb = s_mono + (i & 1) * 768 + q * 64 + L;
+            const cplx* tf = s_monf + (i & 1) * 192 + fsel;
 #pragma unroll
             for (int r = 0; r < 4; ++r) Kown[r] = Koth[r] = make_double2(0.0, 0.0);
 #pragma unroll
             for (int B = 0; B < 3; ++B) {
                 const gcptr b0 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;
                 const gcptr b1 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;
+                const cplx e = cmul(tb[B * 256], tf[B * 64]);  // zeta^((4 j0 + 1) m_B)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const cplx z = qturn(e[B], ((2 * (r & 1) + (r >> 1)) * mB[B]) & 3u);
-                    const cplx wv = make_double2(z.x - 1.0, z.y);
+                    const cplx wv = r == 0 ? make_double2(e.x - 1.0, e.y)
+                                           : turn_m1(e, make_uturn((2 * (r & 1) + (r >> 1)) * mB[B]));
                     Kown[r] = cmul_acc(Kown[r], b0[r * 64], wv);
                     Koth[r] = cmul_acc(Koth[r], b1[r * 64], wv);
                 }
@@ -342,6 +380,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         cplx* inv = s_inv[p];
 #pragma unroll
         for (int r = 0; r < 4; ++r) inv[xE ^ fx(r)] = x[r];
+        if constexpr (G == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the monomial DMA
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = inv[xD ^ fx(4 * r)];

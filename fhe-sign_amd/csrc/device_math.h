@@ -71,6 +71,19 @@ FHE_DEV cplx qturn(cplx z, uint32_t t) {
     const cplx a = (t & 1) ? make_double2(-z.y, z.x) : z;
     return (t & 2) ? make_double2(-a.x, -a.y) : a;
 }
+// i^t e - 1 for a wave-uniform t without per-lane selects: i^t = (c, s) with one of c, s zero, so
+// w.x = fma(c, e.x, fma(-s, e.y, -1)) and w.y = fma(s, e.x, c e.y) round once each, exactly as
+// (qturn(e, t).x - 1.0, qturn(e, t).y) does (up to the sign of a zero); c, s live in SGPRs.
+struct uturn {
+    double c, s;
+};
+FHE_DEV uturn make_uturn(uint32_t t) {
+    t &= 3u;
+    return uturn{t == 0u ? 1.0 : (t == 2u ? -1.0 : 0.0), t == 1u ? 1.0 : (t == 3u ? -1.0 : 0.0)};
+}
+FHE_DEV cplx turn_m1(cplx e, uturn u) {
+    return make_double2(__fma_rn(u.c, e.x, __fma_rn(-u.s, e.y, -1.0)), __fma_rn(u.s, e.x, u.c * e.y));
+}
 FHE_DEV cplx cadd(cplx a, cplx b) { return make_double2(a.x + b.x, a.y + b.y); }
 FHE_DEV cplx csub(cplx a, cplx b) { return make_double2(a.x - b.x, a.y - b.y); }
 FHE_DEV cplx conj_(cplx a) { return make_double2(a.x, -a.y); }
@@ -163,6 +176,39 @@ struct gcptr {
     FHE_DEV gcptr operator+(long i) const { return gcptr{p + i}; }
 };
 FHE_DEV gcptr as_global(const cplx* p) { return gcptr{(const __attribute__((address_space(1))) dvec2*)p}; }
+
+// One 1 KiB LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes from src land at LDS byte address
+// lds_base + 16 l, no VGPR written.  Inline asm on purpose: hipcc treats the builtin as a pending
+// write to every LDS object and drains it (vmcnt(0)) before the next LDS access anywhere in the
+// kernel.  The caller retires it itself: VMEM loads return in order, so any wait for a load issued
+// after it (the compiler's own vmcnt for that load) also retires the DMA; a barrier after that
+// publishes the bytes to the workgroup.  M0 (the LDS base) is saved and restored.
+FHE_DEV uint32_t lds_off(const void* p) { return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p; }
+// The same through a buffer resource (base in SGPRs, one VGPR byte offset per lane)
+typedef int __attribute__((ext_vector_type(4))) rsrc_t;
+FHE_DEV rsrc_t buffer_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    rsrc_t r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));  // stride 0
+    r.z = (int)bytes;
+    r.w = 0x00020000;  // gfx9 raw buffer, 32-bit data format
+    return r;
+}
+FHE_DEV void dma16_buf(rsrc_t rs, uint32_t byte_off, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(byte_off), "s"(rs), "s"(lds_base)
+                 : "memory");
+}
+FHE_DEV void dma16(const cplx* src, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_base)
+                 : "memory");
+}
 
 // Twiddles come from a per-lane table Wl[slot * 64] (Wl = table + lane), slot = tw_slot(s, g):
 // phase A (stages 0-3) slot(s, g) = 16 - 2 hd + g holds W[(L + 64 g) << s]; phase B (stages 4-7)

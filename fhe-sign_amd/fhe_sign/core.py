@@ -212,7 +212,8 @@ class Context:
         check(load().fhe_ctx_sync(self._h))
 
     def set_br_kernel(self, kind: int) -> None:
-        """0 = 2-wave throughput kernel, 1 = 4-wave (default); identical results"""
+        """1 = 4 waves per ciphertext (the throughput kernel); 0, the retired 2-wave kernel, is
+        refused.  The throughput and latency kernels give identical results."""
         check(load().fhe_ctx_set_br_kernel(self._h, int(kind)))
 
     def set_ks_kernel(self, kind: int) -> None:

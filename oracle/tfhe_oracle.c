@@ -501,9 +501,16 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
          *   acc += ExtProd(sum_B (X^(m_B) - 1) GGSW(f_B), acc)
          * in the Fourier domain: digits of acc itself (no rotation), and per point q (natural index
          * j = bitrev(q)) the key bundle K_rc = sum_B cmul_acc(G_B,r,c, w_B) for B = 1, 2, 3 in order,
-         * w_B = E[((4 j + 1) m_B) mod 4096] - 1 (real part minus 1.0), cmul_acc(k, g, w) =
+         * w_B = e_B - 1 (real part minus 1.0), cmul_acc(k, g, w) =
          * (fma(g.re, w.re, fma(-g.im, w.im, k.re)), fma(g.re, w.im, fma(g.im, w.re, k.im))) from
-         * k = (+0, +0); then O = D0 K_0c + D1 K_1c as in the classic MAC. */
+         * k = (+0, +0); then O = D0 K_0c + D1 K_1c as in the classic MAC.
+         * The monomial e_B = zeta^((4j+1) m_B) (zeta = exp(i pi / 2048)) is formed from the exact
+         * table E[k] = zeta^k by the split (4j+1) m = (4 (j mod 64) + 1) m + 256 ((j >> 6) mod 4) m
+         * + 1024 (j >> 8) m:  e = i^((j >> 8) m) cmul(E[(4 (j mod 64) + 1) m], E[256 ((j >> 6) mod 4) m])
+         * (indices mod 4096, cmul(x, w) = (fma(x.re, w.re, -(x.im w.im)), fma(x.re, w.im, x.im w.re)),
+         * the quarter turn exact).  The split matches the GPU kernels' lane layouts:
+         * the first factor takes 64 (latency kernel: 16) distinct values per wave -- one gather of
+         * few cache lines -- and the second is wave-uniform or one of 4. */
         const double* E = fho_monomials();
         for (uint32_t i = 0; i < n / 2; ++i) {
             const uint32_t a0 = fho_modswitch(ct_small[2 * i]), a1 = fho_modswitch(ct_small[2 * i + 1]);
@@ -517,11 +524,19 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
             const double* gi = k->bsk_f + (size_t)(3 * i) * 4 * FHO_HALF * 2;
             for (int w = 0; w < 2; ++w) {
                 for (int q = 0; q < FHO_HALF; ++q) {
-                    const uint32_t jn = bitrev((uint32_t)q, 10), c4 = 4 * jn + 1;
+                    const uint32_t jn = bitrev((uint32_t)q, 10);
                     double kr[2] = {0.0, 0.0}, ki[2] = {0.0, 0.0};
                     for (int B = 0; B < 3; ++B) {
-                        const double* e = E + 2 * ((c4 * m[B]) & 4095u);
-                        const double wr = e[0] - 1.0, wi = e[1];
+                        const double* b = E + 2 * (((4 * (jn & 63) + 1) * m[B]) & 4095u);
+                        const double* f = E + 2 * ((256 * ((jn >> 6) & 3) * m[B]) & 4095u);
+                        double er = fma(b[0], f[0], -(b[1] * f[1])), ei = fma(b[0], f[1], b[1] * f[0]);
+                        switch (((jn >> 8) * m[B]) & 3u) { /* i^t e, exact */
+                            case 0: break;
+                            case 1: { const double t = er; er = -ei; ei = t; break; }
+                            case 2: er = -er; ei = -ei; break;
+                            default: { const double t = er; er = ei; ei = -t; break; }
+                        }
+                        const double wr = er - 1.0, wi = ei;
                         for (int row = 0; row < 2; ++row) {
                             const double* G = gi + (((size_t)B * 2 + row) * 2 + w) * FHO_HALF * 2 + 2 * q;
                             kr[row] = fma(G[0], wr, fma(-G[1], wi, kr[row]));
