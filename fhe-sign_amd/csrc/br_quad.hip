@@ -421,8 +421,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                     if (qk == 0) {
                         em[B] = eb[B];
                     } else {
-                        const uint32_t fi = __builtin_amdgcn_readfirstlane((256u * qk * mB[B]) & 4095u);
-                        em[B] = cmul(eb[B], as_global(mono)[fi]);
+                        em[B] = cmul(eb[B], sload(mono, (256u * qk * mB[B]) & 4095u));
                     }
                 }
             }

@@ -62,9 +62,10 @@ struct fhe_ctx {
     int8_t* d_ks_digits = nullptr;  // keyswitch digits workspace
     uint64_t* d_ks_body = nullptr;
     size_t ks_cap = 0;              // ciphertexts
-    // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU)
-    // (one ciphertext per CU at a time -- 144 KB LDS -- so up to two rounds over the 256 CUs); quad above
-    int wide_threshold = 512;  // profiles/r1/latency_sweep_r1p.txt
+    // levels with at most this many bootstraps use the latency kernel (one ciphertext per CU at a
+    // time -- >128 KB LDS -- so one round over the 256 CUs); the throughput kernel above, which holds
+    // 2-3 per CU (profiles/r2/latency_sweep_r2b.txt: from 320 on it is as fast or faster)
+    int wide_threshold = 256;
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;

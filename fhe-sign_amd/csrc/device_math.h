@@ -177,6 +177,13 @@ struct gcptr {
 };
 FHE_DEV gcptr as_global(const cplx* p) { return gcptr{(const __attribute__((address_space(1))) dvec2*)p}; }
 
+// Wave-uniform table entry through the scalar cache (s_load_dwordx4): constant address space
+FHE_DEV cplx sload(const cplx* base, uint32_t uniform_idx) {
+    const __attribute__((address_space(4))) dvec2* p = (const __attribute__((address_space(4))) dvec2*)base;
+    const dvec2 v = p[__builtin_amdgcn_readfirstlane(uniform_idx)];
+    return make_double2(v.x, v.y);
+}
+
 // One 1 KiB LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes from src land at LDS byte address
 // lds_base + 16 l, no VGPR written.  Inline asm on purpose: hipcc treats the builtin as a pending
 // write to every LDS object and drains it (vmcnt(0)) before the next LDS access anywhere in the

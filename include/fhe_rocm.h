@@ -147,7 +147,7 @@ int fhe_memcpy_d2h(fhe_ctx* ctx, void* dst, const void* src, size_t bytes);
 int fhe_ctx_last_pbs_timing(fhe_ctx* ctx, float* ks_ms, float* br_ms);
 int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
- * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 512. */
+ * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
 /* Throughput blind-rotate kernel for levels above the threshold: 4 waves per ciphertext
  * (FHE_BR_QUAD, the default and only one; FHE_BR_NARROW, the retired 2-wave kernel, is refused with

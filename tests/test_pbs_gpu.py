@@ -108,7 +108,7 @@ def test_wide_and_quad_kernels_bit_identical(env):
         ctx.set_wide_threshold(1 << 30)
         wide = ctx.pbs(cts, lut_ids)
     finally:
-        ctx.set_wide_threshold(512)
+        ctx.set_wide_threshold(256)
     assert np.array_equal(quad, wide)
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(wide[:6], ref)
