@@ -1,13 +1,14 @@
 """Per-level schedule trace of the headline ops (FHE_TRACE_LEVELS=1: the engine synchronizes after
 every level and prints its PBS count and wall time to stderr).
-usage: FHE_TRACE_LEVELS=1 python3 tools/level_trace.py [op ...]  (ops: mul_compat mul_fast sign div_enc)"""
+usage: FHE_TRACE_LEVELS=1 [FHE_PROBE_MB=1] python3 tools/level_trace.py [op ...]  (ops: mul_compat mul_fast sign div_enc)"""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd")); sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import random
 from fhe_sign import *
 
-ck, sk = generate_keys(seed=9)
+MB = os.environ.get("FHE_PROBE_MB") == "1"  # multi-bit (grouping 2) keys
+ck, sk = generate_keys(multi_bit_params() if MB else None, seed=9)
 ctx = Context(0); ctx.set_server_key(sk); set_server_key(ctx)
 rng = random.Random(0xF11E51)
 a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(256) | 1 << 255
