@@ -45,7 +45,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=8192, help="PBS per step per GPU")
+    # 32768 = the widest PBS level of configs[1]'s compat 256-bit mul (the first level: every block
+    # product of the 8x8 limb products, profiles/r2/level_trace_r2c.txt), 42.7 rounds of the
+    # throughput kernel's 768 resident workgroups
+    ap.add_argument("--batch", type=int, default=32768, help="PBS per step per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0xF11E51)
@@ -463,7 +466,7 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"batched programmable bootstrap (KS+MS+BR+SE) of {B} 2_2 radix blocks per GPU "
-                        "= one PBS level of BigUintFHE 256-bit mul (configs[1])",
+                        "= one PBS level of BigUintFHE 256-bit mul (configs[1]; 32768 = its widest level)",
             "batch_pbs_per_gpu": B,
             "params": cl["params"],
             "parallelism": f"replicas x{world}",
