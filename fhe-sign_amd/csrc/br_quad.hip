@@ -139,31 +139,7 @@ FHE_DEV void q_stage9(cplx (&x)[8]) {
     }
 }
 // ---- B <-> C as register transposes (no LDS): register bits (2,1,0) <-> lane bits (5,4,3)
-FHE_DEV void qsplit(double d, uint32_t& lo, uint32_t& hi) {
-    const uint64_t b = (uint64_t)__double_as_longlong(d);
-    lo = (uint32_t)b;
-    hi = (uint32_t)(b >> 32);
-}
-FHE_DEV double qjoin(uint32_t lo, uint32_t hi) { return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)); }
-// X holds register bit 0, Y register bit 1 of the pair; afterwards that register bit and lane bit K
-// are swapped.  K = 5, 4: v_permlane32_swap / v_permlane16_swap, one instruction per dword pair.
-template <int K>
-FHE_DEV void qx_permlane(cplx& X, cplx& Y) {
-    uint32_t x[4], y[4];
-    qsplit(X.x, x[0], x[1]);
-    qsplit(X.y, x[2], x[3]);
-    qsplit(Y.x, y[0], y[1]);
-    qsplit(Y.y, y[2], y[3]);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        auto r = K == 5 ? __builtin_amdgcn_permlane32_swap(x[d], y[d], false, false)
-                        : __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
-        x[d] = r[0];
-        y[d] = r[1];
-    }
-    X = make_double2(qjoin(x[0], x[1]), qjoin(x[2], x[3]));
-    Y = make_double2(qjoin(y[0], y[1]), qjoin(y[2], y[3]));
-}
+// (lane bits 5, 4: qx_permlane<K> in device_math.h)
 // K = 3: lanes with lane bit 3 set are whole 4-lane DPP banks, one masked move per half
 FHE_DEV void qx_banked3(cplx& X, cplx& Y) {
     uint32_t x[4], y[4];

@@ -183,18 +183,20 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     // usable until every collective and conversion has succeeded, then the two are swapped.
     uint64_t* n_ksk = nullptr;
     int8_t* n_planes = nullptr;
-    double2 *n_bsk = nullptr, *n_quad = nullptr;
+    double2 *n_bsk = nullptr, *n_quad = nullptr, *n_pair = nullptr;
     auto drop_new = [&] {
         (void)hipStreamSynchronize(c->stream);
         if (n_ksk) (void)hipFree(n_ksk);
         if (n_planes) (void)hipFree(n_planes);
         if (n_bsk) (void)hipFree(n_bsk);
         if (n_quad) (void)hipFree(n_quad);
+        if (n_pair) (void)hipFree(n_pair);
     };
     hipError_t he = hipMalloc(&n_ksk, ksk_words * 8);
     if (he == hipSuccess) he = hipMalloc(&n_planes, fhe::ks_planes_bytes((int)p.n));
     if (he == hipSuccess) he = hipMalloc(&n_bsk, bsk_doubles * 8);
     if (he == hipSuccess) he = hipMalloc(&n_quad, bsk_doubles * 8);
+    if (he == hipSuccess && p.grouping == 1) he = hipMalloc(&n_pair, bsk_doubles * 8);
     if (he != hipSuccess) {
         drop_new();
         set_error(std::string("broadcast_server_key: ") + hipGetErrorString(he));
@@ -207,6 +209,7 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
                          "ncclBroadcast", tmo, false);
     if (!rc) rc = launch_ksk_to_planes(n_ksk, (int)p.n, n_planes, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = launch_bsk_to_quad(n_bsk, npoly, n_quad, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc && n_pair) rc = launch_bsk_to_pair(n_bsk, npoly, n_pair, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (rc) {
         drop_new();
@@ -226,6 +229,7 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     std::swap(c->d_ksk_planes, n_planes);
     std::swap(c->d_bsk, n_bsk);
     std::swap(c->d_bsk_quad, n_quad);
+    std::swap(c->d_bsk_pair, n_pair);
     drop_new();  // frees the previous key's buffers (null when there was none)
     if (!(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
         c->lut_ids.clear();

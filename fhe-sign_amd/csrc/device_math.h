@@ -150,6 +150,33 @@ FHE_DEV uint32_t modswitch_2n(uint64_t x) {  // 2^64 -> 2N = 4096
     return (uint32_t)((((x >> 51) + 1) >> 1) & 4095u);
 }
 
+// ---- register transposes: a register bit of a pair of complex registers <-> lane bit 5 or 4
+FHE_DEV void qsplit(double d, uint32_t& lo, uint32_t& hi) {
+    const uint64_t b = (uint64_t)__double_as_longlong(d);
+    lo = (uint32_t)b;
+    hi = (uint32_t)(b >> 32);
+}
+FHE_DEV double qjoin(uint32_t lo, uint32_t hi) { return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)); }
+// X holds register bit 0, Y register bit 1 of the pair; afterwards that register bit and lane bit K
+// are swapped.  K = 5, 4: v_permlane32_swap / v_permlane16_swap, one instruction per dword pair.
+template <int K>
+FHE_DEV void qx_permlane(cplx& X, cplx& Y) {
+    uint32_t x[4], y[4];
+    qsplit(X.x, x[0], x[1]);
+    qsplit(X.y, x[2], x[3]);
+    qsplit(Y.x, y[0], y[1]);
+    qsplit(Y.y, y[2], y[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        auto r = K == 5 ? __builtin_amdgcn_permlane32_swap(x[d], y[d], false, false)
+                        : __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+        x[d] = r[0];
+        y[d] = r[1];
+    }
+    X = make_double2(qjoin(x[0], x[1]), qjoin(x[2], x[3]));
+    Y = make_double2(qjoin(y[0], y[1]), qjoin(y[2], y[3]));
+}
+
 // wave-level LDS ordering (rocPRIM wave_barrier idiom)
 FHE_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
