@@ -39,6 +39,11 @@
 #ifndef QCL_D
 #define QCL_D 4
 #endif
+// G = 1: MAC split around the digit-swap barrier (own row prefetched whole, other row loaded as
+// the own products free its registers) instead of the QCL_D-deep ring
+#ifndef QCL_SPLIT
+#define QCL_SPLIT 1
+#endif
 
 namespace fhe {
 
@@ -327,15 +332,20 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         q_xpose_bc(x);
         // BSK ring head, in flight across phase C and the digit swap
         constexpr int QR = G == 1 ? QCL_D : QMB_D;
-        cplx Bq0[G == 1 ? QR : 3 * QR], Bq1[G == 1 ? QR : 3 * QR];
+        cplx Bq0[G == 1 ? (QCL_SPLIT ? 8 : QR) : 3 * QR], Bq1[G == 1 ? (QCL_SPLIT ? 8 : QR) : 3 * QR];
         cplx em[G == 2 ? 3 : 1];  // G = 2: monomials of the current register pair, per pattern
         cplx eb[G == 2 ? 3 : 1];  // G = 2: lane factors of the group, per pattern
         if constexpr (G == 1) {
+#if QCL_SPLIT
+#pragma unroll
+        for (int r = 0; r < 8; ++r) Bq0[r] = bm[r * 64];  // the whole own-row slice
+#else
 #pragma unroll
         for (int r = 0; r < QR; ++r) {
             Bq0[r] = bm[r * 64];
             Bq1[r] = bo[r * 64];
         }
+#endif
         } else {
 #pragma unroll
         for (int B = 0; B < 3; ++B) {
@@ -364,9 +374,25 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         wave_sync();
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bC + fq(2 * r)] = x[r];
+#if QCL_SPLIT
+        // G = 1: mac2 = own digit x row p + other digit x row 1 - p (its two rounded products and
+        // their sum), split around the barrier; the other row's loads go out as the own row's
+        // registers free up
+        if constexpr (G == 1) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                x[r] = cmul(x[r], Bq0[r]);
+                Bq1[r] = bo[r * 64];
+            }
+        }
+#endif
         __syncthreads();
         // mac2 is symmetric in its two rows: own digit x BSK row p, other digit x row 1 - p
         if constexpr (G == 1) {
+#if QCL_SPLIT
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = cadd(x[r], cmul(other[bC + fq(2 * r)], Bq1[r]));
+#else
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const cplx Bm = Bq0[r % QR], Bo = Bq1[r % QR];
@@ -376,6 +402,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             }
             x[r] = mac2(x[r], Bm, other[bC + fq(2 * r)], Bo);
         }
+#endif
         } else {
         // key bundle per point (oracle cmul_acc, patterns in order), then the MAC; the slice of the
         // next registers stream in behind (QR registers ahead), the monomials per register pair
