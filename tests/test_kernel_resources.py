@@ -30,18 +30,21 @@ def descriptors(src, tmp_path):
 
 
 @pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src,kernel,lds_per_cu_ok,max_regs", [
-    ("br_wide.hip", "k_blind_rotate_wideILi1", 1, 256),  # one 8-wave workgroup per CU (classic)
-    ("br_wide.hip", "k_blind_rotate_wideILi2", 1, 256),  # the same, multi-bit
-    ("br_quad.hip", "k_blind_rotate_quadILi1", 3, 168),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
-    ("br_quad.hip", "k_blind_rotate_quadILi2", 2, 256),  # multi-bit: 2 per CU, 2 waves/SIMD, deeper BSK ring
+@pytest.mark.parametrize("src,kernel,lds_per_cu_ok,max_regs,max_scratch", [
+    ("br_wide.hip", "k_blind_rotate_wideILi1", 1, 256, 0),  # one 8-wave workgroup per CU (classic)
+    ("br_wide.hip", "k_blind_rotate_wideILi2", 1, 256, 0),  # the same, multi-bit
+    ("br_quad.hip", "k_blind_rotate_quadILi1", 3, 168, 0),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
+    ("br_quad.hip", "k_blind_rotate_quadILi2", 2, 256, 0),  # multi-bit: 2 per CU, 2 waves/SIMD, deeper BSK ring
+    # opt-in pair kernel: 2 two-ciphertext workgroups per CU, 2 waves/SIMD; its 112 B of scratch are
+    # loop-invariant values reloaded once per CMUX (profiles/r2/ab_pair_r2.txt)
+    ("br_pair.hip", "k_blind_rotate_pair", 2, 256, 128),
 ])
-def test_blind_rotate_occupancy(tmp_path, src, kernel, lds_per_cu_ok, max_regs):
+def test_blind_rotate_occupancy(tmp_path, src, kernel, lds_per_cu_ok, max_regs, max_scratch):
     d = descriptors(os.path.join(CSRC, src), tmp_path)
     ks = [v for k, v in d.items() if kernel in k]
     assert ks, f"{kernel} not found in {src}"
     for f in ks:
         total = max(f["next_free_vgpr"], f["accum_offset"])
         assert total <= max_regs, f"{kernel}: {f['next_free_vgpr']} registers -> below the designed occupancy"
-        assert f["private_segment_fixed_size"] == 0, f"{kernel}: scratch spill"
+        assert f["private_segment_fixed_size"] <= max_scratch, f"{kernel}: scratch spill"
         assert f["group_segment_fixed_size"] * lds_per_cu_ok <= 160 * 1024, f"{kernel}: LDS limits occupancy"

@@ -2,7 +2,7 @@
 # Profiling session (run on the GPU box via gpurun).  Kernel trace + stats of the exact bench
 # command whose roofline lines are reported (classic headline and the multi-bit variant), a trace of
 # the ops legs, then separate PMC passes (never combined with other trace domains) over one launch
-# of the throughput kernel (B=8192) and one of the latency kernel (B=256), classic and multi-bit.
+# of the throughput kernel (B=32768, the bench batch) and one of the latency kernel (B=256), classic and multi-bit.
 # Output under gpurun_out/$1; summarise with tools/pmc_summary.py gpurun_out/$1 profiles/rN/...json
 set -o pipefail
 OUT=gpurun_out/${1:-prof}
@@ -12,7 +12,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_ops -o run --output-format csv -- python3 tools/ops_timing.py > $OUT/ops_under_trace.log 2>&1 || exit 2
 for kind in cl mb; do
   if [ $kind = mb ]; then export FHE_PROBE_MB=1; else unset FHE_PROBE_MB; fi
-  for B in 8192 256; do
+  for B in 32768 256; do
     P="python3 tools/pbs_probe.py $B 1"
     D=$OUT/pmc_${kind}_$B
     run() { local n=$1; shift; timeout -k 10 120 rocprofv3 --pmc "$@" --kernel-trace -d $D/$n -o run --output-format csv -- $P > $D.$n.log 2>&1; }
