@@ -24,6 +24,10 @@
 #include "device_math.h"
 #include "kernels.h"
 
+#ifndef PAIR_CTS
+#define PAIR_CTS 2  // ciphertexts per workgroup (lock-stepped: they share each BSK line in L1)
+#endif
+
 namespace fhe {
 
 namespace {
@@ -43,20 +47,20 @@ FHE_DEV cplx zi(cplx z, bool odd) { return odd ? mul_i(z) : z; }
 }  // namespace
 
 
-__global__ __launch_bounds__(256, 2) void k_blind_rotate_pair(const uint64_t* __restrict__ ms, int ms_stride,
+__global__ __launch_bounds__(128 * PAIR_CTS, 2) void k_blind_rotate_pair(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
                                                               const uint32_t* __restrict__ lut_idx,
                                                               const uint64_t* __restrict__ luts,
                                                               const cplx* __restrict__ bsk,  // pair layout
                                                               const cplx* __restrict__ tab,  // pair_tables
                                                               uint64_t* __restrict__ out, int count, int n) {
-    __shared__ __attribute__((aligned(16))) cplx s_x[4][PR_SLOTS];
+    __shared__ __attribute__((aligned(16))) cplx s_x[2 * PAIR_CTS][PR_SLOTS];
     __shared__ __attribute__((aligned(16))) cplx s_t[PT_LDS];
-    for (int k = threadIdx.x; k < PT_LDS; k += 256) s_t[k] = tab[k];
+    for (int k = threadIdx.x; k < PT_LDS; k += 128 * PAIR_CTS) s_t[k] = tab[k];
     __syncthreads();
     const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
     const int p = w & 1;
-    const int ct_raw = 2 * (int)blockIdx.x + (w >> 1);
+    const int ct_raw = PAIR_CTS * (int)blockIdx.x + (w >> 1);
     const bool live = ct_raw < count;
     const int ct = live ? ct_raw : count - 1;  // an odd batch's spare ciphertext repeats the last one, unwritten
     cplx* reg = s_x[w];
@@ -319,7 +323,8 @@ hipError_t launch_blind_rotate_pair(const uint64_t* ms, int ms_stride, const Pbs
                                     const uint64_t* luts, const cplx* bsk_pair, const cplx* tab, uint64_t* out,
                                     int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blind_rotate_pair, dim3((count + 1) / 2), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
+    hipLaunchKernelGGL(k_blind_rotate_pair, dim3((count + PAIR_CTS - 1) / PAIR_CTS), dim3(128 * PAIR_CTS), 0, s, ms,
+                       ms_stride, desc, lut_idx, luts,
                        bsk_pair, tab, out, count, n);
     return hipGetLastError();
 }
