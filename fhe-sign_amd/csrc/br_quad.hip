@@ -44,6 +44,10 @@
 #ifndef QCL_SPLIT
 #define QCL_SPLIT 1
 #endif
+// G = 1: rotation reads with the region base as an immediate offset (one VALU op less per read)
+#ifndef QROT_IMM
+#define QROT_IMM 1
+#endif
 
 namespace fhe {
 
@@ -195,17 +199,22 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                                                               const cplx* __restrict__ zq,  // quad_zetas
                                                               const cplx* __restrict__ mono,  // E[4096] (G = 2)
                                                               uint64_t* __restrict__ out, int n) {
-    __shared__ __attribute__((aligned(16))) cplx s_x[2][QX_SZ];
-    __shared__ __attribute__((aligned(16))) cplx s_w[QTW_SZ];
-    __shared__ __attribute__((aligned(16))) cplx s_z[QZ_LDS];
-    // G = 2: this group's monomials E[(4 j + 1) m_B] of every lane's register pairs, [pair k][B][h][lane]
-    __shared__ __attribute__((aligned(16))) cplx s_mono[G == 2 ? 3 * 2 * 64 : 1];  // [B][h][lane]
+    // one LDS block (the kernel's only LDS object, so it starts at address 0): the polynomials'
+    // exchange regions first -- the rotation reads address them with immediate offsets (QROT_IMM)
+    constexpr int QL_W = 2 * QX_SZ, QL_Z = QL_W + QTW_SZ, QL_M = QL_Z + QZ_LDS;
+    __shared__ __attribute__((aligned(16))) cplx s_lds[QL_M + (G == 2 ? 3 * 2 * 64 : 1)];
+    cplx(*s_x)[QX_SZ] = reinterpret_cast<cplx(*)[QX_SZ]>(s_lds);
+    cplx* s_w = s_lds + QL_W;
+    cplx* s_z = s_lds + QL_Z;
+    // G = 2: this group's monomials E[(4 j + 1) m_B] of every lane's register pairs, [B][h][lane]
+    cplx* s_mono = s_lds + QL_M;
     for (int k = threadIdx.x; k < 512; k += 256) s_w[tpos(k)] = W[k];
     for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[k] = zq[k];
     __syncthreads();
     const int ct = blockIdx.x;
     const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
     const int p = w >> 1, h = w & 1, t = threadIdx.x & 127;
+    const int p_u = __builtin_amdgcn_readfirstlane(p);  // wave-uniform (scalar branch)
     cplx* reg = s_x[p];
     const cplx* other = s_x[p ^ 1];
     double* rot = reinterpret_cast<double*>(reg);
@@ -297,6 +306,42 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         __syncthreads();
         double dg[16];  // digits of X^a acc - acc (all 16 rotated reads issued before the first use)
         double rv[16];
+#if QROT_IMM
+        // byte offsets of the source coefficients (128 r + t - a) mod 4096: bits 0..13 address the
+        // region (mod 2048), bit 14 is the negacyclic sign.  Each polynomial's waves run their own
+        // copy of the reads with the region base as the immediate offset (inline asm: the compiler
+        // would fold the two copies into one with a base register add); lgkmcnt drained by hand.
+        uint32_t yy[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yy[r] = (((uint32_t)(t - (int)a) & 4095u) << 3) + 1024u * r;
+        uint32_t ad[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ad[r] = yy[r] & 0x3FFFu;
+        // the 16 reads and the wait in ONE asm statement: the compiler sees the results only after
+        // the wait (split statements let it copy a result register before its data arrived)
+#define QROT_READS(OFF)                                                                                         \
+    asm volatile("ds_read_b64 %0, %16" OFF "\n\tds_read_b64 %1, %17" OFF "\n\tds_read_b64 %2, %18" OFF         \
+                 "\n\tds_read_b64 %3, %19" OFF "\n\tds_read_b64 %4, %20" OFF "\n\tds_read_b64 %5, %21" OFF        \
+                 "\n\tds_read_b64 %6, %22" OFF "\n\tds_read_b64 %7, %23" OFF "\n\tds_read_b64 %8, %24" OFF        \
+                 "\n\tds_read_b64 %9, %25" OFF "\n\tds_read_b64 %10, %26" OFF "\n\tds_read_b64 %11, %27" OFF      \
+                 "\n\tds_read_b64 %12, %28" OFF "\n\tds_read_b64 %13, %29" OFF "\n\tds_read_b64 %14, %30" OFF    \
+                 "\n\tds_read_b64 %15, %31" OFF "\n\ts_waitcnt lgkmcnt(0)"                                         \
+                 : "=&v"(rv[0]), "=&v"(rv[1]), "=&v"(rv[2]), "=&v"(rv[3]), "=&v"(rv[4]), "=&v"(rv[5]),          \
+                   "=&v"(rv[6]), "=&v"(rv[7]), "=&v"(rv[8]), "=&v"(rv[9]), "=&v"(rv[10]), "=&v"(rv[11]),        \
+                   "=&v"(rv[12]), "=&v"(rv[13]), "=&v"(rv[14]), "=&v"(rv[15])                                  \
+                 : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]),          \
+                   "v"(ad[7]), "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]),      \
+                   "v"(ad[14]), "v"(ad[15]))
+        if (p_u == 0) {
+            QROT_READS("");
+        } else {
+            QROT_READS(" offset:17488");  // QX_SZ * 16: the second polynomial's region
+        }
+#undef QROT_READS
+        static_assert(QX_SZ * 16 == 17488, "region offset of the rotation reads");
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dg[r] = tor_digit_s(neg_bit14(rv[r], yy[r]) - acc[r]);
+#else
         uint32_t uu[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -305,6 +350,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) dg[r] = tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]);
+#endif
         __syncthreads();  // every rotation read done before the region is reused
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = make_double2(dg[r], dg[r + 8]);

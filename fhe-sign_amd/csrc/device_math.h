@@ -132,6 +132,13 @@ FHE_DEV double neg_bit11(double v, uint32_t u) {
     asm("v_lshl_add_u32 %0, %1, 20, %2" : "=v"(hi) : "v"(u & 2048u), "v"((uint32_t)(b >> 32)));
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint32_t)b));
 }
+// the same with the sign at bit 14 of a byte offset (8-byte coefficients: bit 11 of the index)
+FHE_DEV double neg_bit14(double v, uint32_t y) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    uint32_t hi;
+    asm("v_lshl_add_u32 %0, %1, 17, %2" : "=v"(hi) : "v"(y & 0x4000u), "v"((uint32_t)(b >> 32)));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint32_t)b));
+}
 // v or -v by a lane bit (negbit = 0 or 1 << 31 applied to the high word): exact, one VALU op
 FHE_DEV double neg_if(double v, uint32_t negbit) {
     const uint64_t b = (uint64_t)__double_as_longlong(v) ^ ((uint64_t)negbit << 32);

@@ -138,6 +138,12 @@ uint64_t reachable(const std::vector<Term>& terms, int64_t cst, bool* ok) {
 }  // namespace
 
 Blocks Engine::run(std::vector<PbsItem>& items) {
+    struct Clock {  // host time inside run() (FHE_TRACE_LEVELS: printed at the next flush)
+        Engine* e;
+        std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+        ~Clock() { e->run_ns_ += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count(); }
+    } clock{this};
+    ++run_calls_;
     const Params& p = ctx_->p;
     const uint32_t mc = p.msg_carry();
     Blocks out(items.size());
@@ -325,6 +331,11 @@ void Engine::flush() {
     const size_t N = pending_.size();
     if (N == 0) return;
     const auto f0 = std::chrono::steady_clock::now();
+    if (trace_) {
+        fprintf(stderr, "[host] %zu run() calls, %.3f ms inside run() since the last flush\n", run_calls_, run_ns_ * 1e-6);
+        run_ns_ = 0.0;
+        run_calls_ = 0;
+    }
     std::vector<std::vector<int32_t>> deps(N);
     for (size_t k = 0; k < N; ++k) deps[k] = pending_[k].deps;
     // a fanned-out level's round is one latency-kernel round on every rank

@@ -126,6 +126,8 @@ private:
     size_t up_cap_ = 0;
     bool trace_ = false;
     int sched_ = 0;
+    double run_ns_ = 0.0;  // host time inside run() (trace)
+    size_t run_calls_ = 0;
     static constexpr size_t kEagerBatch = 4096;
     bool eager_ok_ = true;
     struct Pending {
