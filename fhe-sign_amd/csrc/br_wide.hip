@@ -281,15 +281,22 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             const int c = 256 * r + 4 * L + q;
             rot_me[c + (c >> 2)] = acc[r];
         }
-        __syncthreads();
         double rv[8];  // all 8 rotated reads issued before the first use
-        uint32_t uu[8];
+        uint32_t uu[8], off[8];
+        // element c of the padded region sits at byte 8 (c + c / 4) = (10 c) & ~7: one 24-bit
+        // multiply-add with the region's (8-aligned) LDS address, one mask; computed before the
+        // barrier (the empty asm pins them there) so the 8 reads issue back to back after it
+        const uint32_t rot_addr = lds_off(rot_me);
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) {
             uu[rr] = (uint32_t)(256 * rr + 4 * L + q - (int)a) & 4095u;
-            const uint32_t c = uu[rr] & 2047u;
-            rv[rr] = rot_me[c + (c >> 2)];
+            off[rr] = (__umul24(uu[rr] & 2047u, 10u) + rot_addr) & ~7u;
         }
+        asm volatile("" ::"v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
+                     "v"(off[7]));
+        __syncthreads();
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) rv[rr] = *(const __attribute__((address_space(3))) double*)(size_t)off[rr];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             x[r] = make_double2(tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]),
