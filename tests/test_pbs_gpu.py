@@ -144,13 +144,14 @@ def test_pair_kernel_bit_identical(env):
 def test_keyswitch_kernels_identical(env):
     """The int8 matrix-core keyswitch (ks_mfma.hip: byte-plane contraction) and the 64-bit VALU
     keyswitch are both exact: the bootstraps they feed give identical words, equal to the oracle.
-    Batches of 1, 16, 37 (ragged tiles) and 130."""
+    Batches of 1, 16, 37 (ragged tiles), 130 and 4160 (the blocked path, ragged)."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = [ctx.lut(t) for t in tables]
     r = ok.rng(4242)
-    for count in (1, 16, 37, 130):
-        cts = np.stack([ok.encrypt(r, i % 16) for i in range(count)])
+    base = np.stack([ok.encrypt(r, i % 16) for i in range(130)])
+    for count in (1, 16, 37, 130, 4160):  # 4160: the blocked MFMA path (4 tiles per wave), ragged end
+        cts = np.ascontiguousarray(np.resize(base, (count, base.shape[1])))
         lut_ids = np.array([ids[i % len(ids)] for i in range(count)], np.uint32)
         try:
             ctx.set_ks_kernel(0)

@@ -1,7 +1,7 @@
 """Quick PBS throughput probe (device-resident batch), used while developing kernels."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
+sys.path.insert(0, os.environ.get("FHE_PROBE_PKG") or os.path.join(ROOT, "fhe-sign_amd"))  # a build_variants/ dir
 import numpy as np
 import fhe_sign
 from fhe_sign import Context, generate_keys
