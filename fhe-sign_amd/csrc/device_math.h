@@ -223,7 +223,7 @@ FHE_DEV cplx sload(const cplx* base, uint32_t uniform_idx) {
 // write to every LDS object and drains it (vmcnt(0)) before the next LDS access anywhere in the
 // kernel.  The caller retires it itself: VMEM loads return in order, so any wait for a load issued
 // after it (the compiler's own vmcnt for that load) also retires the DMA; a barrier after that
-// publishes the bytes to the workgroup.  M0 (the LDS base) is saved and restored.
+// publishes the bytes to the workgroup.  M0 (the LDS base, wave-uniform) is saved and restored.
 FHE_DEV uint32_t lds_off(const void* p) { return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p; }
 // The same through a buffer resource (base in SGPRs, one VGPR byte offset per lane)
 typedef int __attribute__((ext_vector_type(4))) rsrc_t;
@@ -240,14 +240,14 @@ FHE_DEV void dma16_buf(rsrc_t rs, uint32_t byte_off, uint32_t lds_base) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(byte_off), "s"(rs), "s"(lds_base)
+                 : "v"(byte_off), "s"(rs), "s"(__builtin_amdgcn_readfirstlane(lds_base))
                  : "memory");
 }
 FHE_DEV void dma16(const cplx* src, uint32_t lds_base) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(src), "s"(lds_base)
+                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_base))
                  : "memory");
 }
 

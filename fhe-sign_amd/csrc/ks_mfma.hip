@@ -89,42 +89,85 @@ __global__ __launch_bounds__(256) void k_ks_digits(const uint64_t* __restrict__ 
     }
 }
 
-// out[ct][t] for a 64-ciphertext x 16-column tile: wave w owns ciphertext tile 4 blockIdx.x + w.
+// out[ct][t] for a (64 CW)-ciphertext x 16-column tile: wave w owns the CW ciphertext tiles
+// CW (4 blockIdx.x + w) + c.  The four waves of a workgroup share one column tile, so each of the 8
+// byte-plane fragments of a k-tile is fetched once per workgroup (two per wave) and read by every
+// wave from LDS; a wave's CW digit fragments are reused over the 8 planes.  All loads are LDS-DMAs
+// issued two k-tiles ahead (the digit fragments too, so that no register load makes the compiler
+// drain the DMA queue), retired by explicit vmcnt waits: VMEM returns in order and each wave has
+// CW + 2 DMAs per k-tile in flight.  Every wave takes part in the staging and the barriers; tiles
+// past the batch skip only the stores.  (Per-wave register loads of the planes: 8.1 ms per 32768
+// keyswitches, TA 98 % busy; this kernel at CW = 1: 4.6 ms.)
+template <int CW>
 __global__ __launch_bounds__(256) void k_ks_mfma(const int8_t* __restrict__ digits, const uint64_t* __restrict__ body,
                                                  const int8_t* __restrict__ planes, int tiles, int count, int n,
                                                  uint64_t* __restrict__ small, int stride) {
+    constexpr int D = 3;  // staging depth (k-tiles)
+    __shared__ __attribute__((aligned(16))) int8_t sb[D][8][1024];
+    __shared__ __attribute__((aligned(16))) int8_t sa[D][4 * CW][1024];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const size_t ctile = (size_t)blockIdx.x * 4 + w;
+    const size_t ctile0 = ((size_t)blockIdx.x * 4 + w) * CW;  // inside the digit buffer (ks_digits_bytes)
     const int tt = blockIdx.y;
-    if ((int)(ctile * 16) >= count) return;
-    const v4i* A = reinterpret_cast<const v4i*>(digits + frag_off(ctile, 0, lane));
-    const v4i* B = reinterpret_cast<const v4i*>(planes + frag_off(tt, 0, lane));
-    const size_t plane = (size_t)tiles * KS_KT * 64;  // v4i per plane
-    v4i acc[8];
+    const int8_t* A = digits + frag_off(ctile0, 0, lane);
+    const size_t plane = (size_t)tiles * KS_KT * 1024;  // bytes per plane
+    const rsrc_t rs = buffer_rsrc(planes, (uint32_t)(8 * plane));
+    auto stage = [&](int kt) {
 #pragma unroll
-    for (int b = 0; b < 8; ++b) acc[b] = v4i{0, 0, 0, 0};
-#pragma unroll 2
+        for (int c = 0; c < CW; ++c)
+            dma16(reinterpret_cast<const cplx*>(A + ((size_t)c * KS_KT + kt) * 1024), lds_off(&sa[kt % D][CW * w + c][0]));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int b = 2 * w + j;
+            dma16_buf(rs, (uint32_t)(b * plane + frag_off(tt, kt, lane)), lds_off(&sb[kt % D][b][0]));
+        }
+    };
+    stage(0);
+    stage(1);
+    v4i acc[CW][8];
+#pragma unroll
+    for (int c = 0; c < CW; ++c)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[c][b] = v4i{0, 0, 0, 0};
     for (int kt = 0; kt < KS_KT; ++kt) {
-        const v4i a = A[kt * 64];
+        // this wave's DMAs of k-tile kt have landed (in flight after them: k-tile kt + 1's)
+        if (kt + 1 < KS_KT)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CW + 2) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave's fragments of kt visible; every read of k-tile kt - 1 done
+        if (kt + 2 < KS_KT) stage(kt + 2);  // into the buffers k-tile kt - 1 used
+        v4i a[CW];
 #pragma unroll
-        for (int b = 0; b < 8; ++b) acc[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, B[b * plane + kt * 64], acc[b], 0, 0, 0);
+        for (int c = 0; c < CW; ++c) a[c] = reinterpret_cast<const v4i*>(&sa[kt % D][CW * w + c][0])[lane];
+        const v4i* sbk = reinterpret_cast<const v4i*>(&sb[kt % D][0][0]) + lane;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const v4i bb = sbk[b * 64];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) acc[c][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[c], bb, acc[c][b], 0, 0, 0);
+        }
     }
     const int t = 16 * tt + (lane & 15);
     if (t > n) return;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int ct = (int)ctile * 16 + 4 * (lane >> 4) + r;
-        if (ct >= count) continue;
-        uint64_t v = 0;
+    for (int c = 0; c < CW; ++c)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) v += (uint64_t)(int64_t)acc[b][r] << (8 * b);
-        small[(size_t)ct * stride + t] = (t == n ? body[ct] : 0ull) - v;
-    }
+        for (int r = 0; r < 4; ++r) {
+            const int ct = (int)(ctile0 + c) * 16 + 4 * (lane >> 4) + r;
+            if (ct >= count) continue;
+            uint64_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) v += (uint64_t)(int64_t)acc[c][b][r] << (8 * b);
+            small[(size_t)ct * stride + t] = (t == n ? body[ct] : 0ull) - v;
+        }
 }
 
 int ks_plane_tiles(int n) { return (n + 1 + 15) / 16; }
 size_t ks_planes_bytes(int n) { return (size_t)8 * ks_plane_tiles(n) * KS_KT * 1024; }
-size_t ks_digits_bytes(int count) { return (size_t)((count + 63) / 64) * 4 * KS_KT * 1024; }
+#ifndef KS_CW
+#define KS_CW 2  // ciphertext tiles per wave
+#endif
+size_t ks_digits_bytes(int count) { return (size_t)((count + 127) / 128) * 8 * KS_KT * 1024; }
 
 hipError_t launch_ksk_to_planes(const uint64_t* ksk, int n, int8_t* planes, hipStream_t s) {
     const int tiles = ks_plane_tiles(n);
@@ -140,8 +183,8 @@ hipError_t launch_keyswitch_mfma(const uint64_t* in, const PbsDesc* desc, int co
     else
         hipLaunchKernelGGL(k_ks_digits<false>, dim3(count), dim3(256), 0, s, in, nullptr, digits, body);
     const int tiles = ks_plane_tiles(n);
-    hipLaunchKernelGGL(k_ks_mfma, dim3((count + 63) / 64, tiles), dim3(256), 0, s, digits, body, planes, tiles, count, n,
-                       small, stride);
+    hipLaunchKernelGGL(k_ks_mfma<KS_CW>, dim3((count + 64 * KS_CW - 1) / (64 * KS_CW), tiles), dim3(256), 0, s, digits,
+                       body, planes, tiles, count, n, small, stride);
     return hipGetLastError();
 }
 
