@@ -195,9 +195,8 @@ __global__ __launch_bounds__(128 * PAIR_CTS, 2) void k_blind_rotate_pair(const u
             }
         }
 
-        // ---- MAC = own digit x row p + other digit x row 1 - p (mac2's two rounded products and
-        // their sum, split around the exchange); the other row's loads go out as the own row's
-        // registers free up
+        // ---- MAC = own digit x row p, then other digit x row 1 - p accumulated (mac2, split around
+        // the exchange); the other row's loads go out as the own row's registers free up
         cplx Bo[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
@@ -208,7 +207,7 @@ __global__ __launch_bounds__(128 * PAIR_CTS, 2) void k_blind_rotate_pair(const u
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
             if (c == 8) asm volatile("" ::: "memory");  // at most 8 partner digits in flight (registers)
-            x[c] = cadd(x[c], cmul(other[64 * c + L], Bo[c]));
+            x[c] = cmul_acc(x[c], other[64 * c + L], Bo[c]);
         }
 
         // ---- inverse: phase C (stage 9 plain, stage 8 unit twiddles 1 / -i)

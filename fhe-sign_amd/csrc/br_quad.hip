@@ -212,9 +212,9 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[k] = zq[k];
     __syncthreads();
     const int ct = blockIdx.x;
-    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;  // w in an SGPR
     const int p = w >> 1, h = w & 1, t = threadIdx.x & 127;
-    const int p_u = __builtin_amdgcn_readfirstlane(p);  // wave-uniform (scalar branch)
+    const int p_u = p;  // wave-uniform (scalar branch)
     cplx* reg = s_x[p];
     const cplx* other = s_x[p ^ 1];
     double* rot = reinterpret_cast<double*>(reg);
@@ -421,9 +421,9 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bC + fq(2 * r)] = x[r];
 #if QCL_SPLIT
-        // G = 1: mac2 = own digit x row p + other digit x row 1 - p (its two rounded products and
-        // their sum), split around the barrier; the other row's loads go out as the own row's
-        // registers free up
+        // G = 1: mac2 = own digit x row p (the rounded product), then other digit x row 1 - p
+        // accumulated into it, split around the barrier; the other row's loads go out as the own
+        // row's registers free up
         if constexpr (G == 1) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
@@ -433,11 +433,11 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
 #endif
         __syncthreads();
-        // mac2 is symmetric in its two rows: own digit x BSK row p, other digit x row 1 - p
+        // mac2: own digit x BSK row p, then other digit x row 1 - p accumulated
         if constexpr (G == 1) {
 #if QCL_SPLIT
 #pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = cadd(x[r], cmul(other[bC + fq(2 * r)], Bq1[r]));
+        for (int r = 0; r < 8; ++r) x[r] = cmul_acc(x[r], other[bC + fq(2 * r)], Bq1[r]);
 #else
 #pragma unroll
         for (int r = 0; r < 8; ++r) {

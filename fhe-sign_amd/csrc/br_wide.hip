@@ -371,7 +371,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         ct2_last(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
         ct2_last(y, ZT[8], ZT[9]);
 
-        // ---- pointwise MAC (symmetric: own digit x row p, other digit x row 1 - p)
+        // ---- pointwise MAC (own digit x row p, then other digit x row 1 - p accumulated)
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], Kown[r], y[r], Koth[r]);
 

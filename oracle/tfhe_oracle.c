@@ -468,6 +468,18 @@ static void poly_rotate_d(const double* v, uint32_t r, double* out) {
     }
 }
 
+/* One Fourier point of output polynomial w of the external product, D0 K_0w + D1 K_1w (row r of
+ * column w: kr[r] + i ki[r]), as the GPU kernels form it: the product of the output's own digit
+ * D_w, rounded, then the other digit's product accumulated with two fmas per component (a wave
+ * holds the digit of the polynomial it outputs). */
+static void mac_own_first(const double* D0, const double* D1, const double* kr, const double* ki, int w, double* o) {
+    const double* dn = w ? D1 : D0; /* own */
+    const double* dx = w ? D0 : D1; /* other */
+    const double pr = fma(dn[0], kr[w], -(dn[1] * ki[w])), pi = fma(dn[0], ki[w], dn[1] * kr[w]);
+    o[0] = fma(dx[0], kr[1 - w], fma(-dx[1], ki[1 - w], pr));
+    o[1] = fma(dx[0], ki[1 - w], fma(dx[1], kr[1 - w], pi));
+}
+
 /* Blind rotation ACC = X^{-b} LUT, then n CMUX.  The accumulator's torus coefficients are kept as
  * f64 representatives in [-2^63, 2^63] instead of u64: X^a acc - acc is one f64 subtraction, its
  * gadget digit two rint's (fho_tor_digit, exact integers, no int->f64 conversion), and the external
@@ -543,9 +555,7 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
                             ki[row] = fma(G[0], wi, fma(G[1], wr, ki[row]));
                         }
                     }
-                    const double d0r = D0[2 * q], d0i = D0[2 * q + 1], d1r = D1[2 * q], d1i = D1[2 * q + 1];
-                    O[2 * q] = fma(d0r, kr[0], -(d0i * ki[0])) + fma(d1r, kr[1], -(d1i * ki[1]));
-                    O[2 * q + 1] = fma(d0r, ki[0], d0i * kr[0]) + fma(d1r, ki[1], d1i * kr[1]);
+                    mac_own_first(D0 + 2 * q, D1 + 2 * q, kr, ki, w, O + 2 * q);
                 }
                 fho_fourier_add_to_poly(O, w ? acc1 : acc0);
             }
@@ -565,12 +575,8 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
             const double* B0 = bi + (0 * 2 + w) * FHO_HALF * 2; /* row 0 (mask digit), poly w */
             const double* B1 = bi + (1 * 2 + w) * FHO_HALF * 2; /* row 1 (body digit), poly w */
             for (int q = 0; q < FHO_HALF; ++q) {
-                double d0r = D0[2 * q], d0i = D0[2 * q + 1], d1r = D1[2 * q], d1i = D1[2 * q + 1];
-                double b0r = B0[2 * q], b0i = B0[2 * q + 1], b1r = B1[2 * q], b1i = B1[2 * q + 1];
-                /* D0 B0 + D1 B1 as a sum of two products: symmetric in the two rows, so a GPU wave
-                 * may hold either digit as its own */
-                O[2 * q] = fma(d0r, b0r, -(d0i * b0i)) + fma(d1r, b1r, -(d1i * b1i));
-                O[2 * q + 1] = fma(d0r, b0i, d0i * b0r) + fma(d1r, b1i, d1i * b1r);
+                const double br[2] = {B0[2 * q], B1[2 * q]}, bi[2] = {B0[2 * q + 1], B1[2 * q + 1]};
+                mac_own_first(D0 + 2 * q, D1 + 2 * q, br, bi, w, O + 2 * q);
             }
             fho_fourier_add_to_poly(O, w ? acc1 : acc0);
         }
