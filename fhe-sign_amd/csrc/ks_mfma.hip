@@ -59,10 +59,13 @@ __global__ __launch_bounds__(64) void k_ksk_to_planes(const uint64_t* __restrict
 }
 
 // Digits of one ciphertext per workgroup (input = a contiguous block or a PbsDesc linear
-// combination), staged in LDS and stored as 16-byte fragment rows; body word kept aside.
+// combination), staged in LDS and stored as 16-byte fragment rows; body word kept aside.  With
+// init (split contraction, below) the output row is set to (0, .., 0, body) for the partial sums
+// to be subtracted from.
 template <bool DESC>
 __global__ __launch_bounds__(256) void k_ks_digits(const uint64_t* __restrict__ in, const PbsDesc* __restrict__ desc,
-                                                   int8_t* __restrict__ digits, uint64_t* __restrict__ body) {
+                                                   int8_t* __restrict__ digits, uint64_t* __restrict__ body,
+                                                   uint64_t* __restrict__ init, int stride, int n) {
     __shared__ int8_t sd[KS_K];
     const int ct = blockIdx.x;
     for (int j = threadIdx.x; j < 2048; j += 256) {
@@ -80,6 +83,9 @@ __global__ __launch_bounds__(256) void k_ks_digits(const uint64_t* __restrict__ 
         }
     }
     if (threadIdx.x == 0) body[ct] = ks_input<DESC>(in, desc, ct, 2048);
+    if (init)
+        for (int t = threadIdx.x; t <= n; t += 256)
+            init[(size_t)ct * stride + t] = t == n ? ks_input<DESC>(in, desc, ct, 2048) : 0ull;
     __syncthreads();
     // 640 chunks of 16 digits: (k-tile, lane group)
     for (int c = threadIdx.x; c < KS_K / 16; c += 256) {
@@ -98,10 +104,14 @@ __global__ __launch_bounds__(256) void k_ks_digits(const uint64_t* __restrict__ 
 // CW + 2 DMAs per k-tile in flight.  Every wave takes part in the staging and the barriers; tiles
 // past the batch skip only the stores.  (Per-wave register loads of the planes: 8.1 ms per 32768
 // keyswitches, TA 98 % busy; this kernel at CW = 1: 4.6 ms.)
+// Small batches split the contraction over gridDim.z workgroups of kspan k-tiles each (a latency
+// level's few hundred keyswitches are 2 x 53 workgroups otherwise, each 160 k-tiles deep): every
+// split subtracts its partial sum from the row k_ks_digits initialised, with 64-bit atomic adds --
+// exact, as the sum is taken mod 2^64 in any order.
 template <int CW>
 __global__ __launch_bounds__(256) void k_ks_mfma(const int8_t* __restrict__ digits, const uint64_t* __restrict__ body,
                                                  const int8_t* __restrict__ planes, int tiles, int count, int n,
-                                                 uint64_t* __restrict__ small, int stride) {
+                                                 uint64_t* __restrict__ small, int stride, int kspan) {
     constexpr int D = 3;  // staging depth (k-tiles)
     __shared__ __attribute__((aligned(16))) int8_t sb[D][8][1024];
     __shared__ __attribute__((aligned(16))) int8_t sa[D][4 * CW][1024];
@@ -121,21 +131,22 @@ __global__ __launch_bounds__(256) void k_ks_mfma(const int8_t* __restrict__ digi
             dma16_buf(rs, (uint32_t)(b * plane + frag_off(tt, kt, lane)), lds_off(&sb[kt % D][b][0]));
         }
     };
-    stage(0);
-    stage(1);
+    const int kt0 = blockIdx.z * kspan, kt1 = kt0 + kspan;  // kspan >= 2
+    stage(kt0);
+    stage(kt0 + 1);
     v4i acc[CW][8];
 #pragma unroll
     for (int c = 0; c < CW; ++c)
 #pragma unroll
         for (int b = 0; b < 8; ++b) acc[c][b] = v4i{0, 0, 0, 0};
-    for (int kt = 0; kt < KS_KT; ++kt) {
+    for (int kt = kt0; kt < kt1; ++kt) {
         // this wave's DMAs of k-tile kt have landed (in flight after them: k-tile kt + 1's)
-        if (kt + 1 < KS_KT)
+        if (kt + 1 < kt1)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CW + 2) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // every wave's fragments of kt visible; every read of k-tile kt - 1 done
-        if (kt + 2 < KS_KT) stage(kt + 2);  // into the buffers k-tile kt - 1 used
+        if (kt + 2 < kt1) stage(kt + 2);  // into the buffers k-tile kt - 1 used
         v4i a[CW];
 #pragma unroll
         for (int c = 0; c < CW; ++c) a[c] = reinterpret_cast<const v4i*>(&sa[kt % D][CW * w + c][0])[lane];
@@ -158,7 +169,11 @@ __global__ __launch_bounds__(256) void k_ks_mfma(const int8_t* __restrict__ digi
             uint64_t v = 0;
 #pragma unroll
             for (int b = 0; b < 8; ++b) v += (uint64_t)(int64_t)acc[c][b][r] << (8 * b);
-            small[(size_t)ct * stride + t] = (t == n ? body[ct] : 0ull) - v;
+            uint64_t* o = small + (size_t)ct * stride + t;
+            if (gridDim.z == 1)
+                *o = (t == n ? body[ct] : 0ull) - v;
+            else
+                atomicAdd(reinterpret_cast<unsigned long long*>(o), (unsigned long long)(0ull - v));
         }
 }
 
@@ -167,6 +182,10 @@ size_t ks_planes_bytes(int n) { return (size_t)8 * ks_plane_tiles(n) * KS_KT * 1
 #ifndef KS_CW
 #define KS_CW 2  // ciphertext tiles per wave
 #endif
+#ifndef KS_MAX_SPLITS
+#define KS_MAX_SPLITS 16  // contraction splits for small batches (KS_KT / 16 = 10 k-tiles each)
+#endif
+static_assert(KS_KT % KS_MAX_SPLITS == 0 && KS_KT / KS_MAX_SPLITS >= 2, "split k-tile spans");
 size_t ks_digits_bytes(int count) { return (size_t)((count + 127) / 128) * 8 * KS_KT * 1024; }
 
 hipError_t launch_ksk_to_planes(const uint64_t* ksk, int n, int8_t* planes, hipStream_t s) {
@@ -178,13 +197,18 @@ hipError_t launch_ksk_to_planes(const uint64_t* ksk, int n, int8_t* planes, hipS
 hipError_t launch_keyswitch_mfma(const uint64_t* in, const PbsDesc* desc, int count, const int8_t* planes,
                                  int8_t* digits, uint64_t* body, uint64_t* small, int stride, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
+    const int tiles = ks_plane_tiles(n), xb = (count + 64 * KS_CW - 1) / (64 * KS_CW);
+    // contraction splits: the fewest (of 1, 2, 4, 8, 16; 160 k-tiles) that give >= 768 workgroups
+    // (3 per CU)
+    int splits = 1;
+    while (splits < KS_MAX_SPLITS && (long)xb * tiles * splits < 768) splits *= 2;
+    uint64_t* init = splits > 1 ? small : nullptr;
     if (desc)
-        hipLaunchKernelGGL(k_ks_digits<true>, dim3(count), dim3(256), 0, s, nullptr, desc, digits, body);
+        hipLaunchKernelGGL(k_ks_digits<true>, dim3(count), dim3(256), 0, s, nullptr, desc, digits, body, init, stride, n);
     else
-        hipLaunchKernelGGL(k_ks_digits<false>, dim3(count), dim3(256), 0, s, in, nullptr, digits, body);
-    const int tiles = ks_plane_tiles(n);
-    hipLaunchKernelGGL(k_ks_mfma<KS_CW>, dim3((count + 64 * KS_CW - 1) / (64 * KS_CW), tiles), dim3(256), 0, s, digits,
-                       body, planes, tiles, count, n, small, stride);
+        hipLaunchKernelGGL(k_ks_digits<false>, dim3(count), dim3(256), 0, s, in, nullptr, digits, body, init, stride, n);
+    hipLaunchKernelGGL(k_ks_mfma<KS_CW>, dim3(xb, tiles, splits), dim3(256), 0, s, digits, body, planes, tiles, count,
+                       n, small, stride, KS_KT / splits);
     return hipGetLastError();
 }
 
