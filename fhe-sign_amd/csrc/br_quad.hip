@@ -44,6 +44,10 @@
 #ifndef QCL_SPLIT
 #define QCL_SPLIT 1
 #endif
+// BSK slices and untwist factors through buffer resources (bptr: per-iteration bases in SGPRs)
+#ifndef QBUF
+#define QBUF 1
+#endif
 // G = 1: rotation reads with the region base as an immediate offset (one VALU op less per read)
 #ifndef QROT_IMM
 #define QROT_IMM 1
@@ -272,6 +276,9 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
+#if QBUF
+    const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
+#endif
     for (int i = 0; i < n / G; ++i) {
         uint32_t a = 0, mB[3] = {0u, 0u, 0u};
         if constexpr (G == 1) {
@@ -289,14 +296,20 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             // no skip of m0 = m1 = 0 (the table chain needs every group's barriers): K = 0 exactly,
             // acc comes back unchanged up to the sign of a zero, as in the oracle's skip
         }
-        const cplx* Pg = ps;
-        asm volatile("" : "+s"(Pg));
-        const gcptr P = as_global(Pg) + t;
         // BSK rows for this wave's own digit (row p) and the other polynomial's digit (row 1 - p)
         // (G = 2: pattern B = 1 of the group; patterns 2, 3 follow at +4 and +8 polynomials)
         const size_t g0 = G == 1 ? (size_t)i : (size_t)3 * i;
+#if QBUF
+        const bptr P{ps_rs, 16u * (uint32_t)t, 0u};
+        const bptr bm{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((g0 * 2 + p) * 2 + p) * 16 + 8 * h) * 1024u};
+        const bptr bo{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((g0 * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 1024u};
+#else
+        const cplx* Pg = ps;
+        asm volatile("" : "+s"(Pg));
+        const gcptr P = as_global(Pg) + t;
         const gcptr bm = as_global(bsk) + ((size_t)((g0 * 2 + p) * 2 + p) * 16 + 8 * h) * 64 + L;
         const gcptr bo = as_global(bsk) + ((size_t)((g0 * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 64 + L;
+#endif
 
         cplx x[8];
         if constexpr (G == 1) {

@@ -210,6 +210,22 @@ struct gcptr {
 };
 FHE_DEV gcptr as_global(const cplx* p) { return gcptr{(const __attribute__((address_space(1))) dvec2*)p}; }
 
+// A table read through a buffer resource: the wave-uniform part of the address in SGPRs (soff),
+// the lane part a loop-invariant VGPR (voff), so that a per-iteration base costs scalar adds only
+// (a 64-bit VGPR pointer costs two to three vector ops per base and per 4 KiB of offsets)
+struct bptr {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t voff, soff;
+    FHE_DEV cplx operator[](uint32_t i) const {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff + 16u * i, 0);
+        return make_double2(__longlong_as_double((long long)(((uint64_t)v[1] << 32) | v[0])),
+                            __longlong_as_double((long long)(((uint64_t)v[3] << 32) | v[2])));
+    }
+};
+FHE_DEV __amdgpu_buffer_rsrc_t table_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+
 // Wave-uniform table entry through the scalar cache (s_load_dwordx4): constant address space
 FHE_DEV cplx sload(const cplx* base, uint32_t uniform_idx) {
     const __attribute__((address_space(4))) dvec2* p = (const __attribute__((address_space(4))) dvec2*)base;
