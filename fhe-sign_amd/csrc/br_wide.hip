@@ -184,8 +184,9 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     __shared__ __attribute__((aligned(16))) cplx s_monf[G == 2 ? 2 * 3 * 64 : 1];
 
     const int ct = blockIdx.x;
-    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;  // w in an SGPR
     const int p = w >> 2, q = w & 3, t = threadIdx.x & 255;
+    const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk);  // key slices: per-step bases in SGPRs
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
 
     // loop-invariant per-thread twiddles and twist factors (held in registers)
@@ -266,8 +267,8 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 
         // BSK slice for this iteration (issued early; consumed after the forward FFT)
         {
-            const cplx* b0 = bsk + ((size_t)((i * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;        // own digit's row
-            const cplx* b1 = bsk + ((size_t)((i * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;  // other digit's row
+            const bptr b0{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((i * 2 + p) * 2 + p) * 16 + 4 * q) * 1024u};  // own digit's row
+            const bptr b1{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((i * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 1024u};  // other row
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 Kown[r] = b0[r * 64];
@@ -323,6 +324,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             for (int r = 0; r < 4; ++r) Kown[r] = Koth[r] = make_double2(0.0, 0.0);
 #pragma unroll
             for (int B = 0; B < 3; ++B) {
+                // (64-bit pointers here: the buffer form pushes one value of this kernel to scratch)
                 const gcptr b0 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;
                 const gcptr b1 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;
                 const cplx e = cmul(tb[B * 256], tf[B * 64]);  // zeta^((4 j0 + 1) m_B)
