@@ -279,9 +279,10 @@ __global__ __launch_bounds__(128 * PAIR_CTS, 2) void k_blind_rotate_pair(const u
         // ---- untwist, accumulate (point j = 64 r + L -> coefficients j, j + 1024)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const cplx y = cmul(x[r], pst[r]);
-            acc[r] = tor_red_s(acc[r] + y.x);
-            acc[r + 16] = tor_red_s(acc[r + 16] + y.y);
+            // untwist fused into the accumulation (oracle fho_fourier_add_to_poly: cmul_acc)
+            const cplx y = cmul_acc(make_double2(acc[r], acc[r + 16]), x[r], pst[r]);
+            acc[r] = tor_red_s(y.x);
+            acc[r + 16] = tor_red_s(y.y);
             rot[64 * r + L] = acc[r];  // the next step's rotation source (the A-side reads are done:
             rot[64 * (r + 16) + L] = acc[r + 16];  // their values were consumed above)
         }

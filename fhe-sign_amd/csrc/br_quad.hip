@@ -532,9 +532,10 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         // ---- untwist, accumulate (point j = 128 r + t -> coefficients j, j + 1024)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const cplx y = cmul(x[r], pst[r]);
-            acc[r] = tor_red_s(acc[r] + y.x);
-            acc[r + 8] = tor_red_s(acc[r + 8] + y.y);
+            // untwist fused into the accumulation (oracle fho_fourier_add_to_poly: cmul_acc)
+            const cplx y = cmul_acc(make_double2(acc[r], acc[r + 8]), x[r], pst[r]);
+            acc[r] = tor_red_s(y.x);
+            acc[r + 8] = tor_red_s(y.y);
         }
     }
 

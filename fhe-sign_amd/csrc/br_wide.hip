@@ -408,9 +408,10 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         // ---- untwist, accumulate (x[r] = idx 256 r + 4 L + q -> coefs idx, idx + 1024)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const cplx y = cmul(x[r], PS[r]);  // conj(psi) 2^-10, times the accumulator's 2^-41
-            acc[r] = tor_red_s(acc[r] + y.x);
-            acc[r + 4] = tor_red_s(acc[r + 4] + y.y);
+            // untwist fused into the accumulation (oracle fho_fourier_add_to_poly: cmul_acc)
+            const cplx y = cmul_acc(make_double2(acc[r], acc[r + 4]), x[r], PS[r]);
+            acc[r] = tor_red_s(y.x);
+            acc[r + 4] = tor_red_s(y.y);
         }
     }
 

@@ -304,10 +304,10 @@ void fho_fourier_add_to_poly(double* f, double* acc) {
     const double inv = 0.0009765625; /* 2^-10, exact */
     for (int j = 0; j < 1024; ++j) {
         double ur = g_psi[2 * j] * inv, ui = -g_psi[2 * j + 1] * inv; /* exact scalings */
-        double yr, yi;
-        cmul(f[2 * j], f[2 * j + 1], ur, ui, &yr, &yi);
-        acc[j] = fho_tor_red(acc[j] + yr);
-        acc[j + 1024] = fho_tor_red(acc[j + 1024] + yi);
+        /* untwist product accumulated with two fmas per component (cmul_acc of device_math.h) */
+        const double fr = f[2 * j], fi = f[2 * j + 1];
+        acc[j] = fho_tor_red(fma(fr, ur, fma(-fi, ui, acc[j])));
+        acc[j + 1024] = fho_tor_red(fma(fr, ui, fma(fi, ur, acc[j + 1024])));
     }
 }
 
@@ -483,8 +483,9 @@ static void mac_own_first(const double* D0, const double* D1, const double* kr, 
 /* Blind rotation ACC = X^{-b} LUT, then n CMUX.  The accumulator's torus coefficients are kept as
  * f64 representatives in [-2^63, 2^63] instead of u64: X^a acc - acc is one f64 subtraction, its
  * gadget digit two rint's (fho_tor_digit, exact integers, no int->f64 conversion), and the external
- * product is added without rounding to an integer first (acc = tor_red(acc + y)).  The extra error
- * is the rounding of acc + y at the magnitude of y (~2^90 typical, <= 2^97), i.e. the same order as
+ * product is added without rounding to an integer first (acc = tor_red(acc + y), the untwist
+ * product fused in: fho_fourier_add_to_poly).  The extra error is the rounding of acc + y at the
+ * magnitude of y (~2^90 typical, <= 2^97), i.e. the same order as
  * the f64 transform's own error -- 2^-25 of the torus per CMUX against a blind-rotation noise of
  * ~2^-15 (bootstrapping-key noise x digits); decryption is unaffected.  The GLWE is returned as u64
  * (fho_f64_to_torus, round half even) for sample extraction. */
