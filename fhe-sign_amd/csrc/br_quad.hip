@@ -134,17 +134,9 @@ FHE_DEV double dpp_swap1(double v) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 // partner + sgn * x with sgn = +1 (L0 = 0) or -1 (L0 = 1): one exact-product fma, identical to the
-// add of +-x.  sgn is rebuilt from the lane id at each use (volatile: not hoisted and kept live
-// across the CMUX loop, where the kernel has no register left for it).
-FHE_DEV double q_sgn9() {
-    uint32_t lane;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    const uint32_t hi = 0x3FF00000u | (lane << 31);
-    return __longlong_as_double((long long)((uint64_t)hi << 32));
-}
+// add of +-x (sgn built once per kernel and held in a register).
 // The accumulator is kept in units of 2^41 (device_math.h: tor_red_s, tor_digit_s).
-FHE_DEV void q_stage9(cplx (&x)[8]) {
-    const double sgn = q_sgn9();
+FHE_DEV void q_stage9(cplx (&x)[8], double sgn) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         const cplx p = make_double2(dpp_swap1(x[r].x), dpp_swap1(x[r].y));
@@ -279,6 +271,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
 #if QBUF
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
 #endif
+    const double sgn9 = __longlong_as_double((long long)((uint64_t)(0x3FF00000u | ((uint32_t)L << 31)) << 32));  // +-1 by L0
     for (int i = 0; i < n / G; ++i) {
         uint32_t a = 0, mB[3] = {0u, 0u, 0u};
         if constexpr (G == 1) {
@@ -427,7 +420,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             x[2 * r2] = cmul(x[2 * r2], s_z[ia]);
             x[2 * r2 + 1] = cmul(x[2 * r2 + 1], mul_i(s_z[ib]));
         }
-        q_stage9(x);
+        q_stage9(x, sgn9);
 
         // ---- swap Fourier digits with the other polynomial's wave of the same half, MAC with BSK
         wave_sync();
@@ -504,7 +497,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
 
         // ---- inverse FFT: stage 9 and phase C in registers, then the region again
-        q_stage9(x);
+        q_stage9(x, sgn9);
         q_dit<0>(x, s_w, tpos(256 * (L & 1)));
         q_dit<1>(x, s_w, tpos(128 * (L & 1)));
         q_dit<2>(x, s_w, tpos(64 * (L & 1)));
