@@ -134,7 +134,14 @@ FHE_DEV double dpp_swap1(double v) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 // partner + sgn * x with sgn = +1 (L0 = 0) or -1 (L0 = 1): one exact-product fma, identical to the
-// add of +-x (sgn built once per kernel and held in a register).
+// add of +-x.  The classic kernel builds sgn once and holds it; the multi-bit kernel rebuilds it from
+// the lane id at each use (volatile: not hoisted -- held across its loop it cost 13 % per batch).
+FHE_DEV double q_sgn9() {
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const uint32_t hi = 0x3FF00000u | (lane << 31);
+    return __longlong_as_double((long long)((uint64_t)hi << 32));
+}
 // The accumulator is kept in units of 2^41 (device_math.h: tor_red_s, tor_digit_s).
 FHE_DEV void q_stage9(cplx (&x)[8], double sgn) {
 #pragma unroll
@@ -420,7 +427,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             x[2 * r2] = cmul(x[2 * r2], s_z[ia]);
             x[2 * r2 + 1] = cmul(x[2 * r2 + 1], mul_i(s_z[ib]));
         }
-        q_stage9(x, sgn9);
+        q_stage9(x, G == 1 ? sgn9 : q_sgn9());
 
         // ---- swap Fourier digits with the other polynomial's wave of the same half, MAC with BSK
         wave_sync();
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
 
         // ---- inverse FFT: stage 9 and phase C in registers, then the region again
-        q_stage9(x, sgn9);
+        q_stage9(x, G == 1 ? sgn9 : q_sgn9());
         q_dit<0>(x, s_w, tpos(256 * (L & 1)));
         q_dit<1>(x, s_w, tpos(128 * (L & 1)));
         q_dit<2>(x, s_w, tpos(64 * (L & 1)));
