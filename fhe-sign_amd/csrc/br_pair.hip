@@ -91,11 +91,16 @@ __global__ __launch_bounds__(128 * PAIR_CTS, 2) void k_blind_rotate_pair(const u
     uint32_t a_next = modswitch_2n(a_ct[0]);
 #pragma unroll
     for (int r = 0; r < 32; ++r) rot[64 * r + L] = acc[r];
+    uint32_t upd = 0;
     for (int i = 0; i < n; ++i) {
         // a = 0 is not skipped: the two ciphertexts of a workgroup share its barriers.  The CMUX
         // then adds an exact zero (acc unchanged up to the sign of a zero, as the oracle's skip).
         const uint32_t a = a_next;
         a_next = modswitch_2n(a_ct[i + 1]);  // i + 1 = n reads the body: in bounds, unused
+        // acc + y reduced mod 2^64 on every second performed update (oracle; a = 0 steps run here
+        // with y = 0 but are no update there: never reduced, not counted)
+        const bool reduce = a != 0 && (upd & 1u) != 0;
+        upd += a != 0 ? 1u : 0u;
         const gcptr bm = as_global(bsk) + (size_t)((i * 2 + p) * 2 + p) * 1024 + L;
         const gcptr bo = as_global(bsk) + (size_t)((i * 2 + (p ^ 1)) * 2 + p) * 1024 + L;
 
@@ -281,11 +286,16 @@ __global__ __launch_bounds__(128 * PAIR_CTS, 2) void k_blind_rotate_pair(const u
         for (int r = 0; r < 16; ++r) {
             // untwist fused into the accumulation (oracle fho_fourier_add_to_poly: cmul_acc)
             const cplx y = cmul_acc(make_double2(acc[r], acc[r + 16]), x[r], pst[r]);
-            acc[r] = tor_red_s(y.x);
-            acc[r + 16] = tor_red_s(y.y);
-            rot[64 * r + L] = acc[r];  // the next step's rotation source (the A-side reads are done:
-            rot[64 * (r + 16) + L] = acc[r + 16];  // their values were consumed above)
+            acc[r] = y.x;
+            acc[r + 16] = y.y;
         }
+        if (reduce) {  // wave-uniform: a scalar branch
+#pragma unroll
+            for (int r = 0; r < 32; ++r) acc[r] = tor_red_s(acc[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < 32; ++r) rot[64 * r + L] = acc[r];  // the next step's rotation source (the
+        // A-side reads are done: their values were consumed above)
     }
 
     // ---- sample extract (coefficient 0)

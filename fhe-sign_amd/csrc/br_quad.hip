@@ -279,13 +279,16 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
 #endif
     const double sgn9 = __longlong_as_double((long long)((uint64_t)(0x3FF00000u | ((uint32_t)L << 31)) << 32));  // +-1 by L0
+    uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
     for (int i = 0; i < n / G; ++i) {
         uint32_t a = 0, mB[3] = {0u, 0u, 0u};
         if constexpr (G == 1) {
             a = a_next;
             a_next = modswitch_2n(a_ct[i + 1]);
             if (a == 0) continue;  // X^0 - 1 = 0 (uniform over the workgroup)
-        } else {
+        }
+        const bool reduce = (upd++ & 1u) != 0;
+        if constexpr (G == 2) {
             mB[0] = a_next;
             mB[1] = a_next1;
             mB[2] = (a_next + a_next1) & 4095u;
@@ -534,8 +537,12 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         for (int r = 0; r < 8; ++r) {
             // untwist fused into the accumulation (oracle fho_fourier_add_to_poly: cmul_acc)
             const cplx y = cmul_acc(make_double2(acc[r], acc[r + 8]), x[r], pst[r]);
-            acc[r] = tor_red_s(y.x);
-            acc[r + 8] = tor_red_s(y.y);
+            acc[r] = y.x;
+            acc[r + 8] = y.y;
+        }
+        if (reduce) {  // wave-uniform: a scalar branch
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = tor_red_s(acc[r]);
         }
     }
 

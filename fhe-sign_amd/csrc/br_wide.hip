@@ -256,14 +256,17 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
+    uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
     for (int i = 0; i < n / G; ++i) {
         cplx x[4];
         cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
         uint32_t mB[3] = {0u, 0u, 0u};
+        bool reduce;
         if constexpr (G == 1) {
         const uint32_t a = a_next;
         a_next = modswitch_2n(a_ct[i + 1]);
         if (a == 0) continue;
+        reduce = (upd++ & 1u) != 0;
 
         // BSK slice for this iteration (issued early; consumed after the forward FFT)
         {
@@ -303,6 +306,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             x[r] = make_double2(tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]),
                                 tor_digit_s(neg_bit11(rv[r + 4], uu[r + 4]) - acc[r + 4]));
         } else {
+        reduce = (upd++ & 1u) != 0;
         mB[0] = a_next;
         mB[1] = a_next1;
         mB[2] = (a_next + a_next1) & 4095u;
@@ -410,8 +414,12 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         for (int r = 0; r < 4; ++r) {
             // untwist fused into the accumulation (oracle fho_fourier_add_to_poly: cmul_acc)
             const cplx y = cmul_acc(make_double2(acc[r], acc[r + 4]), x[r], PS[r]);
-            acc[r] = tor_red_s(y.x);
-            acc[r + 4] = tor_red_s(y.y);
+            acc[r] = y.x;
+            acc[r + 4] = y.y;
+        }
+        if (reduce) {  // wave-uniform: a scalar branch
+#pragma unroll
+            for (int r = 0; r < 8; ++r) acc[r] = tor_red_s(acc[r]);
         }
     }
 

@@ -108,6 +108,8 @@ const double* fho_zetas(void);
 void fho_dpoly_to_fourier(const double* poly, double* out);
 /* Fourier (bit-reversed) -> torus polynomial ADDED into an f64 accumulator: acc = red(acc + y) */
 void fho_fourier_add_to_poly(double* f /* clobbered */, double* acc);
+/* the same with the mod-2^64 reduction of the sum optional (reduce = 0: acc + y as is) */
+void fho_fourier_add_to_poly_r(double* f /* clobbered */, double* acc, int reduce);
 /* f64 torus representatives: v mod 2^64 into [-2^63, 2^63]; one-level gadget digit */
 double fho_tor_red(double v);
 double fho_tor_digit(double v, uint32_t base_log);
