@@ -289,9 +289,11 @@ __global__ __launch_bounds__(128 * PAIR_CTS, 2) void k_blind_rotate_pair(const u
             acc[r] = y.x;
             acc[r + 16] = y.y;
         }
-        if (reduce) {  // wave-uniform: a scalar branch
+        {  // branch-free (a branch here cost spills and drained loads in flight): tor_red_s with the
+           // scale 2^-23 or 0, the latter leaving acc exactly as it is
+            const double sc = reduce ? 0x1p-23 : 0.0;
 #pragma unroll
-            for (int r = 0; r < 32; ++r) acc[r] = tor_red_s(acc[r]);
+            for (int r = 0; r < 32; ++r) acc[r] = __fma_rn(-0x1p23, __builtin_rint(acc[r] * sc), acc[r]);
         }
 #pragma unroll
         for (int r = 0; r < 32; ++r) rot[64 * r + L] = acc[r];  // the next step's rotation source (the
