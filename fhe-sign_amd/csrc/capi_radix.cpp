@@ -370,10 +370,58 @@ int fhe_schedule_levels(const int32_t* off, const int32_t* deps, size_t n, int m
     });
 }
 
+int fhe_ctx_level_log(fhe_ctx* c, uint32_t* sizes, size_t cap, size_t* n, int reset) {
+    if (!c || !n || (cap && !sizes)) return FHE_ERR_INVALID;
+    if (!c->engine) {
+        *n = 0;
+        return FHE_OK;
+    }
+    const std::vector<uint32_t>& log = c->engine->level_log;
+    *n = log.size();
+    std::memcpy(sizes, log.data(), std::min(cap, log.size()) * 4);
+    if (reset) c->engine->level_log.clear();
+    return FHE_OK;
+}
+
 int fhe_ctx_stats(fhe_ctx* c, uint64_t* pbs, uint64_t* levels) {
     if (!c) return FHE_ERR_INVALID;
     if (pbs) *pbs = c->engine ? c->engine->pbs_count : 0;
     if (levels) *levels = c->engine ? c->engine->levels : 0;
+    return FHE_OK;
+}
+
+// ----------------------------------------------------------------- operand distribution (comm.cpp)
+int fhe_ctx_broadcast_radix(fhe_ctx* c, fhe_radix** x, int root) {
+    const bool sends = c && (!c->comm || c->rank == root);
+    if (!c || !x || (sends && !*x)) return FHE_ERR_INVALID;
+    std::vector<Radix> g;
+    if (sends) g.push_back((*x)->r);
+    const int rc = bcast_radix_groups(c, root, &g);
+    if (rc || (c->comm && c->rank == root)) return rc;  // the root keeps its handle
+    if (g.size() != 1) {
+        set_error("broadcast_radix: the root sent a BigUintFHE, not one radix integer");
+        return FHE_ERR_INVALID;
+    }
+    const uint32_t bits = 2 * g[0].nblocks();
+    *x = wrap(std::move(g[0]), bits);
+    return FHE_OK;
+}
+
+int fhe_ctx_broadcast_biguint(fhe_ctx* c, fhe_biguint** x, int root) {
+    const bool sends = c && (!c->comm || c->rank == root);
+    if (!c || !x || (sends && !*x)) return FHE_ERR_INVALID;
+    std::vector<Radix> g;
+    if (sends) g = (*x)->v.digits;
+    const int rc = bcast_radix_groups(c, root, &g);
+    if (rc || (c->comm && c->rank == root)) return rc;
+    for (const Radix& d : g)
+        if (d.nblocks() != kLimbBlocks) {
+            set_error("broadcast_biguint: the root sent digits that are not FheUint32");
+            return FHE_ERR_INVALID;
+        }
+    auto* b = new fhe_biguint();
+    b->v.digits = std::move(g);
+    *x = b;
     return FHE_OK;
 }
 

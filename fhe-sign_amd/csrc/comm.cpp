@@ -43,6 +43,84 @@ int nccl_settle(ncclComm_t comm, ncclResult_t r, const char* what, uint32_t time
     }
     return nccl_check(r, what);
 }
+
+// Bounded wait for the context stream while collectives are queued on it: polls the stream and the
+// communicator's async error against the deadline; on a timeout or a communicator error the
+// communicator is aborted and detached (a peer that died after the enqueue cannot hang this rank).
+int comm_wait_impl(fhe_ctx* c, const char* what) {
+    ncclComm_t cm = (ncclComm_t)c->comm;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) return FHE_OK;
+        if (q != hipErrorNotReady) {
+            set_error(std::string(what) + ": " + hipGetErrorString(q));
+            return FHE_ERR_HIP;
+        }
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(cm, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
+            (void)ncclCommAbort(cm);
+            c->comm = nullptr;
+            c->nranks = 1;
+            c->rank = 0;
+            set_error(std::string(what) + ": " + ncclGetErrorString(st) + " (communicator aborted)");
+            return FHE_ERR_HIP;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->comm_timeout_ms)) {
+            (void)ncclCommAbort(cm);
+            c->comm = nullptr;
+            c->nranks = 1;
+            c->rank = 0;
+            set_error(std::string(what) + ": collective did not complete within " + std::to_string(c->comm_timeout_ms) +
+                      " ms (communicator aborted)");
+            return FHE_ERR_TIMEOUT;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
+// broadcast `bytes` of host memory from root (in place on every rank), through a device bounce buffer
+int bcast_host(fhe_ctx* c, void* host, size_t bytes, int root) {
+    void* d = nullptr;
+    FHE_HIP_CHECK(hipMalloc(&d, bytes));
+    ncclComm_t cm = (ncclComm_t)c->comm;
+    int rc = hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc)
+        rc = nccl_settle(cm, ncclBroadcast(d, d, bytes, ncclUint8, root, cm, c->stream), "ncclBroadcast",
+                         c->comm_timeout_ms, false);
+    if (!rc) rc = hipMemcpyAsync(host, d, bytes, hipMemcpyDeviceToHost, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = comm_wait_impl(c, "ncclBroadcast");
+    if (c->comm) (void)hipStreamSynchronize(c->stream);  // (after an abort the stream may not drain)
+    (void)hipFree(d);
+    return rc;
+}
+
+// every rank contributes ok (0/1); *all = min over the ranks (one-word all-reduce)
+int agree(fhe_ctx* c, int ok, int* all) {
+    int32_t v = ok ? 1 : 0;
+    int32_t* d = nullptr;
+    FHE_HIP_CHECK(hipMalloc(&d, sizeof v));
+    ncclComm_t cm = (ncclComm_t)c->comm;
+    int rc = hipMemcpyAsync(d, &v, sizeof v, hipMemcpyHostToDevice, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc)
+        rc = nccl_settle(cm, ncclAllReduce(d, d, 1, ncclInt32, ncclMin, cm, c->stream), "ncclAllReduce",
+                         c->comm_timeout_ms, false);
+    if (!rc) rc = hipMemcpyAsync(&v, d, sizeof v, hipMemcpyDeviceToHost, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = comm_wait_impl(c, "ncclAllReduce");
+    if (c->comm) (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    *all = v;
+    return rc;
+}
+}  // namespace
+
+int fhe_ctx::wait_stream(const char* what) {
+    if (!comm) return hipStreamSynchronize(stream) == hipSuccess ? FHE_OK : (set_error(std::string(what) + ": stream sync failed"), FHE_ERR_HIP);
+    return comm_wait_impl(this, what);
+}
+
+namespace {
+int comm_wait(fhe_ctx* c, const char* what) { return comm_wait_impl(c, what); }
 }  // namespace
 
 int fhe_ctx::ensure_gather(size_t n) {
@@ -71,6 +149,197 @@ void fhe_ctx::release_comm() {
     nranks = 1;
     rank = 0;
 }
+
+namespace fhe {
+
+// Operand distribution for the fan-out (config 5a): every rank must run the radix program on
+// byte-identical inputs, e.g. the private key d' that reaches sign_fhe_with_k0 as an argument
+// (/root/reference/src/schnorr.rs:235,270-277) only on the rank that received it.
+//   1. header from the root: ok flag, group count, block count, slot-block count, message/carry
+//      modulus (receivers check them against their installed key);
+//   2. every rank allocates its buffers; one all-reduce (min) agrees that all succeeded;
+//   3. metadata (group sizes; per block: kind, trivial value, degree, noise) and the slot blocks'
+//      ciphertexts (gathered into one contiguous device buffer on the root) are broadcast;
+//   4. bounded wait; the receivers validate the metadata and scatter the ciphertexts into slots.
+namespace {
+constexpr uint32_t kBcastMagic = 0x46524243u;  // "FRBC"
+struct BcastHdr {
+    uint32_t magic, ok, ngroups, nblocks, nslot, msg, carry, pad;
+};
+
+// root side: header, metadata (group sizes; per block kind, trivial value, degree, noise) and the
+// slot blocks in gather order
+void bcast_encode(fhe_ctx* c, const std::vector<Radix>& groups, BcastHdr* h, std::vector<uint32_t>* meta,
+                  std::vector<const Block*>* slot_blocks, std::string* why) {
+    *h = BcastHdr{};
+    h->magic = kBcastMagic;
+    h->ok = 1;
+    h->ngroups = (uint32_t)groups.size();
+    h->msg = c->p.message_modulus;
+    h->carry = c->p.carry_modulus;
+    meta->assign(groups.size(), 0);
+    for (size_t g = 0; g < groups.size(); ++g) {
+        (*meta)[g] = groups[g].nblocks();
+        for (const Block& b : groups[g].blocks) {
+            ++h->nblocks;
+            if (b.lazy()) {
+                h->ok = 0;
+                *why = "broadcast of a lazy (un-bootstrapped) block";
+            } else if (!b.trivial()) {
+                slot_blocks->push_back(&b);
+            }
+            meta->push_back(b.trivial() ? 0u : 1u);
+            meta->push_back(b.value);
+            meta->push_back(b.degree);
+            meta->push_back(b.noise);
+        }
+    }
+    h->nslot = (uint32_t)slot_blocks->size();
+}
+
+// receiver side: validate the metadata against this context and build the groups from the
+// ciphertexts in d_data (scattered into fresh slots)
+int bcast_decode(fhe_ctx* c, const BcastHdr& h, const std::vector<uint32_t>& meta, const uint64_t* d_data,
+                 std::vector<Radix>* groups) {
+    size_t total = 0, nslot = 0;
+    for (uint32_t g = 0; g < h.ngroups; ++g) total += meta[g];
+    bool valid = total == h.nblocks && meta.size() == h.ngroups + 4 * (size_t)h.nblocks;
+    const uint32_t mc = c->p.msg_carry();
+    for (size_t k = 0; valid && k < h.nblocks; ++k) {
+        const uint32_t* m = &meta[h.ngroups + 4 * k];
+        valid = m[0] <= 1 && m[2] < mc && (m[0] ? m[3] >= 1 && m[3] <= kMaxNoise : m[1] <= m[2]);
+        nslot += m[0];
+    }
+    if (!valid || nslot != h.nslot) {
+        set_error("broadcast: invalid block metadata from the root");
+        return FHE_ERR_INVALID;
+    }
+    try {
+        Blocks slots = c->engine->adopt_device(d_data, nslot);
+        std::vector<Radix> out(h.ngroups);
+        size_t k = 0, s = 0;
+        for (uint32_t g = 0; g < h.ngroups; ++g)
+            for (uint32_t j = 0; j < meta[g]; ++j, ++k) {
+                const uint32_t* m = &meta[h.ngroups + 4 * k];
+                Block b;
+                if (m[0]) {
+                    b = slots[s++];
+                    b.degree = m[2];
+                    b.noise = m[3];
+                } else {
+                    b = Block::make_trivial(m[1]);
+                    b.degree = m[2];
+                }
+                out[g].blocks.push_back(std::move(b));
+            }
+        *groups = std::move(out);
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return FHE_ERR_HIP;
+    }
+    return FHE_OK;
+}
+}  // namespace
+
+int bcast_radix_groups(fhe_ctx* c, int root, std::vector<Radix>* groups) {
+    if (!c || !groups || root < 0 || root >= c->fanout_world()) {
+        set_error("broadcast needs a valid root rank");
+        return FHE_ERR_INVALID;
+    }
+    if (!c->has_key || !c->engine) {
+        set_error("broadcast of ciphertexts needs an installed server key on every rank");
+        return FHE_ERR_NO_KEY;  // local misuse, caught before any collective (all ranks must pass it)
+    }
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    const bool loopback = !c->comm;  // emulated ranks (test hook): the root's data through the receiver path
+    const bool is_root = loopback || c->rank == root;
+    BcastHdr h{};
+    std::vector<uint32_t> meta;
+    std::vector<const Block*> slot_blocks;
+    std::string local_why;
+    if (is_root) {
+        bcast_encode(c, *groups, &h, &meta, &slot_blocks, &local_why);
+        try {
+            c->engine->flush();
+        } catch (const std::exception& e) {
+            h.ok = 0;
+            local_why = e.what();
+        }
+    }
+    int rc = loopback ? FHE_OK : bcast_host(c, &h, sizeof h, root);
+    if (rc) return rc;
+    if (h.magic != kBcastMagic || !h.ok) {
+        set_error(is_root ? local_why : std::string("broadcast: the root rank failed"));
+        return FHE_ERR_INVALID;
+    }
+    int local_ok = 1;
+    if (!is_root && (h.msg != c->p.message_modulus || h.carry != c->p.carry_modulus || h.nblocks > (1u << 24) ||
+                     h.nslot > h.nblocks || h.ngroups > h.nblocks + 1)) {
+        local_ok = 0;
+        local_why = "broadcast: the root's ciphertexts do not fit this rank's parameters";
+    }
+    const size_t meta_words = (size_t)h.ngroups + 4 * (size_t)h.nblocks;
+    const size_t data_words = (size_t)h.nslot * kBigCt;
+    uint32_t* d_meta = nullptr;
+    uint64_t* d_data = nullptr;
+    if (local_ok) {
+        hipError_t he = hipMalloc(&d_meta, std::max<size_t>(meta_words, 1) * 4);
+        if (he == hipSuccess) he = hipMalloc(&d_data, std::max<size_t>(data_words, 1) * 8);
+        if (he != hipSuccess) {
+            local_ok = 0;
+            local_why = std::string("broadcast: ") + hipGetErrorString(he);
+        }
+    }
+    auto release = [&] {
+        (void)hipStreamSynchronize(c->stream);
+        if (d_meta) (void)hipFree(d_meta);
+        if (d_data) (void)hipFree(d_data);
+    };
+    if (is_root && local_ok) {
+        try {
+            c->engine->gather_device(slot_blocks, d_data);
+        } catch (const std::exception& e) {
+            local_ok = 0;
+            local_why = e.what();
+        }
+        if (local_ok && hipMemcpyAsync(d_meta, meta.data(), meta_words * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+            local_ok = 0;
+            local_why = "broadcast: metadata upload failed";
+        }
+    }
+    int all_ok = local_ok;
+    rc = loopback ? FHE_OK : agree(c, local_ok, &all_ok);
+    if (rc || !all_ok) {
+        release();
+        if (rc) return rc;
+        set_error(local_ok ? std::string("broadcast: another rank failed") : local_why);
+        return local_ok ? FHE_ERR_INVALID : FHE_ERR_ALLOC;
+    }
+    if (loopback) {
+        rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+        if (!rc) rc = bcast_decode(c, h, meta, d_data, groups);
+        release();
+        return rc;
+    }
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    rc = nccl_settle(comm, ncclBroadcast(d_meta, d_meta, meta_words, ncclUint32, root, comm, c->stream),
+                     "ncclBroadcast", c->comm_timeout_ms, false);
+    if (!rc && data_words)
+        rc = nccl_settle(comm, ncclBroadcast(d_data, d_data, data_words, ncclUint64, root, comm, c->stream),
+                         "ncclBroadcast", c->comm_timeout_ms, false);
+    if (!rc && !is_root) {
+        meta.resize(meta_words);
+        rc = hipMemcpyAsync(meta.data(), d_meta, meta_words * 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess
+                 ? FHE_OK
+                 : FHE_ERR_HIP;
+    }
+    if (!rc) rc = comm_wait(c, "broadcast");
+    if (!rc && !is_root) rc = bcast_decode(c, h, meta, d_data, groups);
+    release();
+    return rc;
+}
+
+}  // namespace fhe
 
 extern "C" {
 
@@ -127,89 +396,104 @@ int fhe_ctx_detach_comm(fhe_ctx* c) {
 // standard-layout KSK and Fourier BSK (123 MB at the default parameters); every other rank
 // derives the kernels' layouts (KSK byte planes, quad BSK) with its own conversion kernels, exactly
 // as fhe_set_server_key would.  Collective: every rank of the communicator calls it.
+//
+// Failure handling (every rank takes the same branch, so no rank is left inside a collective its
+// peers skipped): the root's header carries an ok flag (root without a key -> everyone stops);
+// the receivers' buffer allocations are agreed with a one-word all-reduce (min) before any data
+// moves; the final wait is bounded (comm_wait: deadline, then ncclCommAbort).
 int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     if (!c || !c->comm || root < 0 || root >= c->nranks) {
         set_error("broadcast_server_key needs an attached communicator and a valid root");
         return FHE_ERR_INVALID;
     }
     FHE_HIP_CHECK(hipSetDevice(c->device));
-    ncclComm_t comm = (ncclComm_t)c->comm;
     const bool is_root = c->rank == root;
+    int local_ok = 1;
+    std::string local_why;
     if (is_root && !c->has_key) {
-        set_error("the root rank has no server key installed");
-        return FHE_ERR_NO_KEY;
+        local_ok = 0;
+        local_why = "the root rank has no server key installed";
     }
     if (c->engine) {
         try {
             c->engine->flush();  // pending work of the old key runs first
         } catch (const std::exception& e) {
-            set_error(e.what());
-            return FHE_ERR_HIP;
+            local_ok = 0;
+            local_why = e.what();
         }
     }
-    const uint32_t tmo = c->comm_timeout_ms;
-    // parameters (a few words; also tells the receivers the buffer sizes)
-    fhe_params hp = c->p.to_c();
-    fhe_params* dp = nullptr;
-    FHE_HIP_CHECK(hipMalloc(&dp, sizeof(fhe_params)));
-    int rc = hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
-    if (!rc)
-        rc = nccl_settle(comm, ncclBroadcast(dp, dp, sizeof(fhe_params), ncclUint8, root, comm, c->stream),
-                         "ncclBroadcast", tmo, false);
-    if (!rc) rc = hipMemcpyAsync(&hp, dp, sizeof hp, hipMemcpyDeviceToHost, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
-    if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
-    (void)hipFree(dp);
+    // header: the root's ok flag + parameters (a few words; also tells the receivers the sizes)
+    struct Hdr {
+        int32_t ok;
+        fhe_params p;
+    } h{};
+    h.ok = is_root ? local_ok : 1;
+    if (is_root && c->has_key) h.p = c->p.to_c();
+    int rc = bcast_host(c, &h, sizeof h, root);
     if (rc) return rc;
+    if (!h.ok) {
+        set_error(is_root ? local_why : std::string("broadcast_server_key: the root rank failed (no key installed)"));
+        return is_root && !c->has_key ? FHE_ERR_NO_KEY : FHE_ERR_INVALID;
+    }
     Params p;
     const char* why = nullptr;
-    if (!Params::from_c(hp, &p, &why)) {
-        set_error(why);
-        return FHE_ERR_UNSUPPORTED;
+    if (!Params::from_c(h.p, &p, &why)) {
+        local_ok = 0;
+        local_why = why ? why : "invalid parameters";
     }
     const size_t ksk_words = (size_t)kBigDim * p.ks_level * (p.n + 1);
     const int npoly = (int)(p.ggsw_count() * 4);
     const size_t bsk_doubles = (size_t)npoly * 1024 * 2;
-    if (is_root) {
-        rc = nccl_settle(comm, ncclBroadcast(c->d_ksk, c->d_ksk, ksk_words, ncclUint64, root, comm, c->stream),
-                         "ncclBroadcast", tmo, false);
-        if (!rc)
-            rc = nccl_settle(comm, ncclBroadcast(c->d_bsk, c->d_bsk, bsk_doubles, ncclFloat64, root, comm, c->stream),
-                             "ncclBroadcast", tmo, false);
-        if (rc) return rc;
-        FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
-        return FHE_OK;
-    }
     // Receivers: the new key lands in fresh buffers; the installed key (if any) stays in place and
     // usable until every collective and conversion has succeeded, then the two are swapped.
     uint64_t* n_ksk = nullptr;
     int8_t* n_planes = nullptr;
-    double2 *n_bsk = nullptr, *n_quad = nullptr, *n_pair = nullptr;
+    double2 *n_bsk = nullptr, *n_quad = nullptr;
     auto drop_new = [&] {
         (void)hipStreamSynchronize(c->stream);
         if (n_ksk) (void)hipFree(n_ksk);
         if (n_planes) (void)hipFree(n_planes);
         if (n_bsk) (void)hipFree(n_bsk);
         if (n_quad) (void)hipFree(n_quad);
-        if (n_pair) (void)hipFree(n_pair);
+        n_ksk = nullptr;
+        n_planes = nullptr;
+        n_bsk = n_quad = nullptr;
     };
-    hipError_t he = hipMalloc(&n_ksk, ksk_words * 8);
-    if (he == hipSuccess) he = hipMalloc(&n_planes, fhe::ks_planes_bytes((int)p.n));
-    if (he == hipSuccess) he = hipMalloc(&n_bsk, bsk_doubles * 8);
-    if (he == hipSuccess) he = hipMalloc(&n_quad, bsk_doubles * 8);
-    if (he == hipSuccess && p.grouping == 1) he = hipMalloc(&n_pair, bsk_doubles * 8);
-    if (he != hipSuccess) {
-        drop_new();
-        set_error(std::string("broadcast_server_key: ") + hipGetErrorString(he));
-        return FHE_ERR_ALLOC;
+    if (!is_root && local_ok) {
+        hipError_t he = hipMalloc(&n_ksk, ksk_words * 8);
+        if (he == hipSuccess) he = hipMalloc(&n_planes, fhe::ks_planes_bytes((int)p.n));
+        if (he == hipSuccess) he = hipMalloc(&n_bsk, bsk_doubles * 8);
+        if (he == hipSuccess) he = hipMalloc(&n_quad, bsk_doubles * 8);
+        if (he != hipSuccess) {
+            drop_new();
+            local_ok = 0;
+            local_why = std::string("broadcast_server_key: ") + hipGetErrorString(he);
+        }
     }
-    rc = nccl_settle(comm, ncclBroadcast(n_ksk, n_ksk, ksk_words, ncclUint64, root, comm, c->stream), "ncclBroadcast",
-                     tmo, false);
+    int all_ok = 0;
+    rc = agree(c, local_ok, &all_ok);
+    if (rc || !all_ok) {
+        drop_new();
+        if (rc) return rc;
+        set_error(local_ok ? std::string("broadcast_server_key: another rank could not take the key") : local_why);
+        return local_ok ? FHE_ERR_INVALID : FHE_ERR_ALLOC;
+    }
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    const uint32_t tmo = c->comm_timeout_ms;
+    uint64_t* ksk_buf = is_root ? c->d_ksk : n_ksk;
+    double2* bsk_buf = is_root ? c->d_bsk : n_bsk;
+    rc = nccl_settle(comm, ncclBroadcast(ksk_buf, ksk_buf, ksk_words, ncclUint64, root, comm, c->stream),
+                     "ncclBroadcast", tmo, false);
     if (!rc)
-        rc = nccl_settle(comm, ncclBroadcast(n_bsk, n_bsk, bsk_doubles, ncclFloat64, root, comm, c->stream),
+        rc = nccl_settle(comm, ncclBroadcast(bsk_buf, bsk_buf, bsk_doubles, ncclFloat64, root, comm, c->stream),
                          "ncclBroadcast", tmo, false);
-    if (!rc) rc = launch_ksk_to_planes(n_ksk, (int)p.n, n_planes, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = comm_wait(c, "broadcast_server_key");
+    if (rc || is_root) {
+        if (rc) drop_new();
+        return rc;
+    }
+    rc = launch_ksk_to_planes(n_ksk, (int)p.n, n_planes, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = launch_bsk_to_quad(n_bsk, npoly, n_quad, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
-    if (!rc && n_pair) rc = launch_bsk_to_pair(n_bsk, npoly, n_pair, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (rc) {
         drop_new();
@@ -224,13 +508,17 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
             return FHE_ERR_HIP;
         }
     }
-    // commit: swap in the new key, release the old one
+    // commit: swap in the new key, release the old one (the pair kernel's layout, if any, is
+    // re-derived on its next use)
     std::swap(c->d_ksk, n_ksk);
     std::swap(c->d_ksk_planes, n_planes);
     std::swap(c->d_bsk, n_bsk);
     std::swap(c->d_bsk_quad, n_quad);
-    std::swap(c->d_bsk_pair, n_pair);
     drop_new();  // frees the previous key's buffers (null when there was none)
+    if (c->d_bsk_pair) {
+        (void)hipFree(c->d_bsk_pair);
+        c->d_bsk_pair = nullptr;
+    }
     if (!(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
         c->lut_ids.clear();
         c->h_luts.clear();

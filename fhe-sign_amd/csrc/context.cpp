@@ -307,9 +307,19 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     if ((int)count <= wide_threshold)
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
-    if (br_kernel == FHE_BR_PAIR && p.grouping == 1 && d_bsk_pair)
+    if (br_kernel == FHE_BR_PAIR && p.grouping == 1) {
+        // the opt-in pair kernel's BSK layout is derived on first use (stream-ordered after the
+        // Fourier BSK), not at every key install
+        if (!d_bsk_pair) {
+            const int npoly = (int)(p.ggsw_count() * 4);
+            hipError_t e = hipMalloc(&d_bsk_pair, (size_t)npoly * 1024 * sizeof(double2));
+            if (e != hipSuccess) return e;
+            e = launch_bsk_to_pair(d_bsk, npoly, d_bsk_pair, stream);
+            if (e != hipSuccess) return e;
+        }
         return launch_blind_rotate_pair(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_pair, d_tab_pair, out,
                                         (int)count, (int)p.n, stream);
+    }
     return launch_blind_rotate_quad(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_quad, d_tw_quad, d_psi_quad,
                                     d_zeta_quad, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
 }
@@ -635,10 +645,6 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     FHE_HIP_CHECK(launch_bsk_to_fourier(d_std, npoly, c->d_W, c->d_psi, c->d_bsk, c->stream));
     FHE_HIP_CHECK(hipMalloc(&c->d_bsk_quad, (size_t)npoly * 1024 * sizeof(double2)));
     FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, c->d_bsk_quad, c->stream));
-    if (p.grouping == 1) {  // the pair kernel runs the classic blind rotation only
-        FHE_HIP_CHECK(hipMalloc(&c->d_bsk_pair, (size_t)npoly * 1024 * sizeof(double2)));
-        FHE_HIP_CHECK(launch_bsk_to_pair(c->d_bsk, npoly, c->d_bsk_pair, c->stream));
-    }
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
     FHE_HIP_CHECK(hipFree(d_std));
     if (!c->has_key || !(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {

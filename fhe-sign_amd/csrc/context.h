@@ -14,6 +14,7 @@ namespace fhe {
 
 class Engine;
 void set_error(const std::string& msg);
+const char* last_error();
 #define FHE_HIP_CHECK(expr)                                                                   \
     do {                                                                                      \
         hipError_t _e = (expr);                                                               \
@@ -108,6 +109,9 @@ struct fhe_ctx {
     // in-place all-gather of nranks segments of `words` u64 each (segment `rank` is local)
     int allgather(uint64_t* buf, size_t words);
     void release_comm();
+    // wait for the stream; with a communicator attached, bounded by comm_timeout_ms (a collective
+    // whose peer died is aborted instead of hanging this rank)
+    int wait_stream(const char* what);
 
     int ensure_ms(size_t count);
     int ensure_ks(size_t count);

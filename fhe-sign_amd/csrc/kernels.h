@@ -63,6 +63,8 @@ hipError_t launch_blind_rotate_pair(const uint64_t* ms, int ms_stride, const Pbs
 hipError_t launch_bsk_to_pair(const double2* bsk, int npoly, double2* out, hipStream_t s);
 // dst[i][0..2049) = src[i * 2049 ..] for i < count (all-gathered level outputs -> block slots)
 hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s);
+// the reverse: block slots -> contiguous [count][2049] (operand broadcast, comm.cpp)
+hipError_t launch_gather_blocks(const uint64_t* const* src, uint64_t* dst, int count, hipStream_t s);
 hipError_t launch_bsk_to_fourier(const uint64_t* bsk, int npoly, const double2* W,
                                  const double2* psi, double2* out, hipStream_t s);
 

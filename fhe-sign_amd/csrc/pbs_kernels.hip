@@ -187,6 +187,18 @@ __global__ __launch_bounds__(256) void k_scatter_blocks(const uint64_t* __restri
     for (int j = threadIdx.x; j < 2049; j += 256) d[j] = s[j];
 }
 
+__global__ __launch_bounds__(256) void k_gather_blocks(const uint64_t* const* __restrict__ src, uint64_t* __restrict__ dst) {
+    const uint64_t* s = src[blockIdx.x];
+    uint64_t* d = dst + (size_t)blockIdx.x * 2049;
+    for (int j = threadIdx.x; j < 2049; j += 256) d[j] = s[j];
+}
+
+hipError_t launch_gather_blocks(const uint64_t* const* src, uint64_t* dst, int count, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_blocks, dim3(count), dim3(256), 0, s, src, dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_scatter_blocks, dim3(count), dim3(256), 0, s, src, dst);

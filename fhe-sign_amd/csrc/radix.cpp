@@ -405,6 +405,7 @@ void Engine::flush() {
         }
         pbs_count += G;
         levels += 1;
+        if (level_log.size() < kLevelLogCap) level_log.push_back((uint32_t)G);
         if (trace_) {
             hip_check(hipStreamSynchronize(ctx_->stream), "trace sync");
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -497,12 +498,54 @@ void Engine::download(const Block& b, uint64_t* ct) {
     engine_check(!b.trivial() && !b.lazy(), "download of a trivial or lazy block");
     flush();
     hip_check(hipMemcpyAsync(ct, b.slot->p, kBigCt * 8, hipMemcpyDeviceToHost, ctx_->stream), "download");
-    hip_check(hipStreamSynchronize(ctx_->stream), "download sync");
+    if (ctx_->wait_stream("download") != FHE_OK) throw std::runtime_error(last_error());
 }
 
 void Engine::sync() {
     flush();
-    hip_check(hipStreamSynchronize(ctx_->stream), "sync");
+    if (ctx_->wait_stream("sync") != FHE_OK) throw std::runtime_error(last_error());
+}
+
+Blocks Engine::adopt_device(const uint64_t* d_cts, size_t n) {
+    Blocks out(n);
+    if (n == 0) return out;
+    if (n > up_cap_) {
+        hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");
+        if (d_up_) hip_check(hipFree(d_up_), "hipFree");
+        hip_check(hipMalloc(&d_up_, n * 8), "hipMalloc upload");
+        up_cap_ = n;
+    }
+    std::vector<uint64_t*> dst(n);
+    for (size_t i = 0; i < n; ++i) {
+        out[i].slot = pool_->alloc();
+        dst[i] = out[i].slot->p;
+    }
+    uint64_t** d_dst = reinterpret_cast<uint64_t**>(d_up_);
+    hip_check(hipMemcpyAsync(d_dst, dst.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice, ctx_->stream), "adopt");
+    hip_check(launch_scatter_blocks(d_cts, d_dst, (int)n, ctx_->stream), "adopt scatter");
+    hip_check(hipStreamSynchronize(ctx_->stream), "adopt sync");  // the pointer staging may be reused
+    return out;
+}
+
+void Engine::gather_device(const std::vector<const Block*>& blocks, uint64_t* d_out) {
+    flush();
+    const size_t n = blocks.size();
+    if (n == 0) return;
+    if (n > up_cap_) {
+        hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");
+        if (d_up_) hip_check(hipFree(d_up_), "hipFree");
+        hip_check(hipMalloc(&d_up_, n * 8), "hipMalloc upload");
+        up_cap_ = n;
+    }
+    std::vector<const uint64_t*> src(n);
+    for (size_t i = 0; i < n; ++i) {
+        engine_check(blocks[i]->slot != nullptr && !blocks[i]->lazy(), "gather of a trivial or lazy block");
+        src[i] = blocks[i]->slot->p;
+    }
+    const uint64_t** d_src = reinterpret_cast<const uint64_t**>(d_up_);
+    hip_check(hipMemcpyAsync(d_src, src.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice, ctx_->stream), "gather");
+    hip_check(launch_gather_blocks(d_src, d_out, (int)n, ctx_->stream), "gather");
+    hip_check(hipStreamSynchronize(ctx_->stream), "gather sync");
 }
 
 Block block_lazy(const std::vector<Term>& terms, int32_t cst, uint32_t degree) {

@@ -115,9 +115,16 @@ public:
     // n client-encrypted blocks (contiguous big LWEs): one copy + one scatter into their slots
     Blocks upload_many(const uint64_t* cts, size_t n, uint32_t degree);
     void download(const Block& b, uint64_t* ct);
+    // n big LWEs contiguous in device memory -> fresh slots (one scatter); degree/noise set by the caller
+    Blocks adopt_device(const uint64_t* d_cts, size_t n);
+    // the slot blocks' ciphertexts -> contiguous device buffer (one gather; flushes first)
+    void gather_device(const std::vector<const Block*>& blocks, uint64_t* d_out);
     void sync();
     // statistics
     uint64_t pbs_count = 0, levels = 0, fanout_levels = 0;
+    // bootstraps per launched level, in launch order (fhe_ctx_level_log; the bench's CPU replay)
+    std::vector<uint32_t> level_log;
+    static constexpr size_t kLevelLogCap = 1u << 20;
 
 private:
     fhe_ctx* ctx_;
@@ -218,5 +225,10 @@ Radix radix_shl(Engine& e, const Radix& a, const Radix& amount);
 Radix radix_bitand(Engine& e, const Radix& a, const Radix& b);
 // refresh every block through an identity bootstrap (noise reset)
 Radix radix_clean(Engine& e, const Radix& a);
+
+// Collective over the context's communicator (comm.cpp): rank `root` replicates radix integers
+// (its `groups`) to every rank device-to-device; on the receivers `groups` is replaced by copies
+// whose block ciphertexts and metadata (degree, noise, trivial values) equal the root's.
+int bcast_radix_groups(fhe_ctx* c, int root, std::vector<Radix>* groups);
 
 }  // namespace fhe

@@ -73,6 +73,8 @@ _SIGNATURES = [
     ("fhe_ctx_attach_comm", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     ("fhe_ctx_attach_comm_timeout", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_uint32]),
     ("fhe_ctx_broadcast_server_key", C.c_int, [C.c_void_p, C.c_int]),
+    ("fhe_ctx_broadcast_radix", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int]),
+    ("fhe_ctx_broadcast_biguint", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int]),
     ("fhe_ctx_params", C.c_int, [C.c_void_p, C.POINTER(FheParams)]),
     ("fhe_ctx_detach_comm", C.c_int, [C.c_void_p]),
     ("fhe_ctx_set_fanout", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
@@ -122,6 +124,7 @@ _SIGNATURES = [
     ("fhe_radix_shl", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("fhe_radix_bitand", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("fhe_ctx_stats", C.c_int, [C.c_void_p, u64p, u64p]),
+    ("fhe_ctx_level_log", C.c_int, [C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_size_t), C.c_int]),
     ("fhe_schedule_levels", C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_size_t, C.c_int,
                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("fhe_biguint_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_void_p)]),

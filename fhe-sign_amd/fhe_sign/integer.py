@@ -34,6 +34,11 @@ def _ctx():
     return ctx
 
 
+def _hval(h):
+    """the address of a handle (c_void_p or int)"""
+    return h.value if isinstance(h, C.c_void_p) else h
+
+
 def _words(value: int, bits: int) -> np.ndarray:
     n = (bits + 63) // 64
     v = value % (1 << bits)
@@ -92,6 +97,19 @@ class FheUint:
         h = C.c_void_p()
         check(load().fhe_radix_clone(self._h, C.byref(h)))
         return self._wrap(h, self.bits)
+
+    @classmethod
+    def broadcast(cls, x, root: int = 0, ctx=None):
+        """Collective (fhe_ctx_broadcast_radix): rank `root` passes its FheUint, every other rank
+        passes None and receives a copy with byte-identical block ciphertexts (RCCL over xGMI)."""
+        ctx = ctx or _ctx()
+        h = C.c_void_p(_hval(x.handle) if x is not None else None)
+        check(load().fhe_ctx_broadcast_radix(ctx.handle, C.byref(h), root))
+        if x is not None and h.value == _hval(x.handle):
+            return x
+        bits = C.c_uint32()
+        check(load().fhe_radix_num_bits(h, C.byref(bits)))
+        return cls._wrap(h, int(bits.value))
 
     def export(self) -> np.ndarray:
         nb = self.bits // 2
@@ -305,6 +323,17 @@ class BigUintFHE:
             out.append(FheUint._wrap(h, 32))
         return out
 
+    @classmethod
+    def broadcast(cls, x, root: int = 0, ctx=None):
+        """Collective (fhe_ctx_broadcast_biguint): the root's BigUintFHE (e.g. sign_fhe_with_k0's
+        encrypted private key, src/schnorr.rs:235) replicated to every rank; other ranks pass None."""
+        ctx = ctx or _ctx()
+        h = C.c_void_p(_hval(x.handle) if x is not None else None)
+        check(load().fhe_ctx_broadcast_biguint(ctx.handle, C.byref(h), root))
+        if x is not None and h.value == _hval(x.handle):
+            return x
+        return cls(h)
+
     def decrypt_limbs(self, client_key) -> list[int]:
         n = len(self)
         buf = np.zeros(max(n, 1), np.uint32)
@@ -354,6 +383,15 @@ class BigUintFHE:
 
     __add__ = add
     __mul__ = mul
+
+
+def level_log(ctx, reset: bool = True) -> list[int]:
+    """bootstraps per launched level since the last reset (fhe_ctx_level_log)"""
+    n = C.c_size_t()
+    check(load().fhe_ctx_level_log(ctx.handle, None, 0, C.byref(n), 0))
+    buf = np.zeros(max(1, n.value), np.uint32)
+    check(load().fhe_ctx_level_log(ctx.handle, ptr(buf, C.c_uint32), buf.size, C.byref(n), 1 if reset else 0))
+    return [int(x) for x in buf[: n.value]]
 
 
 def stats(ctx):

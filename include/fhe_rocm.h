@@ -58,6 +58,8 @@ typedef struct fhe_params {
 typedef struct fhe_client_key fhe_client_key;
 typedef struct fhe_server_key fhe_server_key;
 typedef struct fhe_ctx fhe_ctx;
+typedef struct fhe_radix fhe_radix;     /* FheUint<num_bits> (radix integers, below) */
+typedef struct fhe_biguint fhe_biguint; /* BigUintFHE (below) */
 
 const char* fhe_last_error(void);
 int fhe_params_default(fhe_params* out);
@@ -174,7 +176,10 @@ int fhe_comm_unique_id(uint8_t id[FHE_COMM_ID_BYTES]);
 /* Non-blocking communicator init (RCCL ncclCommInitRankConfig, blocking = 0) polled against a
  * deadline: if a peer never joins, the communicator is aborted and FHE_ERR_TIMEOUT returned on the
  * ranks that did -- no rank is left waiting inside the library.  The same deadline bounds the
- * enqueue of every later collective (all-gather, key broadcast).  Callers should still agree out of
+ * enqueue of every later collective (all-gather, key and operand broadcasts) and, while a
+ * communicator is attached, every wait for the engine's stream (fhe_ctx_sync, downloads,
+ * decryption): a peer that dies after a collective was enqueued gives FHE_ERR_TIMEOUT (or the
+ * communicator's error) and an aborted, detached communicator instead of a hang.  Callers should still agree out of
  * band that every rank is ready before attaching (fhe_sign/dist.py: attach_fanout). */
 int fhe_ctx_attach_comm_timeout(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank,
                                 uint32_t timeout_ms);
@@ -186,6 +191,18 @@ int fhe_ctx_attach_comm(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int n
  * fhe_set_server_key had been called with the root's key.  A receiver keeps its previously installed
  * key (if any) until the collectives and conversions have succeeded: on any error it is unchanged. */
 int fhe_ctx_broadcast_server_key(fhe_ctx* ctx, int root);
+/* Collective operand distribution for the fan-out (config 5a): all ranks must run the radix
+ * program on byte-identical ciphertexts, but an input such as sign_fhe_with_k0's encrypted private
+ * key (src/schnorr.rs:235,270-277) arrives on one rank.  Rank `root` passes its handle in *x;
+ * every other rank receives a new handle in *x (its previous value is not read) whose block
+ * ciphertexts and metadata equal the root's (RCCL broadcast over xGMI, device to device).  Every
+ * rank needs an installed server key of the same message/carry parameters.  Failures are agreed
+ * before any data moves (every rank returns an error, none waits), and the final wait is bounded
+ * by the communicator's timeout (then the communicator is aborted).  Without a communicator (one
+ * GPU, emulated ranks) the root's blocks take the receiving path locally (gather, scatter into new
+ * slots) and *x is replaced by the new handle; the caller still owns the one it passed. */
+int fhe_ctx_broadcast_radix(fhe_ctx* ctx, fhe_radix** x, int root);
+int fhe_ctx_broadcast_biguint(fhe_ctx* ctx, fhe_biguint** x, int root);
 /* parameters of the server key installed in a context */
 int fhe_ctx_params(const fhe_ctx* ctx, fhe_params* out);
 int fhe_ctx_detach_comm(fhe_ctx* ctx);
@@ -198,7 +215,6 @@ int fhe_ctx_fanout_info(const fhe_ctx* ctx, int* rank, int* nranks, uint64_t* fa
 /* FheUint<num_bits> (num_bits even, <= FHE_RADIX_MAX_BITS): num_bits/2 radix blocks, device-resident.
  * Replaces tfhe's FheUint8/32/64 as used at src/biguint.rs:26,135-143,221-248 and
  * src/perf_test.rs:19-54.  Arithmetic wraps modulo 2^num_bits (tfhe semantics). */
-typedef struct fhe_radix fhe_radix;
 #define FHE_RADIX_MAX_BITS 4096
 /* FheUint::try_encrypt (src/biguint.rs:26, src/perf_test.rs:19-21); words little-endian */
 int fhe_radix_encrypt(fhe_ctx* ctx, fhe_client_key* ck, const uint64_t* words, uint32_t num_bits,
@@ -263,6 +279,10 @@ int fhe_radix_shl(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* amount, fhe
 int fhe_radix_bitand(fhe_ctx* ctx, const fhe_radix* a, const fhe_radix* b, fhe_radix** out);
 /* engine statistics since context creation: bootstraps executed and dependency levels */
 int fhe_ctx_stats(fhe_ctx* ctx, uint64_t* pbs_count, uint64_t* levels);
+/* bootstraps per launched dependency level, in launch order, since the last reset (host-side
+ * record, at most 2^20 levels): *n = the number recorded, min(cap, *n) written to sizes; reset != 0
+ * clears the record.  bench.py replays these level sizes through the CPU restatement. */
+int fhe_ctx_level_log(fhe_ctx* ctx, uint32_t* sizes, size_t cap, size_t* n, int reset);
 /* The engine's level scheduler on an explicit dependency graph (host only, no GPU): node i reads
  * nodes deps[dep_offsets[i] .. dep_offsets[i+1]) (all < i).  Writes each node's launch level
  * (1-based) to level_of[i] and the level count (= the critical path) to *nlevels.  mode 0: backward
@@ -272,7 +292,6 @@ int fhe_schedule_levels(const int32_t* dep_offsets, const int32_t* deps, size_t 
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */
-typedef struct fhe_biguint fhe_biguint;
 #define FHE_BIGUINT_COMPAT 0 /* exact reference limb loop incl. src/biguint.rs:247-249 wrap */
 #define FHE_BIGUINT_FAST 1   /* true sum/product, one wide carry propagation */
 /* BigUintFHE::new (src/biguint.rs:17-31): limbs = value.to_u32_digits() (LSB first, no

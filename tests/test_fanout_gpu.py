@@ -113,6 +113,65 @@ def test_rccl_world1_server_key_broadcast(keys):
     ref_ctx.close()
 
 
+def _bcast_case(ctx, ck):
+    """inputs of a fanned-out sign: a BigUintFHE private key (8 limbs) and a 256-bit FheUint whose
+    upper blocks are trivial (cast up from 64 bits) -- both through the broadcast's receiving path"""
+    set_server_key(ctx)
+    d = int(CSV["1"]["secret key"], 16)
+    D = BigUintFHE.new(d, ck)
+    X = FheUint64.try_encrypt(0x0123_4567_89AB_CDEF, ck).cast_into(FheUint256)
+    return d, D, X
+
+
+@pytest.mark.parametrize("ranks", [0, 2])
+def test_operand_broadcast_loopback(keys, ranks):
+    """fhe_ctx_broadcast_biguint / _radix without a communicator (one GPU; `ranks` emulated): the
+    root's blocks take the receiving path locally -- gather into one device buffer, metadata encode /
+    validate, scatter into fresh slots -- so the copy's ciphertext words must equal the original's,
+    trivial blocks stay trivial, and the copies compute: sign_fhe_with_k0 on the broadcast key ==
+    the CSV (BIP-340 vector 1, src/schnorr.rs:270-277)."""
+    ck, sk = keys
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    if ranks:
+        ctx.set_fanout(min_level=257, emulate_ranks=ranks)
+    d, D, X = _bcast_case(ctx, ck)
+    D2 = BigUintFHE.broadcast(D, 0, ctx)
+    X2 = FheUint256.broadcast(X, 0, ctx)
+    assert D2.handle.value != D.handle.value and X2.handle.value != X.handle.value
+    for u, v in zip(D.digits, D2.digits):
+        assert np.array_equal(u.export(), v.export())
+    assert np.array_equal(X.export(), X2.export())
+    assert X2.decrypt(ck) == 0x0123_4567_89AB_CDEF
+    row = CSV["1"]
+    msg, aux = bytes.fromhex(row["message"]), bytes.fromhex(row["aux_rand"])
+    k0 = compute_nonce(d, msg, aux)
+    sig = Schnorr().sign_fhe_with_k0(msg, k0, d, D2, ck, COMPAT)
+    assert sig.hex().upper() == row["signature"].upper()
+    with pytest.raises(RuntimeError):
+        BigUintFHE.broadcast(D, 1 if ranks == 0 else ranks, ctx)  # root outside the world
+    set_server_key(None)
+    ctx.close()
+
+
+def test_rccl_world1_operand_broadcast(keys):
+    """the same collectives through a real RCCL communicator of world 1 (header, agreement
+    all-reduce, metadata and ciphertext broadcasts, bounded wait): the root keeps its handle, and the
+    context keeps computing afterwards.  The receiving side of a real communicator needs a second GPU
+    (the driver's multi-GPU node); its code path is the loopback one above."""
+    ck, sk = keys
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    ctx.attach_comm(comm_unique_id(), 1, 0)
+    d, D, X = _bcast_case(ctx, ck)
+    assert BigUintFHE.broadcast(D, 0, ctx) is D
+    assert FheUint256.broadcast(X, 0, ctx) is X
+    assert D.to_biguint(ck) == d and X.decrypt(ck) == 0x0123_4567_89AB_CDEF
+    ctx.detach_comm()
+    set_server_key(None)
+    ctx.close()
+
+
 # ---------------------------------------------------------------- config 5 at the production split
 CSV = {r["index"]: r for r in csv.DictReader(open(os.path.join(ROOT, "tests", "golden", "bip340_vectors.csv")))}
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -123,7 +182,7 @@ def _limbs(x):
 
 
 def _config5(ctx, ck):
-    """What config 5 runs: sign_fhe_with_k0 (compat, fast) on vector 0, its FHE block k + e*d' for
+    """What config 5 runs (inputs via the operand broadcast): sign_fhe_with_k0 (compat, fast) on vector 0, its FHE block k + e*d' for
     vector 1 (8x8 limbs) as ciphertexts, the compat 256-bit mul, and the 8-sign batch of SURVEY 8d
     (vectors 0, 1, 2, 15, 16, 17, 18, 0).  Returns (ciphertext words, decrypted values)."""
     set_server_key(ctx)
@@ -132,8 +191,11 @@ def _config5(ctx, ck):
     g = json.load(open(os.path.join(GOLD, "biguint_vectors.json")))["mul"][0]
     v1 = json.load(open(os.path.join(GOLD, "sign_vectors.json")))["vectors"][1]
     val = lambda limbs: sum(int(x) << (32 * i) for i, x in enumerate(limbs))  # noqa: E731
-    A, B = BigUintFHE.new(val(g["a"]), ck), BigUintFHE.new(val(g["b"]), ck)
-    E, D, K = (BigUintFHE.new(val(v1[k]), ck) for k in ("e", "d", "k"))
+    # the inputs through the operand broadcast (on one GPU its receiving path, locally), as a
+    # fanned-out run receives them from rank 0
+    bc = lambda v: BigUintFHE.broadcast(BigUintFHE.new(v, ck), 0, ctx)  # noqa: E731
+    A, B = bc(val(g["a"])), bc(val(g["b"]))
+    E, D, K = (bc(val(v1[k])) for k in ("e", "d", "k"))
     mul = A.mul(B, COMPAT)
     block = E.mul_add(D, K, COMPAT)
     cts = {"mul_compat": [x.export() for x in mul.digits], "sign_block_v1": [x.export() for x in block.digits]}
