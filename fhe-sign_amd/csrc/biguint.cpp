@@ -17,7 +17,6 @@ static Radix slice(const Radix& r, uint32_t from, uint32_t count) {
     return s;
 }
 
-// impl Add for BigUintFHE (src/biguint.rs:120-192)
 // impl Add for BigUintFHE (src/biguint.rs:120-192).  The reference's limb loop never wraps (each
 // FheUint64 sum is < 2^34, the carry is its bit 32) and it always appends the final carry limb,
 // except that a zero (empty) operand returns the other one cloned (:163-165, :175-177).  So the

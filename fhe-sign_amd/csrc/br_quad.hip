@@ -32,25 +32,9 @@
 #ifndef QMB_D
 #define QMB_D 3
 #endif
-// the same for the classic (G = 1) kernel
+// waves per SIMD of the classic (G = 1) kernel
 #ifndef QCL_W
 #define QCL_W 3
-#endif
-#ifndef QCL_D
-#define QCL_D 4
-#endif
-// G = 1: MAC split around the digit-swap barrier (own row prefetched whole, other row loaded as
-// the own products free its registers) instead of the QCL_D-deep ring
-#ifndef QCL_SPLIT
-#define QCL_SPLIT 1
-#endif
-// BSK slices and untwist factors through buffer resources (bptr: per-iteration bases in SGPRs)
-#ifndef QBUF
-#define QBUF 1
-#endif
-// G = 1: rotation reads with the region base as an immediate offset (one VALU op less per read)
-#ifndef QROT_IMM
-#define QROT_IMM 1
 #endif
 
 namespace fhe {
@@ -203,7 +187,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                                                               const cplx* __restrict__ mono,  // E[4096] (G = 2)
                                                               uint64_t* __restrict__ out, int n) {
     // one LDS block (the kernel's only LDS object, so it starts at address 0): the polynomials'
-    // exchange regions first -- the rotation reads address them with immediate offsets (QROT_IMM)
+    // exchange regions first -- the rotation reads address them with immediate offsets
     constexpr int QL_W = 2 * QX_SZ, QL_Z = QL_W + QTW_SZ, QL_M = QL_Z + QZ_LDS;
     __shared__ __attribute__((aligned(16))) cplx s_lds[QL_M + (G == 2 ? 3 * 2 * 64 : 1)];
     cplx(*s_x)[QX_SZ] = reinterpret_cast<cplx(*)[QX_SZ]>(s_lds);
@@ -275,9 +259,8 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-#if QBUF
+    // key slices and untwist factors through buffer resources (bptr: per-step bases in SGPRs)
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
-#endif
     const double sgn9 = __longlong_as_double((long long)((uint64_t)(0x3FF00000u | ((uint32_t)L << 31)) << 32));  // +-1 by L0
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
     for (int i = 0; i < n / G; ++i) {
@@ -302,17 +285,9 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         // BSK rows for this wave's own digit (row p) and the other polynomial's digit (row 1 - p)
         // (G = 2: pattern B = 1 of the group; patterns 2, 3 follow at +4 and +8 polynomials)
         const size_t g0 = G == 1 ? (size_t)i : (size_t)3 * i;
-#if QBUF
         const bptr P{ps_rs, 16u * (uint32_t)t, 0u};
         const bptr bm{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((g0 * 2 + p) * 2 + p) * 16 + 8 * h) * 1024u};
         const bptr bo{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((g0 * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 1024u};
-#else
-        const cplx* Pg = ps;
-        asm volatile("" : "+s"(Pg));
-        const gcptr P = as_global(Pg) + t;
-        const gcptr bm = as_global(bsk) + ((size_t)((g0 * 2 + p) * 2 + p) * 16 + 8 * h) * 64 + L;
-        const gcptr bo = as_global(bsk) + ((size_t)((g0 * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 64 + L;
-#endif
 
         cplx x[8];
         if constexpr (G == 1) {
@@ -322,7 +297,6 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         __syncthreads();
         double dg[16];  // digits of X^a acc - acc (all 16 rotated reads issued before the first use)
         double rv[16];
-#if QROT_IMM
         // byte offsets of the source coefficients (128 r + t - a) mod 4096: bits 0..13 address the
         // region (mod 2048), bit 14 is the negacyclic sign.  Each polynomial's waves run their own
         // copy of the reads with the region base as the immediate offset (inline asm: the compiler
@@ -357,16 +331,6 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         static_assert(QX_SZ * 16 == 17488, "region offset of the rotation reads");
 #pragma unroll
         for (int r = 0; r < 16; ++r) dg[r] = tor_digit_s(neg_bit14(rv[r], yy[r]) - acc[r]);
-#else
-        uint32_t uu[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            uu[r] = (uint32_t)(128 * r + t - (int)a) & 4095u;
-            rv[r] = rot[uu[r] & 2047u];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dg[r] = tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]);
-#endif
         __syncthreads();  // every rotation read done before the region is reused
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = make_double2(dg[r], dg[r + 8]);
@@ -392,22 +356,14 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         q_ct<1>(x, s_z[8 + B3], s_z[8 + B3]);
         q_ct<0>(x, s_z[16 + B3], s_z[24 + B3]);
         q_xpose_bc(x);
-        // BSK ring head, in flight across phase C and the digit swap
-        constexpr int QR = G == 1 ? QCL_D : QMB_D;
-        cplx Bq0[G == 1 ? (QCL_SPLIT ? 8 : QR) : 3 * QR], Bq1[G == 1 ? (QCL_SPLIT ? 8 : QR) : 3 * QR];
+        // BSK ring head, in flight across phase C and the digit swap (G = 1: the whole own-row slice)
+        constexpr int QR = G == 1 ? 8 : QMB_D;
+        cplx Bq0[G == 1 ? 8 : 3 * QR], Bq1[G == 1 ? 8 : 3 * QR];
         cplx em[G == 2 ? 3 : 1];  // G = 2: monomials of the current register pair, per pattern
         cplx eb[G == 2 ? 3 : 1];  // G = 2: lane factors of the group, per pattern
         if constexpr (G == 1) {
-#if QCL_SPLIT
 #pragma unroll
         for (int r = 0; r < 8; ++r) Bq0[r] = bm[r * 64];  // the whole own-row slice
-#else
-#pragma unroll
-        for (int r = 0; r < QR; ++r) {
-            Bq0[r] = bm[r * 64];
-            Bq1[r] = bo[r * 64];
-        }
-#endif
         } else {
 #pragma unroll
         for (int B = 0; B < 3; ++B) {
@@ -436,7 +392,6 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         wave_sync();
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bC + fq(2 * r)] = x[r];
-#if QCL_SPLIT
         // G = 1: mac2 = own digit x row p (the rounded product), then other digit x row 1 - p
         // accumulated into it, split around the barrier; the other row's loads go out as the own
         // row's registers free up
@@ -447,24 +402,11 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                 Bq1[r] = bo[r * 64];
             }
         }
-#endif
         __syncthreads();
         // mac2: own digit x BSK row p, then other digit x row 1 - p accumulated
         if constexpr (G == 1) {
-#if QCL_SPLIT
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = cmul_acc(x[r], other[bC + fq(2 * r)], Bq1[r]);
-#else
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const cplx Bm = Bq0[r % QR], Bo = Bq1[r % QR];
-            if (r + QR < 8) {
-                Bq0[r % QR] = bm[(r + QR) * 64];
-                Bq1[r % QR] = bo[(r + QR) * 64];
-            }
-            x[r] = mac2(x[r], Bm, other[bC + fq(2 * r)], Bo);
-        }
-#endif
         } else {
         // key bundle per point (oracle cmul_acc, patterns in order), then the MAC; the slice of the
         // next registers stream in behind (QR registers ahead), the monomials per register pair

@@ -25,6 +25,47 @@
 
 namespace fhe {
 
+// WIDE_STAMPS (diagnostic variant build only, tools/wide_stamps.sh): lane 0 of every wave of the
+// first WS_CT ciphertexts records the shader clock (s_memtime) at the phase boundaries of WS_IT
+// CMUX iterations from WS_I0 on, written with vector stores to g_wide_stamps, read back by
+// fhe_debug_wide_stamps.  The product build compiles none of it.
+#ifdef WIDE_STAMPS
+constexpr int WS_CT = 2, WS_I0 = 200, WS_IT = 32, WS_N = 10;
+__device__ uint64_t g_wide_stamps[WS_CT][8][WS_IT][WS_N];
+#define WSTAMP(k)                                                                                      \
+    do {                                                                                               \
+        if (ct < WS_CT && i >= WS_I0 && i < WS_I0 + WS_IT && L == 0)                                   \
+            g_wide_stamps[ct][w][i - WS_I0][(k) + L] = __builtin_amdgcn_s_memtime();                   \
+    } while (0)
+#else
+#define WSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
+// Wave priorities (s_setprio) of the two waves a SIMD holds (polynomial p = 0 and p = 1 of the same
+// q): with equal priority the older wave (p = 0) wins every issue conflict and the p = 1 waves are
+// the critical path (WIDE_STAMPS: they arrive ~900 cycles late at each barrier).  WIDE_PRIO
+// selects a schedule that hands the priority to the other polynomial's waves mid-phase.
+#ifndef WIDE_PRIO
+#define WIDE_PRIO 0
+#endif
+#define WP(a, b)                                 \
+    do {                                         \
+        if (p) __builtin_amdgcn_s_setprio(b);    \
+        else __builtin_amdgcn_s_setprio(a);      \
+    } while (0)
+#if WIDE_PRIO == 2
+#define WP_A() WP(0, 1)
+#define WP_B() WP(1, 0)
+#elif WIDE_PRIO == 3
+#define WP_A() WP(1, 0)
+#define WP_B() WP(0, 1)
+#else
+#define WP_A() do {} while (0)
+#define WP_B() do {} while (0)
+#endif
+
 namespace {
 // cross-wave regions: an XOR swizzle pos = A idx over GF(2) (bijective, no padding) under which the
 // D-side stores/loads and E-side loads/stores are all conflict-free by the gfx950 lane-group rules
@@ -257,6 +298,9 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         __syncthreads();
     }
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
+#if WIDE_PRIO == 1
+    WP(0, 1);
+#endif
     for (int i = 0; i < n / G; ++i) {
         cplx x[4];
         cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
@@ -267,6 +311,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         a_next = modswitch_2n(a_ct[i + 1]);
         if (a == 0) continue;
         reduce = (upd++ & 1u) != 0;
+        WSTAMP(0);
 
         // BSK slice for this iteration (issued early; consumed after the forward FFT)
         {
@@ -280,6 +325,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         }
 
         // ---- rotate (X^a acc - acc), decompose, twist
+        WP_A();
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int c = 256 * r + 4 * L + q;
@@ -298,13 +344,16 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         }
         asm volatile("" ::"v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
                      "v"(off[7]));
+        WSTAMP(1);
         __syncthreads();
+        WSTAMP(2);
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) rv[rr] = *(const __attribute__((address_space(3))) double*)(size_t)off[rr];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             x[r] = make_double2(tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]),
                                 tor_digit_s(neg_bit11(rv[r + 4], uu[r + 4]) - acc[r + 4]));
+        WSTAMP(3);
         } else {
         reduce = (upd++ & 1u) != 0;
         mB[0] = a_next;
@@ -351,6 +400,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         ct2(x, ZT[0], ZT[1]);
         xpose_AB(x);                 // A -> B: regs <-> lane bits 5,4
         ct2(x, ZT[2], ZT[3]);
+        WP_B();
         xpose_dpp32(x);              // B -> C: regs <-> lane bits 3,2
         ct2(x, ZT[4], ZT[5]);
 #pragma unroll
@@ -361,7 +411,9 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         ct2(x, ZT[6], ZT[7]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) cross[xD ^ fx(4 * r)] = x[r];
+        if constexpr (G == 1) WSTAMP(4);
         __syncthreads();
+        if constexpr (G == 1) WSTAMP(5);
         // phase E reads both polynomials' regions: stages 8, 9 of the other polynomial's digits are
         // recomputed here (identical operations to its own waves') instead of swapping the results
         // through LDS -- one barrier and one exchange less per CMUX
@@ -374,14 +426,17 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 y[r] = cross_other[xE ^ fx(r)];
             }
         }
+        WP_A();
         ct2_last(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
         ct2_last(y, ZT[8], ZT[9]);
 
         // ---- pointwise MAC (own digit x row p, then other digit x row 1 - p accumulated)
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], Kown[r], y[r], Koth[r]);
+        if constexpr (G == 1) WSTAMP(6);
 
         // ---- inverse FFT: E -> D (cross-wave) -> C -> B -> A (wave-private)
+        WP_B();
         {
             cplx a0 = x[0], c0 = x[1], a1 = x[2], c1 = x[3];
             x[0] = cadd(a0, c0); x[1] = csub(a0, c0);
@@ -394,9 +449,12 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 4; ++r) inv[xE ^ fx(r)] = x[r];
         if constexpr (G == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the monomial DMA
+        if constexpr (G == 1) WSTAMP(7);
         __syncthreads();
+        if constexpr (G == 1) WSTAMP(8);
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = inv[xD ^ fx(4 * r)];
+        WP_A();
         dit2(x, T[9], T[10], T[11]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) cd[cdpos(gL, r, aL)] = x[r];  // D -> C
@@ -404,6 +462,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = cd[cdpos(gL, aL, r)];
         dit2(x, T[6], T[7], T[8]);
+        WP_B();
         xpose_dpp32(x);              // C -> B
         dit2(x, T[3], T[4], T[5]);
         xpose_AB(x);                 // B -> A
@@ -422,6 +481,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
                 for (int r = 0; r < 8; ++r) acc[r] = tor_red_s(acc[r]);
             }
+            WSTAMP(9);
         } else {
             // branch-free here (a branch made the compiler drain the key-bundle loads in flight
             // across it: 1.63 -> 3.86 ms per level): tor_red_s with the scale 2^-23 or 0, the latter
@@ -446,6 +506,17 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         o[2048] = f64_to_torus(acc[0] * 0x1p41);
     }
 }
+
+#ifdef WIDE_STAMPS
+}  // namespace fhe
+extern "C" int fhe_debug_wide_stamps(uint64_t* out, size_t n) {
+    const size_t words = sizeof(fhe::g_wide_stamps) / 8;
+    if (n < words) return (int)words;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fhe::g_wide_stamps), words * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+namespace fhe {
+#endif
 
 hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const double2* bsk, const double2* tw, const double2* psiw,

@@ -18,7 +18,7 @@ if distinct:
     cts = np.ascontiguousarray(np.stack([ck.encrypt_block(m % 16) for m in range(B)]))
 else:
     cts = np.stack([ck.encrypt_block(m % 16) for m in range(64)])
-    cts = np.ascontiguousarray(np.concatenate([cts] * (B // 64)))
+    cts = np.ascontiguousarray(np.concatenate([cts] * max(1, B // 64))[:B])
 d_in = ctx.alloc(cts.nbytes); d_out = ctx.alloc(cts.nbytes); d_lut = ctx.alloc(B * 4)
 ctx.h2d(d_in, cts); ctx.h2d(d_lut, np.full(B, lid, np.uint32))
 ctx.enable_timing(True)

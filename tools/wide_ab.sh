@@ -1,15 +1,14 @@
 #!/bin/bash
-# Same-box A/B of the latency kernel (default build vs build_variants/$1) at B = 1, 128, 256, classic
-# and multi-bit (both template instances: a change can help one and hurt the other), after the PBS
-# parity tests.
+# Same-box A/B of latency-kernel variants (built by tools/build_variant.sh ... br_wide) at the
+# latency-level batches B = 1 and 256: the product build, then each variant, twice round.
+# usage: tools/wide_ab.sh OUTFILE VARIANT...
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_pbs_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/w_t.log 2>&1 || exit 1
+OUT=$1; shift
 for rep in 1 2; do
-  for mb in 0 1; do
-    for B in 1 128 256; do
-      for v in fhe-sign_amd build_variants/$1; do
-        FHE_PROBE_MB=$mb timeout -k 10 60 python tools/variant_probe.py $v $B 6 distinct >> gpurun_out/w_ab.txt 2>&1 || exit 2
-      done
+  for B in 1 256; do
+    timeout -k 10 120 python3 tools/variant_probe.py fhe-sign_amd $B 5 >> $OUT 2>&1 || exit 2
+    for v in "$@"; do
+      timeout -k 10 120 python3 tools/variant_probe.py build_variants/$v $B 5 >> $OUT 2>&1 || exit 3
     done
   done
 done
