@@ -186,7 +186,11 @@ size_t ks_planes_bytes(int n) { return (size_t)8 * ks_plane_tiles(n) * KS_KT * 1
 #define KS_MAX_SPLITS 16  // contraction splits for small batches (KS_KT / 16 = 10 k-tiles each)
 #endif
 static_assert(KS_KT % KS_MAX_SPLITS == 0 && KS_KT / KS_MAX_SPLITS >= 2, "split k-tile spans");
-size_t ks_digits_bytes(int count) { return (size_t)((count + 127) / 128) * 8 * KS_KT * 1024; }
+// k_ks_mfma reads the digit fragments of every tile its grid covers (64 KS_CW ciphertexts per
+// workgroup column, 4 KS_CW 16-row tiles), including tiles past the batch: size for whole columns
+size_t ks_digits_bytes(int count) {
+    return (size_t)((count + 64 * KS_CW - 1) / (64 * KS_CW)) * 4 * KS_CW * KS_KT * 1024;
+}
 
 hipError_t launch_ksk_to_planes(const uint64_t* ksk, int n, int8_t* planes, hipStream_t s) {
     const int tiles = ks_plane_tiles(n);

@@ -510,10 +510,19 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
         rot[j] = (double)(int64_t)lut[j];
     }
     poly_rotate_d(rot, (2 * FHO_N - bt) & (2 * FHO_N - 1), acc1);
-    /* The sum acc + y is reduced mod 2^64 on every second update only (the first, third, ... stay
-     * unreduced: |acc| <= 2^63 + 2|y| ~ 2^91, far inside the range where the next digit
-     * (rint of a value < 2^93 times 2^-41) is exact); a multi-bit group with no rotation counts as
-     * an update of acc + 0.  Saves a third of the accumulator arithmetic on the GPU. */
+    /* The sum acc + y is reduced mod 2^64 on every second update only; a multi-bit group with no
+     * rotation counts as an update of acc + 0.  Saves a third of the accumulator arithmetic on the GPU.
+     * Error bound.  |y| <= 2 N 2^22 2^63 = 2^97 (two digit polynomials, |digit| <= 2^22, key
+     * coefficients |.| <= 2^63); typical |y| ~ 2^90.5 (random signs: sqrt(2N) 2^22 2^63 / sqrt(3)).
+     * An unreduced acc = red(acc) + y has |acc| <= 2^63 + 2^97, rounded once (<= half an ulp: 2^44
+     * worst case, 2^37 typical); the next X^a acc - acc (|.| <= 2^98) rounds once more (<= 2^45) and
+     * its digit is exact for the value it holds (rint is exact; the digit's own rounding <= 2^40 is
+     * the gadget's).  So the f64 representative drifts from the exact torus value by <= 2^46 per
+     * CMUX in the worst case (2^-18 of the torus), ~2^38 typically, random in sign: after n = 834
+     * CMUXes <= 2^50.8 at worst against the decode half-step 2^58 and the modulus-switch noise
+     * sigma ~ 2^54.6, ~2^43 typically (tests/test_oracle.py::test_unreduced_accumulator_error_bound
+     * checks these bounds on worst-case magnitudes; the 2^20-bootstrap decode test,
+     * tests/test_noise_gpu.py, checks the end result). */
     uint32_t upd = 0;
 
     if (k->p.grouping == 2) {

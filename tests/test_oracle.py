@@ -165,3 +165,50 @@ def test_noise_failure_sample_oracle_10k(okeys):
     assert fails == 0
     for e in (err[:K], err[K:]):
         assert abs(e.std() / model - 1) < 0.15
+
+
+def _exact(x: float) -> int:
+    return int(x)  # every operand below is an integer-valued double (|x| >= 2^53 or built from an int)
+
+
+def _bal(v: int, m: int) -> int:
+    v %= m
+    return v - m if v >= m // 2 else v
+
+
+@pytest.mark.parametrize("ylog", [97, 90.5])
+def test_unreduced_accumulator_error_bound(ylog):
+    """the f64 accumulator is reduced mod 2^64 only on every second update, so the next
+    rotation difference can be ~2 |y| with |y| <= 2^97 (worst case; ~2^90.5 typical).  Model two
+    accumulator coefficients after an unreduced update, a = red(a0) + ya, b = red(b0) + yb, their
+    rotation difference v = b - a and its digit (oracle fho_tor_digit, base 2^23), and compare with
+    exact integer torus arithmetic: the digit must stay balanced (|d| <= 2^22) and be off the exact
+    digit by at most 2^5 digit units (2^46 of the torus) worst case -- the bound restated at
+    tfhe_oracle.c:fho_blind_rotate, far below the 2^58 decode half-step; then the reducing update
+    red(a + y2) must be exact mod 2^64 and land in [-2^63, 2^63]."""
+    lib = oracle.load()
+    rs = np.random.default_rng(7)
+    T = 1 << 64
+    worst = 0
+    for _ in range(4000):
+        a0, b0 = (float(int(x)) for x in rs.integers(-(1 << 62), 1 << 62, 2, dtype=np.int64) * 2)
+        sa, sb = rs.choice([-1.0, 1.0], 2)
+        ya = sa * float(2.0 ** ylog) * (1 - rs.random() * 2**-20)
+        yb = sb * float(2.0 ** ylog) * (1 - rs.random() * 2**-20)
+        ya, yb = float(round(ya)), float(round(yb))
+        a, b = a0 + ya, b0 + yb  # unreduced update: one rounding each
+        v = b - a  # the rotation difference: one more rounding
+        d = lib.fho_tor_digit(v, 23)
+        assert abs(d) <= 2**22 and d == int(d)
+        v_true = (_exact(b0) + _exact(yb)) - (_exact(a0) + _exact(ya))
+        d_true = _bal((v_true + (1 << 40)) >> 41, 1 << 23)  # round(v / 2^41) mod 2^23, balanced
+        err = abs(_bal(int(d) - d_true, 1 << 23))
+        worst = max(worst, err)
+        # the following (reducing) update: exact mod 2^64 and back in range
+        y2 = float(round(sa * 2.0 ** ylog * rs.random()))
+        s = a + y2
+        r = lib.fho_tor_red(s)
+        assert abs(r) <= 2.0**63 and (_exact(r) - _exact(s)) % T == 0
+    bound = 2**5 if ylog >= 97 else 2**0
+    print(f"\n|y| ~ 2^{ylog}: worst digit error {worst} digit units (bound {bound}; 1 unit = 2^41 of the torus)")
+    assert worst <= bound
