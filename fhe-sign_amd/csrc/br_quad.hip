@@ -37,6 +37,15 @@
 #define QCL_W 3
 #endif
 
+// QMB7 (timing-only variant builds, tools/g3_probe.sh): the G = 2 kernel with a grouping-3 step's
+// shape -- n/3 steps, 7 key patterns per step streamed and bundled -- on the grouping-2 key's slices
+// (wrong numbers; for the grouping-3 cost estimate of DESIGN.md 3a only)
+#ifdef QMB7
+constexpr int QMBP = 7, QMBDIV = 3;
+#else
+constexpr int QMBP = 3, QMBDIV = 2;
+#endif
+
 namespace fhe {
 
 namespace {
@@ -263,7 +272,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
     const double sgn9 = __longlong_as_double((long long)((uint64_t)(0x3FF00000u | ((uint32_t)L << 31)) << 32));  // +-1 by L0
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
-    for (int i = 0; i < n / G; ++i) {
+    for (int i = 0; i < n / (G == 1 ? 1 : QMBDIV); ++i) {
         uint32_t a = 0, mB[3] = {0u, 0u, 0u};
         if constexpr (G == 1) {
             a = a_next;
@@ -284,7 +293,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
         // BSK rows for this wave's own digit (row p) and the other polynomial's digit (row 1 - p)
         // (G = 2: pattern B = 1 of the group; patterns 2, 3 follow at +4 and +8 polynomials)
-        const size_t g0 = G == 1 ? (size_t)i : (size_t)3 * i;
+        const size_t g0 = G == 1 ? (size_t)i : QMBP == 3 ? (size_t)3 * i : (size_t)(7 * i) % (3 * 417 - 7);
         const bptr P{ps_rs, 16u * (uint32_t)t, 0u};
         const bptr bm{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((g0 * 2 + p) * 2 + p) * 16 + 8 * h) * 1024u};
         const bptr bo{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((g0 * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 1024u};
@@ -358,7 +367,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         q_xpose_bc(x);
         // BSK ring head, in flight across phase C and the digit swap (G = 1: the whole own-row slice)
         constexpr int QR = G == 1 ? 8 : QMB_D;
-        cplx Bq0[G == 1 ? 8 : 3 * QR], Bq1[G == 1 ? 8 : 3 * QR];
+        cplx Bq0[G == 1 ? 8 : QMBP * QR], Bq1[G == 1 ? 8 : QMBP * QR];
         cplx em[G == 2 ? 3 : 1];  // G = 2: monomials of the current register pair, per pattern
         cplx eb[G == 2 ? 3 : 1];  // G = 2: lane factors of the group, per pattern
         if constexpr (G == 1) {
@@ -366,11 +375,11 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         for (int r = 0; r < 8; ++r) Bq0[r] = bm[r * 64];  // the whole own-row slice
         } else {
 #pragma unroll
-        for (int B = 0; B < 3; ++B) {
+        for (int B = 0; B < QMBP; ++B) {
 #pragma unroll
             for (int d = 0; d < QR; ++d) {
-                Bq0[3 * d + B] = bm[B * 4 * 1024 + d * 64];
-                Bq1[3 * d + B] = bo[B * 4 * 1024 + d * 64];
+                Bq0[QMBP * d + B] = bm[B * 4 * 1024 + d * 64];
+                Bq1[QMBP * d + B] = bo[B * 4 * 1024 + d * 64];
             }
         }
         }
@@ -433,9 +442,10 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                 }
             }
 #pragma unroll
-            for (int B = 0; B < 3; ++B) {
-                const cplx w = (r & 1) ? turn_m1(em[B], make_uturn(mB[B])) : make_double2(em[B].x - 1.0, em[B].y);
-                const int sl = 3 * (r % QR) + B;
+            for (int B = 0; B < QMBP; ++B) {
+                const int b3 = B % 3;
+                const cplx w = (r & 1) ? turn_m1(em[b3], make_uturn(mB[b3])) : make_double2(em[b3].x - 1.0, em[b3].y);
+                const int sl = QMBP * (r % QR) + B;
                 const cplx Bm = Bq0[sl], Bo = Bq1[sl];
                 if (r + QR < 8) {
                     Bq0[sl] = bm[B * 4 * 1024 + (r + QR) * 64];

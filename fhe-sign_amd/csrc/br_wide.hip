@@ -23,6 +23,15 @@
 #include "device_math.h"
 #include "kernels.h"
 
+// WMB7 (timing-only variant builds, tools/g3_probe.sh): the G = 2 kernel with a grouping-3 step's
+// shape -- n/3 steps, 7 key patterns per step loaded and bundled -- on the grouping-2 key's slices
+// (wrong numbers; for the grouping-3 cost estimate of DESIGN.md 3a only)
+#ifdef WMB7
+constexpr int WMBP = 7, WMBDIV = 3;
+#else
+constexpr int WMBP = 3, WMBDIV = 2;
+#endif
+
 namespace fhe {
 
 // WIDE_STAMPS (diagnostic variant build only, tools/wide_stamps.sh): lane 0 of every wave of the
@@ -301,7 +310,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #if WIDE_PRIO == 1
     WP(0, 1);
 #endif
-    for (int i = 0; i < n / G; ++i) {
+    for (int i = 0; i < n / (G == 1 ? 1 : WMBDIV); ++i) {  // n / G in the product build
         cplx x[4];
         cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
         uint32_t mB[3] = {0u, 0u, 0u};
@@ -375,11 +384,20 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             const cplx* tf = s_monf + (i & 1) * 192 + fsel;
 #pragma unroll
             for (int r = 0; r < 4; ++r) Kown[r] = Koth[r] = make_double2(0.0, 0.0);
+#ifdef WMB7
+#pragma unroll
+            for (int BB = 0; BB < WMBP; ++BB) {
+                const int B = BB % 3;
+                const size_t sl = (size_t)(7 * i + BB) % (3 * 417);
+                const gcptr b0 = as_global(bsk) + ((size_t)((sl * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;
+                const gcptr b1 = as_global(bsk) + ((size_t)((sl * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;
+#else
 #pragma unroll
             for (int B = 0; B < 3; ++B) {
                 // (64-bit pointers here: the buffer form pushes one value of this kernel to scratch)
                 const gcptr b0 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;
                 const gcptr b1 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;
+#endif
                 const cplx e = cmul(tb[B * 256], tf[B * 64]);  // zeta^((4 j0 + 1) m_B)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
