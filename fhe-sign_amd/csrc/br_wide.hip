@@ -393,7 +393,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 const gcptr b1 = as_global(bsk) + ((size_t)((sl * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;
 #else
 #pragma unroll
-            for (int B = 0; B < 3; ++B) {
+            for (int B = 0; B < WMBP; ++B) {
                 // (64-bit pointers here: the buffer form pushes one value of this kernel to scratch)
                 const gcptr b0 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;
                 const gcptr b1 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;

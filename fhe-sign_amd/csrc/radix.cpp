@@ -67,6 +67,8 @@ Engine::Engine(fhe_ctx* ctx) : ctx_(ctx) {
     if (const char* t = getenv("FHE_TRACE_LEVELS")) trace_ = atoi(t) != 0;
     // FHE_SCHED=1: forward (deadline-driven) list scheduling instead of the default backward one
     if (const char* t = getenv("FHE_SCHED")) sched_ = atoi(t);
+    // FHE_ROUND: level fill granule in bootstraps per GPU (schedule experiments; default 256)
+    if (const char* t = getenv("FHE_ROUND")) round_ = std::max(1, atoi(t));
 }
 
 Engine::~Engine() {
@@ -339,7 +341,7 @@ void Engine::flush() {
     std::vector<std::vector<int32_t>> deps(N);
     for (size_t k = 0; k < N; ++k) deps[k] = pending_[k].deps;
     // a fanned-out level's round is one latency-kernel round on every rank
-    const size_t round = 256 * (size_t)std::max(1, ctx_->fanout_world());
+    const size_t round = (size_t)round_ * (size_t)std::max(1, ctx_->fanout_world());
     std::vector<std::vector<int32_t>> lv = schedule_levels(deps, sched_, round);
     // one staging copy of every level's descriptors (+ fanned-out levels' destination tables)
     const int W = ctx_->fanout_world();

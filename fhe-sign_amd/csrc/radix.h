@@ -133,6 +133,7 @@ private:
     size_t up_cap_ = 0;
     bool trace_ = false;
     int sched_ = 0;
+    int round_ = 256;  // level fill granule (bootstraps per GPU)
     double run_ns_ = 0.0;  // host time inside run() (trace)
     size_t run_calls_ = 0;
     static constexpr size_t kEagerBatch = 4096;
