@@ -198,11 +198,14 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     // one LDS block (the kernel's only LDS object, so it starts at address 0): the polynomials'
     // exchange regions first -- the rotation reads address them with immediate offsets
     constexpr int QL_W = 2 * QX_SZ, QL_Z = QL_W + QTW_SZ, QL_M = QL_Z + QZ_LDS;
+    // (G = 1 keeps its monomial factors in registers: 2 KB more LDS per workgroup would drop the
+    // kernel from 3 to 2 workgroups per CU -- 243 -> 263 ms per 32768)
     __shared__ __attribute__((aligned(16))) cplx s_lds[QL_M + (G == 2 ? 3 * 2 * 64 : 1)];
     cplx(*s_x)[QX_SZ] = reinterpret_cast<cplx(*)[QX_SZ]>(s_lds);
     cplx* s_w = s_lds + QL_W;
     cplx* s_z = s_lds + QL_Z;
-    // G = 2: this group's monomials E[(4 j + 1) m_B] of every lane's register pairs, [B][h][lane]
+    // this step's lane factors E[(4 (j0 mod 64) + 1) m_B] of the monomials, [B][h][lane] (G = 1: one
+    // pattern, m = a_i: the factored CMUX)
     cplx* s_mono = s_lds + QL_M;
     for (int k = threadIdx.x; k < 512; k += 256) s_w[tpos(k)] = W[k];
     for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[k] = zq[k];
@@ -210,10 +213,8 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     const int ct = blockIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;  // w in an SGPR
     const int p = w >> 1, h = w & 1, t = threadIdx.x & 127;
-    const int p_u = p;  // wave-uniform (scalar branch)
     cplx* reg = s_x[p];
     const cplx* other = s_x[p ^ 1];
-    double* rot = reinterpret_cast<double*>(reg);
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
     // lane bits of phases B and C (see the layout table above): L5 L4 L3 = (b3 b2 b1) in B, (b6 b5 b4)
     // in C; L2 L1 = b8 b7 and L0 = b0 in both
@@ -244,40 +245,53 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
     }
 
-    // G = 2: 4 (j0 mod 64) + 1 of this lane's phase-C point r = 0 (idx 512 h + 16 u + L0, j0 = bitrev)
+    // 4 (j0 mod 64) + 1 of this lane's phase-C point r = 0 (idx 512 h + 16 u + L0, j0 = bitrev)
     const uint32_t c4 = 4u * ((__builtin_bitreverse32((uint32_t)(512 * h + 16 * u + l0)) >> 22) & 63u) + 1u;
     uint32_t a_next = modswitch_2n(a_ct[0]);
-    uint32_t a_next1 = G == 2 ? modswitch_2n(a_ct[1]) : 0u;
-    // G = 2: the lane factors E[(4 (j0 mod 64) + 1) m_B] of a group by LDS-DMA from the p = 0 wave of
-    // each half (3 per group; the per-lane gathers they replace touched a cache line per lane and
-    // were half the L1 traffic), issued one group ahead.  Single buffer: issued after the inverse's
+    uint32_t a_next1 = modswitch_2n(a_ct[1]);  // G = 1: a of the step after next (two-deep pipeline)
+    // G = 1: the wave-uniform pair factors E[256 k a], k = 1..3, of the next step, loaded one step
+    // ahead as uniform-address vector loads (scalar loads are invariant: the compiler sank them to
+    // their use, where each one's latency sat in the MAC)
+    const __amdgpu_buffer_rsrc_t mono_trs = table_rsrc(mono);
+    auto pair_factor = [&](uint32_t idx) { return bptr{mono_trs, 0u, 16u * idx}[0]; };
+    cplx Fn[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Fn[k] = G == 1 ? pair_factor((256u * (k + 1) * a_next) & 4095u) : make_double2(0.0, 0.0);
+    // ... and the lane factor E[(4 (j0 mod 64) + 1) a] of the next step, one gather per lane
+    auto lane_factor = [&](uint32_t m) { return bptr{mono_trs, ((c4 * m) & 4095u) * 16u, 0u}[0]; };
+    cplx Ebn = G == 1 ? lane_factor(a_next) : make_double2(0.0, 0.0);
+    // The lane factors E[(4 (j0 mod 64) + 1) m_B] of a step by LDS-DMA from the p = 0 wave of each
+    // half (G = 2: 3 per group; the per-lane gathers they replace touched a cache line per lane and
+    // were half the L1 traffic), issued one step ahead.  Single buffer: issued after the inverse's
     // first barrier (every read of the table done), retired by the compiler's wait for the untwist
-    // factors loaded after it (VMEM loads return in order), published by the next group's barriers.
+    // factors loaded after it (VMEM loads return in order), published by the next step's barriers.
     const uint32_t mono_base = __builtin_amdgcn_readfirstlane(lds_off(s_mono + h * 64));
     const rsrc_t mono_rs = buffer_rsrc(mono, 4096 * 16);
     auto mono_dma = [&](uint32_t m0, uint32_t m1) {
         const uint32_t m[3] = {m0, m1, (m0 + m1) & 4095u};
         if (p == 0) {
 #pragma unroll
-            for (int B = 0; B < 3; ++B)
+            for (int B = 0; B < (G == 1 ? 1 : 3); ++B)
                 dma16_buf(mono_rs, ((c4 * m[B]) & 4095u) * 16u, mono_base + (uint32_t)(B * 2 * 64 * 16));
         }
     };
-    if constexpr (G == 2) {
-        mono_dma(a_next, a_next1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    if constexpr (G == 2) mono_dma(a_next, a_next1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     // key slices and untwist factors through buffer resources (bptr: per-step bases in SGPRs)
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
     const double sgn9 = __longlong_as_double((long long)((uint64_t)(0x3FF00000u | ((uint32_t)L << 31)) << 32));  // +-1 by L0
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
+    bool red_in = false;  // the previous update's reduction, deferred to this step's digits (red_digit_s)
     for (int i = 0; i < n / (G == 1 ? 1 : QMBDIV); ++i) {
         uint32_t a = 0, mB[3] = {0u, 0u, 0u};
         if constexpr (G == 1) {
+            // factored CMUX (oracle fho_blind_rotate): acc += (X^a - 1) ExtProd(GGSW(s_i), acc), the
+            // X^a - 1 as one complex multiply per point of the MAC output -- no rotation through
+            // LDS, two barriers less per CMUX.  a = 0 is not skipped: e - 1 = 0 exactly (oracle alike).
             a = a_next;
-            a_next = modswitch_2n(a_ct[i + 1]);
-            if (a == 0) continue;  // X^0 - 1 = 0 (uniform over the workgroup)
+            a_next = a_next1;
+            a_next1 = modswitch_2n(a_ct[i + 2 <= n ? i + 2 : n]);
         }
         const bool reduce = (upd++ & 1u) != 0;
         if constexpr (G == 2) {
@@ -298,55 +312,16 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         const bptr bm{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((g0 * 2 + p) * 2 + p) * 16 + 8 * h) * 1024u};
         const bptr bo{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((g0 * 2 + (p ^ 1)) * 2 + p) * 16 + 8 * h) * 1024u};
 
+        // digits of acc itself (the previous step's last barrier guards the region)
         cplx x[8];
-        if constexpr (G == 1) {
-        // ---- rotate (X^a acc - acc) through the polynomial's region, decompose
+        if (red_in) {  // wave-uniform: a scalar branch (no loads in flight here)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) rot[128 * r + t] = acc[r];
-        __syncthreads();
-        double dg[16];  // digits of X^a acc - acc (all 16 rotated reads issued before the first use)
-        double rv[16];
-        // byte offsets of the source coefficients (128 r + t - a) mod 4096: bits 0..13 address the
-        // region (mod 2048), bit 14 is the negacyclic sign.  Each polynomial's waves run their own
-        // copy of the reads with the region base as the immediate offset (inline asm: the compiler
-        // would fold the two copies into one with a base register add); lgkmcnt drained by hand.
-        uint32_t yy[16];
+            for (int r = 0; r < 8; ++r) x[r].x = red_digit_s(acc[r]);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) yy[r] = (((uint32_t)(t - (int)a) & 4095u) << 3) + 1024u * r;
-        uint32_t ad[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) ad[r] = yy[r] & 0x3FFFu;
-        // the 16 reads and the wait in ONE asm statement: the compiler sees the results only after
-        // the wait (split statements let it copy a result register before its data arrived)
-#define QROT_READS(OFF)                                                                                         \
-    asm volatile("ds_read_b64 %0, %16" OFF "\n\tds_read_b64 %1, %17" OFF "\n\tds_read_b64 %2, %18" OFF         \
-                 "\n\tds_read_b64 %3, %19" OFF "\n\tds_read_b64 %4, %20" OFF "\n\tds_read_b64 %5, %21" OFF        \
-                 "\n\tds_read_b64 %6, %22" OFF "\n\tds_read_b64 %7, %23" OFF "\n\tds_read_b64 %8, %24" OFF        \
-                 "\n\tds_read_b64 %9, %25" OFF "\n\tds_read_b64 %10, %26" OFF "\n\tds_read_b64 %11, %27" OFF      \
-                 "\n\tds_read_b64 %12, %28" OFF "\n\tds_read_b64 %13, %29" OFF "\n\tds_read_b64 %14, %30" OFF    \
-                 "\n\tds_read_b64 %15, %31" OFF "\n\ts_waitcnt lgkmcnt(0)"                                         \
-                 : "=&v"(rv[0]), "=&v"(rv[1]), "=&v"(rv[2]), "=&v"(rv[3]), "=&v"(rv[4]), "=&v"(rv[5]),          \
-                   "=&v"(rv[6]), "=&v"(rv[7]), "=&v"(rv[8]), "=&v"(rv[9]), "=&v"(rv[10]), "=&v"(rv[11]),        \
-                   "=&v"(rv[12]), "=&v"(rv[13]), "=&v"(rv[14]), "=&v"(rv[15])                                  \
-                 : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]),          \
-                   "v"(ad[7]), "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]),      \
-                   "v"(ad[14]), "v"(ad[15]))
-        if (p_u == 0) {
-            QROT_READS("");
+            for (int r = 0; r < 8; ++r) x[r].y = red_digit_s(acc[r + 8]);
         } else {
-            QROT_READS(" offset:17488");  // QX_SZ * 16: the second polynomial's region
-        }
-#undef QROT_READS
-        static_assert(QX_SZ * 16 == 17488, "region offset of the rotation reads");
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dg[r] = tor_digit_s(neg_bit14(rv[r], yy[r]) - acc[r]);
-        __syncthreads();  // every rotation read done before the region is reused
-#pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = make_double2(dg[r], dg[r + 8]);
-        } else {
-        // digits of acc itself: no rotation (the previous step's last barrier guards the region)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 8]));
+            for (int r = 0; r < 8; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 8]));
         }
 
         // ---- forward transform: twisted Cooley-Tukey (the negacyclic twist is in the zetas)
@@ -414,8 +389,31 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         __syncthreads();
         // mac2: own digit x BSK row p, then other digit x row 1 - p accumulated
         if constexpr (G == 1) {
+        // then (X^a - 1) per point: e = zeta^((4j+1) a) by the split of the multi-bit bundle below
+        // (lane factor with the sign (-1)^(L0 a), wave-uniform pair factor, odd registers i e)
+        cplx F[3];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = cmul_acc(x[r], other[bC + fq(2 * r)], Bq1[r]);
+        for (int k = 0; k < 3; ++k) {
+            F[k] = Fn[k];
+            Fn[k] = pair_factor((256u * (k + 1) * a_next) & 4095u);  // the next step's
+        }
+        const cplx Eb = Ebn;
+        Ebn = lane_factor(a_next);
+        cplx eb1, em1;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            x[r] = cmul_acc(x[r], other[bC + fq(2 * r)], Bq1[r]);
+            if (r == 0) {
+                const uint32_t sg = (uint32_t)(l0 & a) << 31;
+                eb1 = make_double2(neg_if(Eb.x, sg), neg_if(Eb.y, sg));
+            }
+            if (!(r & 1)) {
+                const uint32_t qk = ((r >> 2) & 1) + 2u * ((r >> 1) & 1);
+                em1 = qk == 0 ? eb1 : cmul(eb1, F[qk - 1]);
+            }
+            const cplx w = (r & 1) ? turn_sel_m1(em1, a) : make_double2(em1.x - 1.0, em1.y);
+            x[r] = cmul(x[r], w);
+        }
         } else {
         // key bundle per point (oracle cmul_acc, patterns in order), then the MAC; the slice of the
         // next registers stream in behind (QR registers ahead), the monomials per register pair
@@ -444,7 +442,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
 #pragma unroll
             for (int B = 0; B < QMBP; ++B) {
                 const int b3 = B % 3;
-                const cplx w = (r & 1) ? turn_m1(em[b3], make_uturn(mB[b3])) : make_double2(em[b3].x - 1.0, em[b3].y);
+                const cplx w = (r & 1) ? turn_sel_m1(em[b3], mB[b3]) : make_double2(em[b3].x - 1.0, em[b3].y);
                 const int sl = QMBP * (r % QR) + B;
                 const cplx Bm = Bq0[sl], Bo = Bq1[sl];
                 if (r + QR < 8) {
@@ -476,7 +474,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bA + fq(128 * r)];
-        __syncthreads();  // every B->A read done before the next rotation overwrites the region
+        __syncthreads();  // every B->A read done before the next step's A->B stores overwrite the region
         cplx pst[8];  // untwist factors conj(psi) 2^-51
 #pragma unroll
         for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
@@ -492,10 +490,11 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             acc[r] = y.x;
             acc[r + 8] = y.y;
         }
-        if (reduce) {  // wave-uniform: a scalar branch
+        red_in = reduce;  // applied at the next step's digits
+    }
+    if (red_in) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = tor_red_s(acc[r]);
-        }
+        for (int r = 0; r < 16; ++r) acc[r] = tor_red_s(acc[r]);
     }
 
     // ---- sample extract (coefficient 0)

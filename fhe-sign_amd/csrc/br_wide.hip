@@ -86,7 +86,6 @@ constexpr int CROSS_SZ = 1024;
 // both directions' b128 stores (8-lane groups) and loads (16-lane groups)
 constexpr int CD_SZ = 20 * 15 + 16;
 FHE_DEV constexpr int cdpos(int g, int a, int r) { return 20 * g + 4 * a + (r ^ a); }
-constexpr int ROT_SZ = 2560;  // accumulator staging (f64): pos(c) = c + (c >> 2)
 
 FHE_DEV constexpr int fx(int x) {
     int p = 0;
@@ -222,16 +221,17 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                                                               const cplx* __restrict__ zw,   // [10][256]
                                                               const cplx* __restrict__ mono, // E[4096] (G = 2)
                                                               uint64_t* __restrict__ out, int n) {
-    __shared__ __attribute__((aligned(16))) double s_rot[G == 1 ? 2 : 1][G == 1 ? ROT_SZ : 2];
+    constexpr int NMP = G == 1 ? 1 : 3;  // monomial patterns per step
     __shared__ __attribute__((aligned(16))) cplx s_cross[2][CROSS_SZ];
     __shared__ __attribute__((aligned(16))) cplx s_inv[2][CROSS_SZ];  // inverse E -> D exchange
     __shared__ __attribute__((aligned(16))) cplx s_cd[8][CD_SZ];      // C <-> D, one region per wave
-    // G = 2: the monomial factors of each lane's j0 (oracle fho_blind_rotate, grouping 2), gathered
-    // one group ahead by LDS-DMA: E[(4 (j0 mod 64) + 1) m_B] per [group parity][B][q][lane] from the
-    // p = 0 waves (the p = 1 waves' lanes have the same j0), E[256 f m_B] per [parity][B][f] (f < 4,
-    // the lane's (j0 >> 6) mod 4; 64 entries, 4 distinct) from wave 4
-    __shared__ __attribute__((aligned(16))) cplx s_mono[G == 2 ? 2 * 3 * 4 * 64 : 1];
-    __shared__ __attribute__((aligned(16))) cplx s_monf[G == 2 ? 2 * 3 * 64 : 1];
+    // The monomial factors of each lane's j0 (oracle fho_blind_rotate: e = zeta^((4j+1) m) by the
+    // split of DESIGN.md 3a), gathered one step ahead by LDS-DMA: E[(4 (j0 mod 64) + 1) m_B] per
+    // [step parity][B][q][lane] from the p = 0 waves (the p = 1 waves' lanes have the same j0),
+    // E[256 f m_B] per [parity][B][f] (f < 4, the lane's (j0 >> 6) mod 4; 64 entries, 4 distinct) from
+    // wave 4.  G = 1: one pattern, m = a_i (the factored CMUX); G = 2: B = 1..3.
+    __shared__ __attribute__((aligned(16))) cplx s_mono[2 * NMP * 4 * 64];
+    __shared__ __attribute__((aligned(16))) cplx s_monf[2 * NMP * 64];
 
     const int ct = blockIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;  // w in an SGPR
@@ -264,49 +264,52 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             acc[r] = v * 0x1p-41;
         }
     }
-    double* rot_me = s_rot[G == 1 ? p : 0];
     cplx* cd = s_cd[w];
     const int gL = L >> 2, aL = L & 3;
     cplx* cross = s_cross[p];
     // lane parts of the linear LDS maps
     const int xD = fx(16 * L + q), xE = fx(256 * q + 4 * L);
 
-    // G = 2: this lane's phase-E point r = 0 (idx 256 q + 4 L, natural j0 = bitrev): 4 (j0 mod 64) + 1
+    // this lane's phase-E point r = 0 (idx 256 q + 4 L, natural j0 = bitrev): 4 (j0 mod 64) + 1
     // and (j0 >> 6) mod 4 (lane bits 0, 1)
     const uint32_t j0 = __builtin_bitreverse32((uint32_t)(256 * q + 4 * L)) >> 22;
     const uint32_t c4 = 4u * (j0 & 63u) + 1u;
     const int fsel = (int)((j0 >> 6) & 3u);
 
+    // modulus-switched mask of the current step and the next one (G = 1: a_i, a_i+1; G = 2: the pairs)
     uint32_t a_next = modswitch_2n(a_ct[0]);
-    uint32_t a_next1 = G == 2 ? modswitch_2n(a_ct[1]) : 0u;
-    // G = 2: the monomials of group g (exponents m0, m1) for this wave's q, into parity buffer g & 1.
-    // Issued by the p = 0 waves at the top of group g - 1, before that group's key slices: the
-    // compiler's waits for those retire it (VMEM loads return in order; the explicit wait before the
-    // inverse exchange makes sure of it), and that group's barriers publish it.  The per-lane gather
-    // it replaces sat on the critical path of every group (B = 1 latency 2.00 -> 1.70 ms).
+    uint32_t a_next1 = modswitch_2n(a_ct[1]);
+    // The monomials of step g (exponents m[]) for this wave's q, into parity buffer g & 1.  Issued by
+    // the p = 0 waves at the top of step g - 1: the explicit wait before that step's inverse exchange
+    // retires them and its barrier publishes them.  The per-lane gather this replaced sat on the
+    // critical path of every step (multi-bit B = 1 latency 2.00 -> 1.70 ms).
     const uint32_t mono_base = __builtin_amdgcn_readfirstlane(lds_off(s_mono + q * 64));
     const uint32_t monf_base = __builtin_amdgcn_readfirstlane(lds_off(s_monf));
     const rsrc_t mono_rs = buffer_rsrc(mono, 4096 * 16);
-    auto mono_dma = [&](int g, uint32_t m0, uint32_t m1) {
-        const uint32_t m[3] = {m0, m1, (m0 + m1) & 4095u};
+    auto mono_dma = [&](int g, const uint32_t (&m)[NMP]) {
         if (p == 0) {
 #pragma unroll
-            for (int B = 0; B < 3; ++B)
+            for (int B = 0; B < NMP; ++B)
                 dma16_buf(mono_rs, ((c4 * m[B]) & 4095u) * 16u,
-                          mono_base + (uint32_t)(((g & 1) * 3 + B) * 4 * 64 * 16));
+                          mono_base + (uint32_t)(((g & 1) * NMP + B) * 4 * 64 * 16));
         } else if (q == 0) {
 #pragma unroll
-            for (int B = 0; B < 3; ++B)
+            for (int B = 0; B < NMP; ++B)
                 dma16_buf(mono_rs, ((256u * (uint32_t)(L & 3) * m[B]) & 4095u) * 16u,
-                          monf_base + (uint32_t)(((g & 1) * 3 + B) * 64 * 16));
+                          monf_base + (uint32_t)(((g & 1) * NMP + B) * 64 * 16));
         }
     };
-    if constexpr (G == 2) {
-        mono_dma(0, a_next, a_next1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+    if constexpr (G == 1) {
+        const uint32_t m0[1] = {a_next};
+        mono_dma(0, m0);
+    } else {
+        const uint32_t m0[3] = {a_next, a_next1, (a_next + a_next1) & 4095u};
+        mono_dma(0, m0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
+    bool red_in = false;  // the previous update's reduction, deferred to this step's digits (red_digit_s)
 #if WIDE_PRIO == 1
     WP(0, 1);
 #endif
@@ -314,12 +317,35 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         cplx x[4];
         cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
         uint32_t mB[3] = {0u, 0u, 0u};
-        bool reduce;
+        const bool reduce = (upd++ & 1u) != 0;
+        cplx e1;  // G = 1: zeta^((4 j0 + 1) a) of this lane's point r = 0
+        // digits of acc itself (no rotation).  G = 1: with the previous update's deferred reduction
+        // (a scalar branch), first in the step, before its key loads.  G = 2: after the key bundle and
+        // without the deferral (computed first, x live across the bundle's 24 loads made the scheduler
+        // serialise them, 1.6 -> 3.7 ms; after it with the branch the kernel spills)
+        auto digits = [&]() {
+            if (G == 1 && red_in) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[r].x = red_digit_s(acc[r]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[r].y = red_digit_s(acc[r + 4]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 4]));
+            }
+        };
+        if constexpr (G == 1) digits();
         if constexpr (G == 1) {
-        const uint32_t a = a_next;
-        a_next = modswitch_2n(a_ct[i + 1]);
-        if (a == 0) continue;
-        reduce = (upd++ & 1u) != 0;
+        // factored CMUX (oracle fho_blind_rotate): acc += (X^a - 1) ExtProd(GGSW(s_i), acc), the
+        // X^a - 1 as one complex multiply per point of the MAC output -- no rotation through LDS, no
+        // rotation barrier.  a = 0 is not skipped: e - 1 = 0 exactly, acc + (+-0) (oracle alike).
+        mB[0] = a_next;
+        a_next = a_next1;
+        if (i + 1 < n) {
+            const uint32_t m1[1] = {a_next};
+            mono_dma(i + 1, m1);
+        }
+        a_next1 = modswitch_2n(a_ct[i + 2 <= n ? i + 2 : n]);
         WSTAMP(0);
 
         // BSK slice for this iteration (issued early; consumed after the forward FFT)
@@ -332,46 +358,19 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 Koth[r] = b1[r * 64];
             }
         }
-
-        // ---- rotate (X^a acc - acc), decompose, twist
-        WP_A();
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const int c = 256 * r + 4 * L + q;
-            rot_me[c + (c >> 2)] = acc[r];
-        }
-        double rv[8];  // all 8 rotated reads issued before the first use
-        uint32_t uu[8], off[8];
-        // element c of the padded region sits at byte 8 (c + c / 4) = (10 c) & ~7: one 24-bit
-        // multiply-add with the region's (8-aligned) LDS address, one mask; computed before the
-        // barrier (the empty asm pins them there) so the 8 reads issue back to back after it
-        const uint32_t rot_addr = lds_off(rot_me);
-#pragma unroll
-        for (int rr = 0; rr < 8; ++rr) {
-            uu[rr] = (uint32_t)(256 * rr + 4 * L + q - (int)a) & 4095u;
-            off[rr] = (__umul24(uu[rr] & 2047u, 10u) + rot_addr) & ~7u;
-        }
-        asm volatile("" ::"v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
-                     "v"(off[7]));
+        e1 = cmul(s_mono[(i & 1) * 256 + q * 64 + L], s_monf[(i & 1) * 64 + fsel]);
         WSTAMP(1);
-        __syncthreads();
         WSTAMP(2);
-#pragma unroll
-        for (int rr = 0; rr < 8; ++rr) rv[rr] = *(const __attribute__((address_space(3))) double*)(size_t)off[rr];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            x[r] = make_double2(tor_digit_s(neg_bit11(rv[r], uu[r]) - acc[r]),
-                                tor_digit_s(neg_bit11(rv[r + 4], uu[r + 4]) - acc[r + 4]));
         WSTAMP(3);
         } else {
-        reduce = (upd++ & 1u) != 0;
         mB[0] = a_next;
         mB[1] = a_next1;
         mB[2] = (a_next + a_next1) & 4095u;
         if (2 * i + 2 < n) {
             a_next = modswitch_2n(a_ct[2 * i + 2]);
             a_next1 = modswitch_2n(a_ct[2 * i + 3]);
-            mono_dma(i + 1, a_next, a_next1);
+            const uint32_t m1[3] = {a_next, a_next1, (a_next + a_next1) & 4095u};
+            mono_dma(i + 1, m1);
         }
         // no skip of m0 = m1 = 0 (the DMA chain needs every group's barriers): K = 0 exactly and acc
         // comes back unchanged up to the sign of a zero (acc + (+-0), tor_red_s of a reduced value),
@@ -402,15 +401,13 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const cplx wv = r == 0 ? make_double2(e.x - 1.0, e.y)
-                                           : turn_m1(e, make_uturn((2 * (r & 1) + (r >> 1)) * mB[B]));
+                                           : turn_sel_m1(e, (2 * (r & 1) + (r >> 1)) * mB[B]);
                     Kown[r] = cmul_acc(Kown[r], b0[r * 64], wv);
                     Koth[r] = cmul_acc(Koth[r], b1[r * 64], wv);
                 }
             }
         }
-        // digits of acc itself (no rotation)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 4]));
+        digits();
         }
 
         // ---- forward transform (twisted: no twist multiply): A (stages 0,1) -> B -> C -> D
@@ -451,6 +448,14 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         // ---- pointwise MAC (own digit x row p, then other digit x row 1 - p accumulated)
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], Kown[r], y[r], Koth[r]);
+        if constexpr (G == 1) {  // (X^a - 1): point r = j0 + 256 bitrev2(r), e - 1 as in the multi-bit bundle
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const cplx wv = r == 0 ? make_double2(e1.x - 1.0, e1.y)
+                                       : turn_sel_m1(e1, (2 * (r & 1) + (r >> 1)) * mB[0]);
+                x[r] = cmul(x[r], wv);
+            }
+        }
         if constexpr (G == 1) WSTAMP(6);
 
         // ---- inverse FFT: E -> D (cross-wave) -> C -> B -> A (wave-private)
@@ -466,7 +471,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         cplx* inv = s_inv[p];
 #pragma unroll
         for (int r = 0; r < 4; ++r) inv[xE ^ fx(r)] = x[r];
-        if constexpr (G == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the monomial DMA
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the monomial DMA
         if constexpr (G == 1) WSTAMP(7);
         __syncthreads();
         if constexpr (G == 1) WSTAMP(8);
@@ -495,19 +500,19 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             acc[r + 4] = y.y;
         }
         if constexpr (G == 1) {
-            if (reduce) {  // wave-uniform: a scalar branch
-#pragma unroll
-                for (int r = 0; r < 8; ++r) acc[r] = tor_red_s(acc[r]);
-            }
             WSTAMP(9);
+            red_in = reduce;  // applied at the next step's digits
         } else {
-            // branch-free here (a branch made the compiler drain the key-bundle loads in flight
-            // across it: 1.63 -> 3.86 ms per level): tor_red_s with the scale 2^-23 or 0, the latter
-            // leaving acc exactly as it is
+            // branch-free (a branch here made the compiler drain the next key-bundle loads: 1.63 ->
+            // 3.86 ms per level): tor_red_s with the scale 2^-23 or 0, the latter leaving acc as it is
             const double sc = reduce ? 0x1p-23 : 0.0;
 #pragma unroll
             for (int r = 0; r < 8; ++r) acc[r] = __fma_rn(-0x1p23, __builtin_rint(acc[r] * sc), acc[r]);
         }
+    }
+    if (red_in) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[r] = tor_red_s(acc[r]);
     }
 
     // ---- sample extract

@@ -508,17 +508,12 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
             return FHE_ERR_HIP;
         }
     }
-    // commit: swap in the new key, release the old one (the pair kernel's layout, if any, is
-    // re-derived on its next use)
+    // commit: swap in the new key, release the old one
     std::swap(c->d_ksk, n_ksk);
     std::swap(c->d_ksk_planes, n_planes);
     std::swap(c->d_bsk, n_bsk);
     std::swap(c->d_bsk_quad, n_quad);
     drop_new();  // frees the previous key's buffers (null when there was none)
-    if (c->d_bsk_pair) {
-        (void)hipFree(c->d_bsk_pair);
-        c->d_bsk_pair = nullptr;
-    }
     if (!(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
         c->lut_ids.clear();
         c->h_luts.clear();

@@ -128,34 +128,6 @@ void quad_tables(const std::vector<double2>& W, const std::vector<double2>& psi,
         }
 }
 
-void pair_tables(const std::vector<double2>& W, const std::vector<double2>& psi, const std::vector<double2>& Z,
-                 std::vector<double2>* t) {
-    // layout constants: br_pair.hip PT_*
-    t->assign(860 + 1024, make_double2(0.0, 0.0));
-    auto& T = *t;
-    for (int li = 0; li < 16; ++li) {  // phase B: lane part (b9..b6) = L & 15
-        T[li] = Z[16 + li];
-        T[16 + li] = Z[32 + 2 * li];
-        for (int b5 = 0; b5 < 2; ++b5) T[32 + 16 * b5 + li] = Z[64 + 4 * li + 2 * b5];
-        for (int m = 0; m < 4; ++m) T[64 + 16 * m + li] = Z[128 + 8 * li + 2 * m];
-    }
-    for (int L = 0; L < 64; ++L) {  // phase C: lanes L5 L4 = b5 b4, L3..L0 = b9..b6
-        const int li = L & 15, lh = L >> 4;
-        for (int b3 = 0; b3 < 2; ++b3) T[128 + 64 * b3 + L] = Z[256 + 2 * (8 * li + 2 * lh + b3)];
-        for (int m = 0; m < 4; ++m) T[256 + 64 * m + L] = Z[512 + 2 * (16 * li + 4 * lh + m)];
-        T[784 + L] = W[8 * L];
-    }
-    for (int k = 0; k < 256; ++k) T[512 + k + (k >> 4)] = W[k];
-    for (int m = 0; m < 4; ++m) T[848 + m] = W[128 * m];
-    const int uni[8] = {1, 2, 4, 6, 8, 10, 12, 14};
-    for (int k = 0; k < 8; ++k) T[852 + k] = Z[uni[k]];
-    for (int r = 0; r < 16; ++r)
-        for (int L = 0; L < 64; ++L) {
-            const double2 q = psi[64 * r + L];
-            T[860 + 64 * r + L] = make_double2(std::ldexp(q.x, -51), -std::ldexp(q.y, -51));
-        }
-}
-
 void wide_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,
                  std::vector<double2>* psiw) {
     tw->assign(12 * 256, make_double2(0.0, 0.0));
@@ -307,19 +279,6 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     if ((int)count <= wide_threshold)
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
-    if (br_kernel == FHE_BR_PAIR && p.grouping == 1) {
-        // the opt-in pair kernel's BSK layout is derived on first use (stream-ordered after the
-        // Fourier BSK), not at every key install
-        if (!d_bsk_pair) {
-            const int npoly = (int)(p.ggsw_count() * 4);
-            hipError_t e = hipMalloc(&d_bsk_pair, (size_t)npoly * 1024 * sizeof(double2));
-            if (e != hipSuccess) return e;
-            e = launch_bsk_to_pair(d_bsk, npoly, d_bsk_pair, stream);
-            if (e != hipSuccess) return e;
-        }
-        return launch_blind_rotate_pair(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_pair, d_tab_pair, out,
-                                        (int)count, (int)p.n, stream);
-    }
     return launch_blind_rotate_quad(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_quad, d_tw_quad, d_psi_quad,
                                     d_zeta_quad, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
 }
@@ -580,12 +539,7 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
     FHE_HIP_CHECK(hipMalloc(&c->d_psi_wide, psiw.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_tw_wide, tww.data(), tww.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMemcpy(c->d_psi_wide, psiw.data(), psiw.size() * sizeof(double2), hipMemcpyHostToDevice));
-    std::vector<double2> tpair;
-    pair_tables(W0, psi, Z, &tpair);
-    FHE_HIP_CHECK(hipMalloc(&c->d_tab_pair, tpair.size() * sizeof(double2)));
-    FHE_HIP_CHECK(hipMemcpy(c->d_tab_pair, tpair.data(), tpair.size() * sizeof(double2), hipMemcpyHostToDevice));
     if (const char* e = getenv("FHE_WIDE_THRESHOLD")) c->wide_threshold = atoi(e);
-    if (const char* e = getenv("FHE_BR_KERNEL")) c->br_kernel = atoi(e) == FHE_BR_PAIR ? FHE_BR_PAIR : FHE_BR_QUAD;
     std::vector<double2> mono;
     mono_table(psi, &mono);
     FHE_HIP_CHECK(hipMalloc(&c->d_mono, mono.size() * sizeof(double2)));
@@ -605,7 +559,7 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     delete c->engine;
     c->engine = nullptr;
     c->release_comm();
-    void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_bsk_quad, c->d_bsk_pair, c->d_tab_pair, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
+    void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
                     c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_mono, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -624,9 +578,7 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
         FHE_HIP_CHECK(hipFree(c->d_ksk));
         FHE_HIP_CHECK(hipFree(c->d_bsk));
         FHE_HIP_CHECK(hipFree(c->d_bsk_quad));
-        if (c->d_bsk_pair) FHE_HIP_CHECK(hipFree(c->d_bsk_pair));
         FHE_HIP_CHECK(hipFree(c->d_ksk_planes));
-        c->d_bsk_pair = nullptr;
         c->d_ksk_planes = nullptr;
         c->d_ksk = nullptr;
         c->d_bsk = nullptr;
@@ -788,7 +740,12 @@ int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
         set_error("the 2-wave blind-rotate kernel (FHE_BR_NARROW) is retired; FHE_BR_QUAD is the throughput kernel");
         return FHE_ERR_INVALID;
     }
-    if (kind != FHE_BR_QUAD && kind != FHE_BR_PAIR) return FHE_ERR_INVALID;
+    if (kind == FHE_BR_PAIR) {
+        set_error("the 2-wave pair kernel (FHE_BR_PAIR) is retired (it ran at parity with FHE_BR_QUAD); "
+                  "FHE_BR_QUAD is the throughput kernel");
+        return FHE_ERR_INVALID;
+    }
+    if (kind != FHE_BR_QUAD) return FHE_ERR_INVALID;
     c->br_kernel = kind;
     return FHE_OK;
 }

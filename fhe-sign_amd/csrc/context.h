@@ -33,10 +33,6 @@ void quad_tables(const std::vector<double2>& W, const std::vector<double2>& psi,
                  std::vector<double2>* ps);
 void wide_tables(const std::vector<double2>& W, const std::vector<double2>& psi, std::vector<double2>* tw,
                  std::vector<double2>* psiw);
-// br_pair.hip: LDS image (zetas of forward stages 4-9, W[0..256), W[8 L], W[128 m]), then the
-// uniform zetas of stages 0-3 and the untwist factors [r][L] (read from global memory)
-void pair_tables(const std::vector<double2>& W, const std::vector<double2>& psi, const std::vector<double2>& Z,
-                 std::vector<double2>* t);
 // Accumulator polynomial of a univariate LUT (tfhe shortint box encoding, padding bit).
 void make_lut_poly(const Params& p, const uint32_t* f, std::vector<uint64_t>* lut);
 // E[k] = exp(i pi k / 2048), k < 4096, as i^(k >> 10) psi[k & 1023] exactly (oracle fho_monomials)
@@ -56,8 +52,6 @@ struct fhe_ctx {
     double2* d_tw_wide = nullptr;   // [12][256]
     double2* d_psi_wide = nullptr;  // [4][256]
     double2* d_bsk_quad = nullptr;  // Fourier BSK in the 4-wave kernel's layout (br_quad.hip)
-    double2* d_bsk_pair = nullptr;  // Fourier BSK in the 2-wave kernel's layout (br_pair.hip, classic keys)
-    double2* d_tab_pair = nullptr;  // context.cpp:pair_tables
     double2* d_tw_quad = nullptr;   // W[0..512)
     double2* d_psi_quad = nullptr;  // [2][8][128]: twist (unused since the twisted forward), untwist
     double2* d_zeta_quad = nullptr; // br_quad.hip zeta layout (context.cpp:quad_zetas)

@@ -83,6 +83,17 @@ FHE_DEV uturn make_uturn(uint32_t t) {
 FHE_DEV cplx turn_m1(cplx e, uturn u) {
     return make_double2(__fma_rn(u.c, e.x, __fma_rn(-u.s, e.y, -1.0)), __fma_rn(u.s, e.x, u.c * e.y));
 }
+// The same value by selects and sign flips (integer ops) plus one f64 subtract: qturn(e, t).x - 1.0
+// rounds once exactly like turn_m1's fma chain, .y is a move.  For the f64-issue-bound kernels
+// (f64 ops cost twice a 32-bit op on gfx950): 1 f64 op instead of 4.
+FHE_DEV cplx turn_sel_m1(cplx e, uint32_t t) {
+    const bool sw = (t & 1u) != 0;  // wave-uniform: v_cndmask with an SGPR condition
+    const double re = sw ? e.y : e.x, im = sw ? e.x : e.y;
+    const uint32_t nre = ((t + 1u) & 2u) << 30, nim = (t & 2u) << 30;  // i^1, i^2 negate re; i^2, i^3 im
+    const uint64_t bre = (uint64_t)__double_as_longlong(re) ^ ((uint64_t)nre << 32);
+    const uint64_t bim = (uint64_t)__double_as_longlong(im) ^ ((uint64_t)nim << 32);
+    return make_double2(__longlong_as_double((long long)bre) - 1.0, __longlong_as_double((long long)bim));
+}
 FHE_DEV cplx cadd(cplx a, cplx b) { return make_double2(a.x + b.x, a.y + b.y); }
 FHE_DEV cplx csub(cplx a, cplx b) { return make_double2(a.x - b.x, a.y - b.y); }
 FHE_DEV cplx conj_(cplx a) { return make_double2(a.x, -a.y); }
@@ -122,6 +133,15 @@ FHE_DEV double tor_red_s(double v) { return __fma_rn(-0x1p23, __builtin_rint(v *
 FHE_DEV double tor_digit_s(double v) {
     const double g = __builtin_rint(v);
     return __fma_rn(-0x1p23, __builtin_rint(g * 0x1p-23), g);
+}
+// Deferred reduction (bit-identical to the oracle's order): a reducing update leaves acc + y as it is
+// and the next step reduces it right before taking its digits -- tor_red_s lands in [-2^22, 2^22]
+// (units of 2^41), where tor_digit_s(v) = rint(v) (the balancing term is rint(+-0.5 or less) = 0), so
+// reduction + digit cost 3 + 1 f64 ops instead of 3 + 4.  Sample extraction is unchanged by a
+// pending reduction (f64_to_torus is exact mod 2^64), the kernels apply it anyway.
+FHE_DEV double red_digit_s(double& acc) {
+    acc = tor_red_s(acc);
+    return __builtin_rint(acc);
 }
 // -v if bit 11 of u is set (negacyclic wrap of a rotation index): bit 11 added at bit 31 of the high
 // word flips the sign (v_and + v_lshl_add; the compiler's own form of the xor takes three ops)

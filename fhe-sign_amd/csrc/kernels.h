@@ -56,11 +56,6 @@ hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const Pbs
                                     const double2* zq, const double2* mono, int grouping, uint64_t* out, int count,
                                     int n, hipStream_t s);
 hipError_t launch_bsk_to_quad(const double2* bsk, int npoly, double2* out, hipStream_t s);
-// throughput kernel, one wave per GLWE polynomial, two ciphertexts per workgroup (br_pair.hip; grouping 1)
-hipError_t launch_blind_rotate_pair(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
-                                    const uint64_t* luts, const double2* bsk_pair, const double2* tab, uint64_t* out,
-                                    int count, int n, hipStream_t s);
-hipError_t launch_bsk_to_pair(const double2* bsk, int npoly, double2* out, hipStream_t s);
 // dst[i][0..2049) = src[i * 2049 ..] for i < count (all-gathered level outputs -> block slots)
 hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s);
 // the reverse: block slots -> contiguous [count][2049] (operand broadcast, comm.cpp)

@@ -212,10 +212,8 @@ class Context:
         check(load().fhe_ctx_sync(self._h))
 
     def set_br_kernel(self, kind: int) -> None:
-        """1 = 4 waves per ciphertext (the default throughput kernel); 2 = one wave per GLWE
-        polynomial, two ciphertexts per workgroup (br_pair.hip, classic keys; multi-bit keys keep 1);
-        0, the retired round-1 2-wave kernel, is refused.  All blind-rotate kernels give identical
-        results."""
+        """1 = 4 waves per ciphertext (the throughput kernel, the only one); 0 and 2, the retired
+        2-wave and pair kernels, are refused (FHE_ERR_INVALID)."""
         check(load().fhe_ctx_set_br_kernel(self._h, int(kind)))
 
     def set_ks_kernel(self, kind: int) -> None:

@@ -152,9 +152,9 @@ int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
 /* Throughput blind-rotate kernel for levels above the threshold: 4 waves per ciphertext
- * (FHE_BR_QUAD) or one wave per GLWE polynomial, two ciphertexts per workgroup (FHE_BR_PAIR; classic
- * blind rotation only -- multi-bit keys keep FHE_BR_QUAD); FHE_BR_NARROW, the retired 2-wave kernel
- * of round 1, is refused with FHE_ERR_INVALID.  All blind-rotate kernels produce identical bits. */
+ * (FHE_BR_QUAD, the only one).  The retired kernels -- FHE_BR_NARROW (2 waves per ciphertext, round
+ * 1) and FHE_BR_PAIR (two ciphertexts per 4-wave workgroup, rounds 2-3: at parity, never default) --
+ * are refused with FHE_ERR_INVALID.  Both blind-rotate kernels produce identical bits. */
 #define FHE_BR_NARROW 0
 #define FHE_BR_QUAD 1
 #define FHE_BR_PAIR 2

@@ -583,14 +583,28 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
             }
         }
     }
+    /* Classic (grouping 1), factored CMUX:  acc += (X^a - 1) ExtProd(GGSW(s_i), acc).
+     * The textbook CMUX acc += ExtProd(GGSW(s_i), X^a acc - acc) needs the rotated accumulator in
+     * the coefficient domain (a cross-lane permutation on the GPU: an LDS round trip and two
+     * workgroup barriers per CMUX).  Multiplying by X^a - 1 commutes with the external product's
+     * key, so it is applied in the Fourier domain instead, as one complex multiply per point of the
+     * MAC output: O(j) <- cmul(O(j), e(j) - 1), e(j) = zeta^((4j+1) a) formed exactly as the
+     * multi-bit path above forms e_B (same split, same cmul, same quarter turn).  The digits are of
+     * acc itself.  Same key, same decrypted results; the blind-rotation noise doubles in variance
+     * (||X^a - 1||^2 = 2 on the key noise and on the digit rounding; DESIGN.md 3, measured in
+     * tests/test_noise_gpu.py), far below the modulus switch's. */
+    const double* Ecl = fho_monomials();
     for (uint32_t i = 0; i < (k->p.grouping == 2 ? 0 : n); ++i) {
         uint32_t a = fho_modswitch(ct_small[i]);
-        if (a == 0) continue;
         const int reduce = (int)(upd++ & 1u);
+        if (a == 0) { /* e - 1 = 0: acc + 0, reduced on schedule (the kernels run the step) */
+            if (reduce)
+                for (int j = 0; j < FHO_N; ++j) { acc0[j] = fho_tor_red(acc0[j]); acc1[j] = fho_tor_red(acc1[j]); }
+            continue;
+        }
         for (int m = 0; m < 2; ++m) {
             double* acc = m ? acc1 : acc0;
-            poly_rotate_d(acc, a, rot);
-            for (int j = 0; j < FHO_N; ++j) dig[j] = tor_digit(rot[j] - acc[j], down, base, ibase);
+            for (int j = 0; j < FHO_N; ++j) dig[j] = tor_digit(acc[j], down, base, ibase);
             fho_dpoly_to_fourier(dig, m ? D1 : D0);
         }
         const double* bi = k->bsk_f + (size_t)i * 4 * FHO_HALF * 2;
@@ -599,7 +613,20 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
             const double* B1 = bi + (1 * 2 + w) * FHO_HALF * 2; /* row 1 (body digit), poly w */
             for (int q = 0; q < FHO_HALF; ++q) {
                 const double br[2] = {B0[2 * q], B1[2 * q]}, bi[2] = {B0[2 * q + 1], B1[2 * q + 1]};
-                mac_own_first(D0 + 2 * q, D1 + 2 * q, br, bi, w, O + 2 * q);
+                double o[2];
+                mac_own_first(D0 + 2 * q, D1 + 2 * q, br, bi, w, o);
+                const uint32_t jn = bitrev((uint32_t)q, 10);
+                const double* b = Ecl + 2 * (((4 * (jn & 63) + 1) * a) & 4095u);
+                const double* f = Ecl + 2 * ((256 * ((jn >> 6) & 3) * a) & 4095u);
+                double er = fma(b[0], f[0], -(b[1] * f[1])), ei = fma(b[0], f[1], b[1] * f[0]);
+                switch (((jn >> 8) * a) & 3u) { /* i^t e, exact */
+                    case 0: break;
+                    case 1: { const double t = er; er = -ei; ei = t; break; }
+                    case 2: er = -er; ei = -ei; break;
+                    default: { const double t = er; er = ei; ei = -t; break; }
+                }
+                const double wr = er - 1.0, wi = ei;
+                cmul(o[0], o[1], wr, wi, O + 2 * q, O + 2 * q + 1);
             }
             fho_fourier_add_to_poly_r(O, w ? acc1 : acc0, reduce);
         }

@@ -35,9 +35,6 @@ def descriptors(src, tmp_path):
     ("br_wide.hip", "k_blind_rotate_wideILi2", 1, 256, 0),  # the same, multi-bit
     ("br_quad.hip", "k_blind_rotate_quadILi1", 3, 168, 0),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
     ("br_quad.hip", "k_blind_rotate_quadILi2", 2, 256, 0),  # multi-bit: 2 per CU, 2 waves/SIMD, deeper BSK ring
-    # opt-in pair kernel: 2 two-ciphertext workgroups per CU, 2 waves/SIMD; its 112 B of scratch are
-    # loop-invariant values reloaded once per CMUX (profiles/r2/ab_pair_r2.txt)
-    ("br_pair.hip", "k_blind_rotate_pair", 2, 256, 128),
 ])
 def test_blind_rotate_occupancy(tmp_path, src, kernel, lds_per_cu_ok, max_regs, max_scratch):
     d = descriptors(os.path.join(CSRC, src), tmp_path)

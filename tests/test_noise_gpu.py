@@ -16,7 +16,7 @@ are distinct tuples, not independent ones) and is counted separately; rounds 1..
 
 Model (printed beside the measurement): per CMUX the external product adds
 2 N var(digit) var(GGSW) = 2 * 2048 * (2^44/3) * (2^34/3) plus, when s_i = 1, the gadget rounding
-(2^80/3) (1 + N/2); n CMUX.  That gives the output sigma before f64 rounding; the measured excess is
+(2^80/3) (1 + N/2); the factored CMUX multiplies both by ||X^a - 1||^2 = 2; n CMUX.  That gives the output sigma before f64 rounding; the measured excess is
 the f64-accumulator/transform rounding.  The decode margin is set by the modulus switch (sigma =
 2^54.6 at 22 units, tests/test_oracle.py) against the 2^58 half box."""
 import math
@@ -37,8 +37,9 @@ def _model_sigma_log2(n, multibit=False):
     var_digit = 2.0 ** 44 / 3
     var_ggsw = 2.0 ** 34 / 3
     var_dec = (2.0 ** 80 / 3) * (1 + 1024)  # gadget rounding of one digit through the key polynomial
-    if not multibit:  # n CMUX: GGSW(s_i) noise, rounding when s_i = 1
-        return 0.5 * math.log2(n * (2 * 2048 * var_digit * var_ggsw + 0.5 * var_dec))
+    if not multibit:  # n factored CMUX (acc += (X^a - 1) ExtProd(GGSW(s_i), acc)): the GGSW(s_i) noise
+        # and, when s_i = 1, the rounding of acc's digits, both through ||X^a - 1||^2 = 2
+        return 0.5 * math.log2(n * (2 * 2048 * var_digit * var_ggsw * 2 + 0.5 * 2 * var_dec))
     # n/2 groups: the key bundle sum_B (X^m_B - 1) GGSW(f_B) carries 3 GGSW noises, each through
     # ||X^m - 1||^2 = 2; the rounding of acc's digits enters through (X^m(s) - 1) unless s = 00 (3/4)
     return 0.5 * math.log2(n / 2 * (2 * 2048 * var_digit * var_ggsw * 3 * 2 + 0.75 * 2 * var_dec))

@@ -114,11 +114,10 @@ def test_wide_and_quad_kernels_bit_identical(env):
     assert np.array_equal(wide[:6], ref)
 
 
-def test_pair_kernel_bit_identical(env):
-    """The 2-wave-per-ciphertext throughput kernel (br_pair.hip: one wave per GLWE polynomial, two
-    ciphertexts per workgroup) gives the same words as the latency kernel and the oracle; ragged
-    batches (1, 2, 3, 37: an odd batch leaves one spare ciphertext slot) with every LUT.  Multi-bit
-    keys run the 4-wave kernel under the same setting (the pair kernel is classic only)."""
+def test_quad_kernel_ragged_batches_and_retired_kernels(env):
+    """The throughput kernel at ragged batches (1, 2, 3, 37) with every LUT gives the latency kernel's
+    and the oracle's words; the retired blind-rotate kernels (0: round-1 2-wave, 2: the pair kernel)
+    are refused."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = [ctx.lut(t) for t in tables]
@@ -129,16 +128,18 @@ def test_pair_kernel_bit_identical(env):
         ctx.set_wide_threshold(1 << 30)
         wide = ctx.pbs(cts, lut_ids)
         ctx.set_wide_threshold(0)
-        ctx.set_br_kernel(2)
-        pair = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 2, 3, 37)}
+        quad = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 2, 3, 37)}
     finally:
-        ctx.set_br_kernel(1)
         ctx.set_wide_threshold(256)
-    for c, out in pair.items():
+    for c, out in quad.items():
         bad = [i for i in range(c) if not np.array_equal(out[i], wide[i])]
         assert not bad, f"batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
-    assert np.array_equal(pair[37][:6], ref)
+    assert np.array_equal(quad[37][:6], ref)
+    for kind in (0, 2):
+        with pytest.raises(Exception):
+            ctx.set_br_kernel(kind)
+    ctx.set_br_kernel(1)
 
 
 def test_keyswitch_kernels_identical(env):

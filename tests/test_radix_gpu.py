@@ -148,20 +148,6 @@ def test_biguint_mul_256_compat(keys):
     assert p1 > p0 and l1 > l0
 
 
-def test_biguint_mul_256_compat_pair_kernel(keys):
-    """config 2 through the opt-in 2-wave throughput kernel (br_pair.hip, descriptor mode: the radix
-    engine's linear-combination keyswitch feeding it): the same reference limbs.  Multi-bit keys run
-    the 4-wave kernel under the same setting."""
-    ck, ctx = keys
-    v = json.load(open(os.path.join(G, "biguint_vectors.json")))["mul"][1]
-    try:
-        ctx.set_br_kernel(2)
-        out = _big(ck, v["a"]).mul(_big(ck, v["b"]), COMPAT)
-        assert out.decrypt_limbs(ck) == v["out"]
-    finally:
-        ctx.set_br_kernel(1)
-
-
 def test_biguint_mul_256_config2_breadth(keys):
     """config 2 breadth on the HIP path: every committed seeded 8x8 pair, BIP-340 vector 1's e*d'
     and the all-ones (F7) pair, each in compat (the reference's limbs, src/biguint.rs:194-265, lost

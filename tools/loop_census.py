@@ -21,7 +21,7 @@ def census(path, kname):
     for l in lines[start:end]:
         t = l.strip()
         if re.match(r"^\.LBB\d+_\d+:", t):
-            lab = t.split(":")[0][1:]
+            lab = t.split(":")[0][2:]  # ".LBB2_27" -> "BB2_27", the form of "Header=BB2_27"
             mh = re.search(r"Header=(BB\d+_\d+)", t)
             cur = lab if "Loop Header" in t else (mh.group(1) if mh else None)
             continue
