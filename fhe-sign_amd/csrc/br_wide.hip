@@ -334,7 +334,10 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 for (int r = 0; r < 4; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 4]));
             }
         };
-        if constexpr (G == 1) digits();
+        if constexpr (G == 1) {
+            WSTAMP(0);
+            digits();
+        }
         if constexpr (G == 1) {
         // factored CMUX (oracle fho_blind_rotate): acc += (X^a - 1) ExtProd(GGSW(s_i), acc), the
         // X^a - 1 as one complex multiply per point of the MAC output -- no rotation through LDS, no
@@ -346,7 +349,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             mono_dma(i + 1, m1);
         }
         a_next1 = modswitch_2n(a_ct[i + 2 <= n ? i + 2 : n]);
-        WSTAMP(0);
 
         // BSK slice for this iteration (issued early; consumed after the forward FFT)
         {

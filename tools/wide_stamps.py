@@ -1,9 +1,10 @@
 """Per-CMUX critical path of the latency blind rotate (br_wide.hip, classic) from the WIDE_STAMPS
 variant build: lane 0 of every wave records s_memtime at the phase boundaries of 32 CMUX
 iterations.  usage (GPU box): python3 tools/wide_stamps.py [B ...]   (build: tools/wide_stamps.sh)
-Phases (stamp k -> k+1): 0 top -> 1 rotation stores + read addresses issued -> 2 barrier 1 ->
-3 rotated reads + digits -> 4 forward A..D + cross store -> 5 barrier 2 -> 6 phase E (both
-polynomials) + MAC -> 7 inverse first stage + store -> 8 barrier 3 -> 9 inverse D..A + accumulate."""
+Phases (stamp k -> k+1; factored CMUX, round 3): 0 top -> 1 digits (with the deferred reduction),
+monomial DMA, key loads issued, monomial factor -> (2, 3 empty) -> 4 forward A..D + cross store ->
+5 barrier X -> 6 phase E (both polynomials) + MAC + (X^a - 1) -> 7 inverse first stage + store ->
+8 barrier Y -> 9 inverse D..A + accumulate."""
 import ctypes as C
 import os
 import sys
@@ -14,8 +15,8 @@ sys.path.insert(0, VAR)
 import numpy as np  # noqa: E402
 from fhe_sign import Context, generate_keys, load  # noqa: E402
 
-NAMES = ["rot stores+addr", "barrier1", "rot reads+digits", "fwd A..D+store", "barrier2", "E + MAC",
-         "inv first+store", "barrier3", "inv D..A+acc", "loop tail/skip"]
+NAMES = ["digits+loads+e", "-", "-", "fwd A..D+store", "barrier X", "E + MAC + (X^a-1)",
+         "inv first+store", "barrier Y", "inv D..A+acc", "loop tail"]
 WS_CT, WS_IT, WS_N = 2, 32, 10
 
 lib = load()
@@ -65,7 +66,7 @@ for B in sizes:
     for name, d in rows:
         print(f"  {name:<19s} " + " ".join(f"{v:6.0f}" for v in d) + f" {d.max():6.0f} {d.max() / tot:5.1%}")
     # barrier skew: when each wave arrives at / leaves the barriers (relative to the earliest)
-    for k, lab in ((1, "arrive b1"), (4, "arrive b2"), (7, "arrive b3")):
+    for k, lab in ((4, "arrive X"), (7, "arrive Y")):
         arr = s0[:, it, k] - s0[:, it, k].min(axis=0)
         print(f"  {lab}: median lag per wave " + " ".join(f"{v:5.0f}" for v in np.median(arr, axis=1)))
     sys.stdout.flush()
