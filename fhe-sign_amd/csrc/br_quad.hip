@@ -50,7 +50,7 @@ namespace fhe {
 
 namespace {
 constexpr int WQ[10] = {1, 2, 4, 8, 16, 32, 66, 132, 274, 541};
-constexpr int QX_SZ = 1093;  // complex entries per polynomial region (>= 1024 u64 pairs for the rotation)
+constexpr int QX_SZ = 1093;  // complex entries per polynomial region (>= fq(1023) + 1 = 1077)
 
 FHE_DEV constexpr int fq(int i) {
     return ((i & 1) ? WQ[0] : 0) + ((i & 2) ? WQ[1] : 0) + ((i & 4) ? WQ[2] : 0) + ((i & 8) ? WQ[3] : 0) +
@@ -177,8 +177,9 @@ FHE_DEV void q_xpose_bc(cplx (&x)[8]) {
 // psi, then the untwist factors (psi.x 2^-51, -psi.y 2^-51): the oracle's 2^-10 and the accumulator's
 // 2^-41, exact scalings.
 //
-// G = blind-rotation grouping (as br_wide.hip): G = 1 classic; G = 2 multi-bit -- the digits of acc
-// itself (no rotation through LDS: two barriers less per step), and at the MAC the key bundle
+// G = blind-rotation grouping (as br_wide.hip): G = 1 classic, the factored CMUX (oracle
+// fho_blind_rotate: digits of acc itself, the MAC output times e - 1 per point); G = 2 multi-bit --
+// the digits of acc itself, and at the MAC the key bundle
 // K_rc = sum_B (e_B(j) - 1) G_B,rc per point, e_B(j) = zeta^((4j+1) m_B) as the oracle forms it:
 // i^((j >> 8) m) cmul(E[(4 (j mod 64) + 1) m], E[256 ((j >> 6) mod 4) m]).  A lane's phase-C points
 // are j = j0 + 256 (r & 1) + 128 ((r >> 1) & 1) + 64 (r >> 2), j0 = (h + 2 u') + 512 L0: the first
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                                                               const cplx* __restrict__ mono,  // E[4096] (G = 2)
                                                               uint64_t* __restrict__ out, int n) {
     // one LDS block (the kernel's only LDS object, so it starts at address 0): the polynomials'
-    // exchange regions first -- the rotation reads address them with immediate offsets
+    // exchange regions, the twiddles, the zetas (G = 2: the monomial lane factors)
     constexpr int QL_W = 2 * QX_SZ, QL_Z = QL_W + QTW_SZ, QL_M = QL_Z + QZ_LDS;
     // (G = 1 keeps its monomial factors in registers: 2 KB more LDS per workgroup would drop the
     // kernel from 3 to 2 workgroups per CU -- 243 -> 263 ms per 32768)

@@ -204,7 +204,8 @@ FHE_DEV void dit2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
 // (amdgpu-waves-per-eu), not workgroups per CU: the 8 waves of the one workgroup a CU holds (144 KB
 // of LDS) are 2 per SIMD, which caps the kernel at 256 VGPRs.
 //
-// G = blind-rotation grouping.  G = 1: one CMUX per key bit (rotation X^a acc - acc through LDS).
+// G = blind-rotation grouping.  G = 1: one factored CMUX per key bit (oracle fho_blind_rotate:
+// digits of acc itself, the MAC output times e - 1 per point, e = zeta^((4j+1) a) as below).
 // G = 2 (multi-bit, oracle fho_blind_rotate grouping 2): per pair of key bits the digits of acc
 // itself (no rotation, no rotation barrier) and the key bundle K_rc = sum_B (E[(4j+1) m_B] - 1) G_B,rc
 // (B = 1..3) built per Fourier point before the MAC.  In phase E a lane's four points are

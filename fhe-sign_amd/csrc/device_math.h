@@ -13,8 +13,9 @@
 //     zero, which cannot change any nonzero value and converts to torus 0 either way)
 //   * f64 -> torus: rint (v_rndne_f64), then exact mantissa/exponent reconstruction mod 2^64
 //   * blind-rotation accumulator: f64 torus representatives in [-2^63, 2^63] (oracle
-//     fho_blind_rotate): digit = tor_digit(X^a acc - acc), acc = tor_red(acc + y), u64 only at
-//     sample extraction
+//     fho_blind_rotate), factored CMUX: digit = tor_digit(acc), the MAC output times (e - 1) per
+//     Fourier point (X^a - 1), acc = tor_red(acc + y) on every second update, u64 only at sample
+//     extraction
 // The whole translation unit is compiled with -ffp-contract=off.
 //
 // FFT register layout (one wave64 owns one 1024-point complex FFT, 16 points per lane):
@@ -125,7 +126,7 @@ FHE_DEV double tor_digit(double v) {
     const double g = __builtin_rint(v * down);
     return __fma_rn(-base, __builtin_rint(g * ibase), g);
 }
-// The blind-rotation kernels keep the accumulator (and the rotation region) in units of 2^41: every
+// The blind-rotation kernels keep the accumulator in units of 2^41: every
 // operation on it is then an exact power-of-two rescaling of tor_red / tor_digit<23> above (no value
 // comes near the subnormal range), so results are bit-identical while the digit needs no scaling
 // multiply.  The untwist factors carry the 2^-41; sample extraction multiplies by 2^41.

@@ -482,9 +482,9 @@ static void mac_own_first(const double* D0, const double* D1, const double* kr, 
     o[1] = fma(dx[0], ki[1 - w], fma(dx[1], kr[1 - w], pi));
 }
 
-/* Blind rotation ACC = X^{-b} LUT, then n CMUX.  The accumulator's torus coefficients are kept as
- * f64 representatives in [-2^63, 2^63] instead of u64: X^a acc - acc is one f64 subtraction, its
- * gadget digit two rint's (fho_tor_digit, exact integers, no int->f64 conversion), and the external
+/* Blind rotation ACC = X^{-b} LUT, then n CMUX (factored, see the classic loop below).  The
+ * accumulator's torus coefficients are kept as f64 representatives in [-2^63, 2^63] instead of u64:
+ * the gadget digit is two rint's (fho_tor_digit, exact integers, no int->f64 conversion), and the external
  * product is added without rounding to an integer first (acc = tor_red(acc + y), the untwist
  * product fused in: fho_fourier_add_to_poly).  The extra error is the rounding of acc + y at the
  * magnitude of y (~2^90 typical, <= 2^97), i.e. the same order as

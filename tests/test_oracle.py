@@ -179,9 +179,10 @@ def _bal(v: int, m: int) -> int:
 @pytest.mark.parametrize("ylog", [97, 90.5])
 def test_unreduced_accumulator_error_bound(ylog):
     """the f64 accumulator is reduced mod 2^64 only on every second update, so the next
-    rotation difference can be ~2 |y| with |y| <= 2^97 (worst case; ~2^90.5 typical).  Model two
-    accumulator coefficients after an unreduced update, a = red(a0) + ya, b = red(b0) + yb, their
-    rotation difference v = b - a and its digit (oracle fho_tor_digit, base 2^23), and compare with
+    step's digit input can carry |y| <= 2^97 (worst case; ~2^90.5 typical).  Since round 3 the
+    classic CMUX is factored (oracle fho_blind_rotate) and takes the digits of acc itself, as the
+    multi-bit path always did: model an accumulator coefficient after an unreduced update,
+    a = red(a0) + ya (one rounding), and its digit (oracle fho_tor_digit, base 2^23), and compare with
     exact integer torus arithmetic: the digit must stay balanced (|d| <= 2^22) and be off the exact
     digit by at most 2^5 digit units (2^46 of the torus) worst case -- the bound restated at
     tfhe_oracle.c:fho_blind_rotate, far below the 2^58 decode half-step; then the reducing update
@@ -191,16 +192,13 @@ def test_unreduced_accumulator_error_bound(ylog):
     T = 1 << 64
     worst = 0
     for _ in range(4000):
-        a0, b0 = (float(int(x)) for x in rs.integers(-(1 << 62), 1 << 62, 2, dtype=np.int64) * 2)
-        sa, sb = rs.choice([-1.0, 1.0], 2)
-        ya = sa * float(2.0 ** ylog) * (1 - rs.random() * 2**-20)
-        yb = sb * float(2.0 ** ylog) * (1 - rs.random() * 2**-20)
-        ya, yb = float(round(ya)), float(round(yb))
-        a, b = a0 + ya, b0 + yb  # unreduced update: one rounding each
-        v = b - a  # the rotation difference: one more rounding
-        d = lib.fho_tor_digit(v, 23)
+        a0 = float(int(rs.integers(-(1 << 62), 1 << 62, dtype=np.int64)) * 2)
+        sa = rs.choice([-1.0, 1.0])
+        ya = float(round(sa * float(2.0 ** ylog) * (1 - rs.random() * 2**-20)))
+        a = a0 + ya  # unreduced update: one rounding
+        d = lib.fho_tor_digit(a, 23)  # the factored CMUX's digit of acc itself
         assert abs(d) <= 2**22 and d == int(d)
-        v_true = (_exact(b0) + _exact(yb)) - (_exact(a0) + _exact(ya))
+        v_true = _exact(a0) + _exact(ya)
         d_true = _bal((v_true + (1 << 40)) >> 41, 1 << 23)  # round(v / 2^41) mod 2^23, balanced
         err = abs(_bal(int(d) - d_true, 1 << 23))
         worst = max(worst, err)
