@@ -120,6 +120,9 @@ public:
     // the slot blocks' ciphertexts -> contiguous device buffer (one gather; flushes first)
     void gather_device(const std::vector<const Block*>& blocks, uint64_t* d_out);
     void sync();
+    static constexpr size_t kEagerHead = 3072;  // 4 rounds of the throughput kernel (3 x 256 CUs)
+    // nothing pending and no eager batch since the last flush (radix_mul_many's early head launch)
+    bool eager_head_ok() const { return eager_ok_ && pending_.empty(); }
     // statistics
     uint64_t pbs_count = 0, levels = 0, fanout_levels = 0;
     // bootstraps per launched level, in launch order (fhe_ctx_level_log; the bench's CPU replay)
