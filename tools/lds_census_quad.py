@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
 """LDS cycle census of one CMUX of the 4-wave blind rotation (br_quad.hip, classic), per wave.
+(Models the round-2 kernel, whose CMUX still had the rotation exchange; the factored CMUX of round 3
+has no rotation writes/reads -- DESIGN.md 3.)
 
 Every LDS instruction of the loop with its per-lane byte addresses, costed by the gfx950 rules of
 MI355X_MICROARCH.md's LDS table: lane groups per instruction, one LDS-array cycle per group when

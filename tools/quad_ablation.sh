@@ -1,3 +1,5 @@
+# (Round-1 ablations of the textbook-CMUX kernel: its variant sources are not kept; the script records how
+# profiles/r1/quad_ablation_r1o.txt was made.)
 # Quad-kernel ablations (timing only: each variant removes one piece and so decrypts wrongly) plus
 # the PBS tests and the latency sweep.  Variants: built with tools/build_variant.sh NAME SRC "" br_quad.
 set -o pipefail
