@@ -533,6 +533,20 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     }
 }
 
+// WIDE_INST: which instances this object holds.  The product build compiles this file twice
+// (Makefile): WIDE_INST = 1, the classic kernel alone, under the max-ilp machine scheduler
+// (-amdgpu-sched-strategy=max-ilp: B = 1 2.18 -> 2.10 ms, B = 256 2.52 -> 2.46 ms per level, same
+// box, profiles/r3/wide_sched_ab_r3m.txt), and WIDE_INST = 2, the multi-bit kernel under the default
+// one (max-ilp serialises its key-bundle loads: 1.60 -> 3.63 ms) plus the dispatcher.  0 (variant
+// and diagnostic builds): both in one object.
+#ifndef WIDE_INST
+#define WIDE_INST 0
+#endif
+hipError_t launch_blind_rotate_wide_g1(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
+                                       const uint64_t* luts, const double2* bsk, const double2* tw,
+                                       const double2* psiw, const double2* zw, const double2* mono, uint64_t* out,
+                                       int count, int n, hipStream_t s);
+
 #ifdef WIDE_STAMPS
 }  // namespace fhe
 extern "C" int fhe_debug_wide_stamps(uint64_t* out, size_t n) {
@@ -544,18 +558,28 @@ extern "C" int fhe_debug_wide_stamps(uint64_t* out, size_t n) {
 namespace fhe {
 #endif
 
+#if WIDE_INST != 2
+hipError_t launch_blind_rotate_wide_g1(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
+                                       const uint64_t* luts, const double2* bsk, const double2* tw,
+                                       const double2* psiw, const double2* zw, const double2* mono, uint64_t* out,
+                                       int count, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_blind_rotate_wide<1>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk,
+                       tw, psiw, zw, mono, out, n);
+    return hipGetLastError();
+}
+#endif
+#if WIDE_INST != 1
 hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const double2* bsk, const double2* tw, const double2* psiw,
                                     const double2* zw, const double2* mono, int grouping, uint64_t* out, int count,
                                     int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    if (grouping == 2)
-        hipLaunchKernelGGL(k_blind_rotate_wide<2>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts,
-                           bsk, tw, psiw, zw, mono, out, n);
-    else
-        hipLaunchKernelGGL(k_blind_rotate_wide<1>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts,
-                           bsk, tw, psiw, zw, mono, out, n);
+    if (grouping != 2)
+        return launch_blind_rotate_wide_g1(ms, ms_stride, desc, lut_idx, luts, bsk, tw, psiw, zw, mono, out, count, n, s);
+    hipLaunchKernelGGL(k_blind_rotate_wide<2>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk,
+                       tw, psiw, zw, mono, out, n);
     return hipGetLastError();
 }
+#endif
 
 }  // namespace fhe
