@@ -14,7 +14,7 @@ if "--max" in argv:
     Bmax = int(argv[i + 1])
     del argv[i:i + 2]
 args = argv
-sizes = [b for b in [1, 16, 64, 128, 256, 320, 384, 512, 640, 768, 1024, 2048, 4096, 8192] if b <= Bmax]
+sizes = [b for b in [1, 16, 64, 128, 256, 320, 384, 512, 640, 768, 1024, 1536, 2048, 2304, 3072, 4096, 8192] if b <= Bmax]
 for kind in (args or ["classic", "multibit"]):
     P = multi_bit_params() if kind == "multibit" else default_params()
     ck, sk = generate_keys(P, seed=1)
