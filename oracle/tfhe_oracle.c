@@ -20,6 +20,12 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#if defined(__AVX2__) && defined(__FMA__)
+#include <immintrin.h>
+#define FHO_HAVE_SIMD 1
+#else
+#define FHO_HAVE_SIMD 0
+#endif
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -313,6 +319,129 @@ void fho_fourier_add_to_poly_r(double* f, double* acc, int reduce) {
 }
 void fho_fourier_add_to_poly(double* f, double* acc) { fho_fourier_add_to_poly_r(f, acc, 1); }
 
+/* ------------------------------------------------------------------ AVX2 forms of the hot loops
+ * The CPU baseline's speed (bench.py cpu_baseline) comes from these: the same operations as the
+ * scalar loops above, element for element -- each scalar fma() an FMA3 vfmadd/vfmsub lane, each
+ * negation a sign-bit xor, each product a vmulpd lane, shuffles only move data -- so every result is
+ * bit-identical (tests/test_oracle.py::test_simd_paths_bit_identical runs both on the same inputs;
+ * fho_set_simd(0) selects the scalar loops).  Two complex values per 256-bit register, interleaved
+ * (re, im) as the arrays hold them.  Classic (grouping 1) blind rotation only. */
+static int g_simd = FHO_HAVE_SIMD;
+void fho_set_simd(int on) { g_simd = on && FHO_HAVE_SIMD; }
+int fho_simd(void) { return g_simd; }
+
+#if FHO_HAVE_SIMD
+static double g_ur[1024], g_ui[1024]; /* untwist factors psi 2^-10, -psi.im 2^-10 (exact scalings) */
+static uint32_t g_brev10[1024];
+static int g_untwist_ready = 0;
+static void untwist_init(void) { /* called before the worker threads start (fho_pbs_batch) */
+    if (g_untwist_ready) return;
+    fho_tables_init();
+    const double inv = 0.0009765625;
+    for (int j = 0; j < 1024; ++j) {
+        g_ur[j] = g_psi[2 * j] * inv;
+        g_ui[j] = -g_psi[2 * j + 1] * inv;
+        g_brev10[j] = bitrev((uint32_t)j, 10);
+    }
+    g_untwist_ready = 1;
+}
+/* (x) * (w) on two complex lanes, as cmul(): (fma(xr, wr, -(xi wi)), fma(xr, wi, xi wr)) */
+static inline __m256d cmul2(__m256d x, __m256d w) {
+    const __m256d neg_re = _mm256_set_pd(0.0, -0.0, 0.0, -0.0);
+    const __m256d t = _mm256_mul_pd(_mm256_permute_pd(x, 0xF), _mm256_permute_pd(w, 0x5)); /* xi wi, xi wr */
+    return _mm256_fmadd_pd(_mm256_movedup_pd(x), w, _mm256_xor_pd(t, neg_re));
+}
+/* k + g w on two complex lanes, as cmul_acc / mac_own_first's second product:
+ * (fma(gr, wr, fma(-gi, wi, kr)), fma(gr, wi, fma(gi, wr, ki))) */
+static inline __m256d cmul_acc2(__m256d k, __m256d g, __m256d w) {
+    const __m256d neg_re = _mm256_set_pd(0.0, -0.0, 0.0, -0.0);
+    const __m256d inner = _mm256_fmadd_pd(_mm256_xor_pd(_mm256_permute_pd(g, 0xF), neg_re), _mm256_permute_pd(w, 0x5), k);
+    return _mm256_fmadd_pd(_mm256_movedup_pd(g), w, inner);
+}
+
+static void fft_forward_twisted_simd(double* x) {
+    fho_tables_init();
+    const __m256d two = _mm256_set1_pd(2.0);
+    for (int st = 0; st < 9; ++st) {
+        const int h = 512 >> st;
+        for (int b = 0; b < (1 << st); ++b) {
+            const double* z = g_zeta + 2 * ((1 << st) + b);
+            const __m256d z0 = _mm256_set1_pd(z[0]), zs = _mm256_set_pd(z[1], -z[1], z[1], -z[1]);
+            for (int j = 0; j < h; j += 2) {
+                double* p = x + 2 * (2 * h * b + j);
+                double* q = p + 2 * h;
+                const __m256d a = _mm256_loadu_pd(p), c = _mm256_loadu_pd(q);
+                /* pr = fma(z0, cr, fma(-z1, ci, ar)), pi = fma(z0, ci, fma(z1, cr, ai)) */
+                const __m256d pv = _mm256_fmadd_pd(z0, c, _mm256_fmadd_pd(zs, _mm256_permute_pd(c, 0x5), a));
+                _mm256_storeu_pd(p, pv);
+                _mm256_storeu_pd(q, _mm256_fmsub_pd(two, a, pv));
+            }
+        }
+    }
+    for (int b = 0; b < 512; ++b) { /* stage 9 (span 1): t = z c, (a + t, a - t) */
+        const double* z = g_zeta + 2 * (512 + b);
+        double* p = x + 4 * b;
+        double tr, ti;
+        cmul(p[2], p[3], z[0], z[1], &tr, &ti);
+        const double ar = p[0], ai = p[1];
+        p[0] = ar + tr; p[1] = ai + ti;
+        p[2] = ar - tr; p[3] = ai - ti;
+    }
+}
+
+static void fft_inverse_simd(double* x) {
+    fho_tables_init();
+    for (int b = 0; b < 512; ++b) { /* stage s = 9 (span 1, twiddle 1) */
+        double* p = x + 4 * b;
+        const double ar = p[0], ai = p[1], cr = p[2], ci = p[3];
+        p[0] = ar + cr; p[1] = ai + ci;
+        p[2] = ar - cr; p[3] = ai - ci;
+    }
+    const __m256d two = _mm256_set1_pd(2.0), neg_im = _mm256_set_pd(-0.0, 0.0, -0.0, 0.0);
+    for (int s = 8; s >= 0; --s) {
+        const int h = 512 >> s;
+        /* j outer: the twiddle pair of (j, j + 1) is the same in every block of the stage */
+        for (int j = 0; j < h; j += 2) {
+            const __m256d w = _mm256_set_m128d(_mm_loadu_pd(g_tw + 2 * ((j + 1) << s)), _mm_loadu_pd(g_tw + 2 * (j << s)));
+            const __m256d ws = _mm256_xor_pd(_mm256_permute_pd(w, 0xF), neg_im), w0 = _mm256_movedup_pd(w);
+            for (int b = 0; b < 1024; b += 2 * h) {
+                double* p = x + 2 * (b + j);
+                double* q = x + 2 * (b + j + h);
+                const __m256d a = _mm256_loadu_pd(p), c = _mm256_loadu_pd(q);
+                /* pr = fma(w0, cr, fma(w1, ci, ar)), pi = fma(w0, ci, fma(-w1, cr, ai)) */
+                const __m256d pv = _mm256_fmadd_pd(w0, c, _mm256_fmadd_pd(ws, _mm256_permute_pd(c, 0x5), a));
+                _mm256_storeu_pd(p, pv);
+                _mm256_storeu_pd(q, _mm256_fmsub_pd(two, a, pv));
+            }
+        }
+    }
+}
+
+static inline __m256d tor_red4(__m256d v) { /* fho_tor_red on 4 lanes */
+    const __m256d r = _mm256_round_pd(_mm256_mul_pd(v, _mm256_set1_pd(0x1p-64)), _MM_FROUND_TO_NEAREST_INT | _MM_FROUND_NO_EXC);
+    return _mm256_fmadd_pd(_mm256_set1_pd(-0x1p64), r, v);
+}
+static void fourier_add_to_poly_simd(double* f, double* acc, int reduce) {
+    untwist_init();
+    fft_inverse_simd(f);
+    const __m256d sign = _mm256_set1_pd(-0.0);
+    for (int j = 0; j < 1024; j += 4) {
+        const __m256d v0 = _mm256_loadu_pd(f + 2 * j), v1 = _mm256_loadu_pd(f + 2 * j + 4);
+        const __m256d fr = _mm256_permute4x64_pd(_mm256_unpacklo_pd(v0, v1), 0xD8);
+        const __m256d fi = _mm256_permute4x64_pd(_mm256_unpackhi_pd(v0, v1), 0xD8);
+        const __m256d ur = _mm256_loadu_pd(g_ur + j), ui = _mm256_loadu_pd(g_ui + j);
+        __m256d lo = _mm256_fmadd_pd(fr, ur, _mm256_fmadd_pd(_mm256_xor_pd(fi, sign), ui, _mm256_loadu_pd(acc + j)));
+        __m256d hi = _mm256_fmadd_pd(fr, ui, _mm256_fmadd_pd(fi, ur, _mm256_loadu_pd(acc + j + 1024)));
+        if (reduce) {
+            lo = tor_red4(lo);
+            hi = tor_red4(hi);
+        }
+        _mm256_storeu_pd(acc + j, lo);
+        _mm256_storeu_pd(acc + j + 1024, hi);
+    }
+}
+#endif
+
 /* ------------------------------------------------------------------ keygen */
 /* r += S * A  (negacyclic, S binary), exact mod 2^64 */
 static void poly_mul_binary_acc(uint64_t* r, const uint64_t* a, const uint64_t* s) {
@@ -441,7 +570,24 @@ void fho_keyswitch(const fho_keys* k, const uint64_t* in, uint64_t* out) {
             if (!d[l]) continue;
             const uint64_t* row = k->ksk + ((size_t)j * L + l) * (n + 1);
             uint64_t dd = (uint64_t)d[l];
-            for (uint32_t t = 0; t <= n; ++t) out[t] -= dd * row[t];
+            uint32_t t = 0;
+#if FHO_HAVE_SIMD
+            if (g_simd && d[l] >= -4 && d[l] <= 4) {
+                /* |d| <= 4 (base 8, balanced): |d| row by shifts and adds, exact mod 2^64 as dd * row */
+                const int64_t kd = d[l] < 0 ? -d[l] : d[l];
+                for (; t + 4 <= n + 1; t += 4) {
+                    const __m256i r = _mm256_loadu_si256((const __m256i*)(row + t));
+                    __m256i m = r;
+                    if (kd == 2) m = _mm256_slli_epi64(r, 1);
+                    else if (kd == 3) m = _mm256_add_epi64(_mm256_slli_epi64(r, 1), r);
+                    else if (kd == 4) m = _mm256_slli_epi64(r, 2);
+                    __m256i o = _mm256_loadu_si256((const __m256i*)(out + t));
+                    o = d[l] < 0 ? _mm256_add_epi64(o, m) : _mm256_sub_epi64(o, m);
+                    _mm256_storeu_si256((__m256i*)(out + t), o);
+                }
+            }
+#endif
+            for (; t <= n; ++t) out[t] -= dd * row[t];
         }
     }
 }
@@ -494,6 +640,9 @@ static void mac_own_first(const double* D0, const double* D1, const double* kr, 
 void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_t* lut,
                       uint64_t* glwe) {
     const uint32_t n = k->p.n;
+#if FHO_HAVE_SIMD
+    untwist_init();
+#endif
     double* acc0 = (double*)malloc(FHO_N * 8);  /* mask */
     double* acc1 = (double*)malloc(FHO_N * 8);  /* body */
     double* rot = (double*)malloc(FHO_N * 8);
@@ -602,6 +751,64 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
                 for (int j = 0; j < FHO_N; ++j) { acc0[j] = fho_tor_red(acc0[j]); acc1[j] = fho_tor_red(acc1[j]); }
             continue;
         }
+#if FHO_HAVE_SIMD
+        if (g_simd) {
+            /* the same CMUX through the AVX2 loops (bit-identical, see fourier_add_to_poly_simd) */
+            for (int m = 0; m < 2; ++m) {
+                double* acc = m ? acc1 : acc0;
+                double* D = m ? D1 : D0;
+                for (int j = 0; j < FHO_N; ++j) dig[j] = tor_digit(acc[j], down, base, ibase);
+                for (int j = 0; j < 1024; ++j) {
+                    D[2 * j] = dig[j];
+                    D[2 * j + 1] = dig[j + 1024];
+                }
+                fft_forward_twisted_simd(D);
+            }
+            /* e(q) - 1 of this step, once for both outputs, 4 points at a time: the table entries by
+             * gathers, the products as in the scalar loop, i^t as per-lane selects and sign flips */
+            {
+                const __m128i va = _mm_set1_epi32((int)a), m4095 = _mm_set1_epi32(4095);
+                const __m256d one = _mm256_set1_pd(1.0), sign = _mm256_set1_pd(-0.0);
+                const __m256i c1 = _mm256_set1_epi64x(1), c2 = _mm256_set1_epi64x(2);
+                for (int q = 0; q < FHO_HALF; q += 4) {
+                    const __m128i jn = _mm_loadu_si128((const __m128i*)(g_brev10 + q));
+                    const __m128i ib = _mm_and_si128(_mm_mullo_epi32(_mm_add_epi32(_mm_slli_epi32(_mm_and_si128(jn, _mm_set1_epi32(63)), 2), _mm_set1_epi32(1)), va), m4095);
+                    const __m128i iff = _mm_and_si128(_mm_mullo_epi32(_mm_slli_epi32(_mm_and_si128(_mm_srli_epi32(jn, 6), _mm_set1_epi32(3)), 8), va), m4095);
+                    const __m128i tq = _mm_and_si128(_mm_mullo_epi32(_mm_srli_epi32(jn, 8), va), _mm_set1_epi32(3));
+                    const __m128i ib2 = _mm_slli_epi32(ib, 1), if2 = _mm_slli_epi32(iff, 1);
+                    const __m256d b0 = _mm256_i32gather_pd(Ecl, ib2, 8), b1 = _mm256_i32gather_pd(Ecl + 1, ib2, 8);
+                    const __m256d f0 = _mm256_i32gather_pd(Ecl, if2, 8), f1 = _mm256_i32gather_pd(Ecl + 1, if2, 8);
+                    const __m256d er = _mm256_fmadd_pd(b0, f0, _mm256_xor_pd(_mm256_mul_pd(b1, f1), sign));
+                    const __m256d ei = _mm256_fmadd_pd(b0, f1, _mm256_mul_pd(b1, f0));
+                    /* t = 0: (er, ei); 1: (-ei, er); 2: (-er, -ei); 3: (ei, -er) */
+                    const __m256i t64 = _mm256_cvtepi32_epi64(tq);
+                    const __m256d odd = _mm256_castsi256_pd(_mm256_cmpeq_epi64(_mm256_and_si256(t64, c1), c1));
+                    const __m256d neg_x = _mm256_castsi256_pd(_mm256_cmpeq_epi64(_mm256_and_si256(_mm256_add_epi64(t64, c1), c2), c2));
+                    const __m256d neg_y = _mm256_castsi256_pd(_mm256_cmpeq_epi64(_mm256_and_si256(t64, c2), c2));
+                    __m256d x = _mm256_blendv_pd(er, ei, odd), y = _mm256_blendv_pd(ei, er, odd);
+                    x = _mm256_sub_pd(_mm256_xor_pd(x, _mm256_and_pd(neg_x, sign)), one);
+                    y = _mm256_xor_pd(y, _mm256_and_pd(neg_y, sign));
+                    const __m256d lo = _mm256_unpacklo_pd(x, y), hi = _mm256_unpackhi_pd(x, y); /* x0 y0 x2 y2 | x1 y1 x3 y3 */
+                    _mm256_storeu_pd(rot + 2 * q, _mm256_permute2f128_pd(lo, hi, 0x20));
+                    _mm256_storeu_pd(rot + 2 * q + 4, _mm256_permute2f128_pd(lo, hi, 0x31));
+                }
+            }
+            const double* bs = k->bsk_f + (size_t)i * 4 * FHO_HALF * 2;
+            for (int w = 0; w < 2; ++w) {
+                const double* Bn = bs + (w * 2 + w) * FHO_HALF * 2;       /* row w (own digit), poly w */
+                const double* Bx = bs + ((1 - w) * 2 + w) * FHO_HALF * 2; /* row 1 - w, poly w */
+                const double* Dn = w ? D1 : D0;
+                const double* Dx = w ? D0 : D1;
+                for (int q = 0; q < FHO_HALF; q += 2) {
+                    const __m256d pv = cmul2(_mm256_loadu_pd(Dn + 2 * q), _mm256_loadu_pd(Bn + 2 * q));
+                    const __m256d o = cmul_acc2(pv, _mm256_loadu_pd(Dx + 2 * q), _mm256_loadu_pd(Bx + 2 * q));
+                    _mm256_storeu_pd(O + 2 * q, cmul2(o, _mm256_loadu_pd(rot + 2 * q)));
+                }
+                fourier_add_to_poly_simd(O, w ? acc1 : acc0, reduce);
+            }
+            continue;
+        }
+#endif
         for (int m = 0; m < 2; ++m) {
             double* acc = m ? acc1 : acc0;
             for (int j = 0; j < FHO_N; ++j) dig[j] = tor_digit(acc[j], down, base, ibase);
@@ -657,6 +864,10 @@ void fho_pbs(const fho_keys* k, const uint64_t* in, const uint64_t* lut, uint64_
 
 void fho_pbs_batch(const fho_keys* k, const uint64_t* in, size_t count, const uint64_t* luts,
                    const uint32_t* lut_index, uint64_t* out, int threads) {
+    fho_tables_init(); /* the shared tables, before the worker threads read them */
+#if FHO_HAVE_SIMD
+    untwist_init();
+#endif
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 1)
