@@ -5,10 +5,10 @@
 # the validating deserializers (corrupted / truncated / oversized inputs), key generation and
 # encryption, the BIP-340 signer and the level scheduler -- against it.  CPU only: no GPU, and
 # GPU-side sanitizers are not available on the GPU pool.
-# Usage: tools/sanitize_host.sh [log]   (default log: profiles/r2/sanitize_host_r2.log)
+# Usage: tools/sanitize_host.sh [log]   (default log: profiles/r3/sanitize_host_r3.log)
 set -euo pipefail
 cd "$(dirname "$0")/.."
-LOG=${1:-profiles/r2/sanitize_host_r2.log}
+LOG=${1:-profiles/r3/sanitize_host_r3.log}
 mkdir -p "$(dirname "$LOG")"
 make -C fhe-sign_amd asan -j8 >/dev/null
 RT=$(/opt/rocm/lib/llvm/bin/clang -print-file-name=libclang_rt.asan-x86_64.so)
