@@ -120,6 +120,27 @@ int fhe_radix_trivial(fhe_ctx* c, const uint64_t* words, uint32_t bits, fhe_radi
     return FHE_OK;
 }
 
+// the decoded values of a radix's blocks (carry bits included): trivial blocks as they are, the
+// others downloaded together and decrypted on the host
+static std::vector<uint32_t> decrypt_blocks(fhe_ctx* c, const fhe_client_key* ck, const Radix& r) {
+    std::vector<uint32_t> vals(r.nblocks());
+    std::vector<const Block*> enc;
+    for (uint32_t k = 0; k < r.nblocks(); ++k) {
+        if (r.blocks[k].trivial())
+            vals[k] = r.blocks[k].value;
+        else
+            enc.push_back(&r.blocks[k]);
+    }
+    std::vector<uint64_t> cts(enc.size() * kBigCt);
+    c->engine->download_many(enc, cts.data());
+    for (size_t i = 0, k = 0; k < r.nblocks(); ++k)
+        if (!r.blocks[k].trivial()) {
+            vals[k] = (uint32_t)decode_block(ck->params, decrypt_phase_big(ck, cts.data() + i * kBigCt));
+            ++i;
+        }
+    return vals;
+}
+
 int fhe_radix_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_radix* x, uint64_t* words, size_t nwords) {
     int rc = need_engine(c);
     if (rc) return rc;
@@ -129,19 +150,9 @@ int fhe_radix_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_radix* x, 
     }
     return guarded([&] {
         std::memset(words, 0, nwords * 8);
-        std::vector<uint64_t> ct(kBigCt);
         // value = sum v_k 4^k mod 2^bits (v_k incl. carry bits)
         unsigned __int128 lo = 0;  // bits < 128 handled by accumulating per block
-        std::vector<uint32_t> vals(x->r.nblocks());
-        for (uint32_t k = 0; k < x->r.nblocks(); ++k) {
-            const Block& b = x->r.blocks[k];
-            if (b.trivial())
-                vals[k] = b.value;
-            else {
-                c->engine->download(b, ct.data());
-                vals[k] = (uint32_t)decode_block(ck->params, decrypt_phase_big(ck, ct.data()));
-            }
-        }
+        const std::vector<uint32_t> vals = decrypt_blocks(c, ck, x->r);
         // big-integer accumulate in 64-bit words
         std::vector<uint64_t> acc((x->bits + 63) / 64 + 2, 0);
         for (uint32_t k = 0; k < vals.size(); ++k) {
@@ -190,6 +201,7 @@ int fhe_radix_export(fhe_ctx* c, const fhe_radix* x, uint64_t* cts, size_t nword
     if (rc) return rc;
     if (!x || !cts || nwords < (size_t)x->r.nblocks() * kBigCt) return FHE_ERR_INVALID;
     return guarded([&] {
+        std::vector<const Block*> enc;
         for (uint32_t k = 0; k < x->r.nblocks(); ++k) {
             uint64_t* ct = cts + (size_t)k * kBigCt;
             const Block& b = x->r.blocks[k];
@@ -197,9 +209,13 @@ int fhe_radix_export(fhe_ctx* c, const fhe_radix* x, uint64_t* cts, size_t nword
                 std::memset(ct, 0, kBigCt * 8);
                 ct[kBigDim] = (uint64_t)b.value * c->p.delta();
             } else {
-                c->engine->download(b, ct);
+                enc.push_back(&b);
             }
         }
+        std::vector<uint64_t> buf(enc.size() * kBigCt);
+        c->engine->download_many(enc, buf.data());
+        for (size_t i = 0, k = 0; k < x->r.nblocks(); ++k)
+            if (!x->r.blocks[k].trivial()) std::memcpy(cts + (size_t)k * kBigCt, buf.data() + kBigCt * i++, kBigCt * 8);
         return FHE_OK;
     });
 }
@@ -473,16 +489,18 @@ int fhe_biguint_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_biguint*
         set_error("limb buffer too small");
         return FHE_ERR_INVALID;
     }
-    for (size_t i = 0; i < *n; ++i) {
-        fhe_radix tmp;
-        tmp.r = x->v.digits[i];
-        tmp.bits = 32;
-        uint64_t w = 0;
-        rc = fhe_radix_decrypt(c, ck, &tmp, &w, 1);
-        if (rc) return rc;
-        limbs[i] = (uint32_t)w;
-    }
-    return FHE_OK;
+    return guarded([&] {
+        // every limb's blocks in one download: limb = sum v_k 4^k mod 2^32
+        Radix all;
+        for (size_t i = 0; i < *n; ++i) all.blocks.insert(all.blocks.end(), x->v.digits[i].blocks.begin(), x->v.digits[i].blocks.end());
+        const std::vector<uint32_t> vals = decrypt_blocks(c, ck, all);
+        for (size_t i = 0, k = 0; i < *n; ++i) {
+            uint64_t w = 0;
+            for (uint32_t j = 0; j < x->v.digits[i].nblocks(); ++j, ++k) w += (uint64_t)vals[k] << (2 * j);
+            limbs[i] = (uint32_t)w;
+        }
+        return FHE_OK;
+    });
 }
 
 int fhe_biguint_len(const fhe_biguint* x, size_t* n) {

@@ -121,16 +121,23 @@ uint64_t reachable(const std::vector<Term>& terms, int64_t cst, bool* ok) {
     }
     uint64_t set = 1ull << cst;
     for (const Term& t : terms) {
+        // the set shifted by coef * x for every x in [0, degree]; a bit leaving [0, 64) is an input
+        // outside the message space
         uint64_t nxt = 0;
-        for (int v = 0; v < 64; ++v) {
-            if (!(set >> v & 1)) continue;
-            for (uint32_t x = 0; x <= t.b.degree; ++x) {
-                int64_t r = v + (int64_t)t.coef * x;
-                if (r < 0 || r >= 64) {
+        for (uint32_t x = 0; x <= t.b.degree; ++x) {
+            const int64_t sh = (int64_t)t.coef * x;
+            if (sh >= 0) {
+                if (sh >= 64 || (sh > 0 && (set >> (64 - sh)) != 0)) {
                     *ok = false;
                     return 0;
                 }
-                nxt |= 1ull << r;
+                nxt |= set << sh;
+            } else {
+                if (-sh >= 64 || (set & ((1ull << -sh) - 1)) != 0) {
+                    *ok = false;
+                    return 0;
+                }
+                nxt |= set >> -sh;
             }
         }
         set = nxt;
@@ -500,6 +507,30 @@ void Engine::download(const Block& b, uint64_t* ct) {
     engine_check(!b.trivial() && !b.lazy(), "download of a trivial or lazy block");
     flush();
     hip_check(hipMemcpyAsync(ct, b.slot->p, kBigCt * 8, hipMemcpyDeviceToHost, ctx_->stream), "download");
+    if (ctx_->wait_stream("download") != FHE_OK) throw std::runtime_error(last_error());
+}
+
+void Engine::download_many(const std::vector<const Block*>& blocks, uint64_t* cts) {
+    const size_t n = blocks.size();
+    if (n == 0) return;
+    if (n == 1) return download(*blocks[0], cts);
+    flush();
+    const size_t words = n * kBigCt + n;  // gathered ciphertexts, then the slot pointers
+    if (words > up_cap_) {
+        hip_check(hipStreamSynchronize(ctx_->stream), "download sync");
+        if (d_up_) hip_check(hipFree(d_up_), "hipFree");
+        hip_check(hipMalloc(&d_up_, words * 8), "hipMalloc download");
+        up_cap_ = words;
+    }
+    std::vector<const uint64_t*> src(n);
+    for (size_t i = 0; i < n; ++i) {
+        engine_check(blocks[i]->slot != nullptr && !blocks[i]->lazy(), "download of a trivial or lazy block");
+        src[i] = blocks[i]->slot->p;
+    }
+    const uint64_t** d_src = reinterpret_cast<const uint64_t**>(d_up_ + n * kBigCt);
+    hip_check(hipMemcpyAsync(d_src, src.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice, ctx_->stream), "download");
+    hip_check(launch_gather_blocks(d_src, d_up_, (int)n, ctx_->stream), "download gather");
+    hip_check(hipMemcpyAsync(cts, d_up_, n * kBigCt * 8, hipMemcpyDeviceToHost, ctx_->stream), "download");
     if (ctx_->wait_stream("download") != FHE_OK) throw std::runtime_error(last_error());
 }
 

@@ -115,6 +115,9 @@ public:
     // n client-encrypted blocks (contiguous big LWEs): one copy + one scatter into their slots
     Blocks upload_many(const uint64_t* cts, size_t n, uint32_t degree);
     void download(const Block& b, uint64_t* ct);
+    // the slot blocks' ciphertexts -> host, contiguous (one gather + one copy + one wait instead of a
+    // round trip per block: the decryption of a 256-bit result is 128-144 blocks)
+    void download_many(const std::vector<const Block*>& blocks, uint64_t* cts);
     // n big LWEs contiguous in device memory -> fresh slots (one scatter); degree/noise set by the caller
     Blocks adopt_device(const uint64_t* d_cts, size_t n);
     // the slot blocks' ciphertexts -> contiguous device buffer (one gather; flushes first)
