@@ -1,6 +1,8 @@
-# Same-box A/B of throughput-kernel variants (build_variants/*: tools/build_variant.sh); output gpurun_out/stag_ab.txt
+# Same-box A/B of latency-kernel variants (build_variants/*: tools/build_variant.sh) + the variant's
+# bit-exactness (tests/test_pbs_gpu.py against its library); output gpurun_out/psync_ab.txt
 set -o pipefail
-O=gpurun_out/stag_ab.txt
+O=gpurun_out/psync_ab.txt
+FHE_ROCM_LIB=$PWD/build_variants/psync/lib/libfhe_rocm.so timeout -k 10 300 python -u -m pytest tests/test_pbs_gpu.py -x -q --timeout 120 --timeout-method thread >> $O 2>&1 || exit 3
 for r in 1 2; do
-for B in 768 1536 5200 32768; do for v in fhe-sign_amd build_variants/stag4 build_variants/stag8; do R=5; [ $B = 32768 ] && R=2; timeout -k 10 150 python3 tools/variant_probe.py $v $B $R >> $O 2>&1 || exit 2; done; done
+for B in 1 256; do for v in fhe-sign_amd build_variants/psync; do timeout -k 10 150 python3 tools/variant_probe.py $v $B 5 >> $O 2>&1 || exit 2; done; done
 done
