@@ -65,6 +65,27 @@ def test_pbs_bit_exact_vs_oracle(env):
         assert ok.decrypt(gpu[i]) == tables[lut_of[i]][msgs[i]]
 
 
+def test_full_bench_batch_sampled_vs_oracle(env):
+    """bench.py's workload at its full size (BASELINE configs[1]: one level of 32768 blocks, the
+    256-bit mul's widest): 32768 distinct encryptions through 5 LUTs in one launch of the throughput
+    kernel; a seeded sample of 48 outputs bit-exact against the oracle, every 37th decrypting to f(m)."""
+    ck, _, ok, ctx = env
+    tables = _luts()
+    ids = np.array([ctx.lut(t) for t in tables], np.uint32)
+    B = 32768
+    r = ok.rng(777)
+    cts = np.stack([ok.encrypt(r, i % 16) for i in range(B)])
+    lut_of = np.arange(B) % len(tables)
+    gpu = ctx.pbs(cts, ids[lut_of])
+    for i in range(0, B, 37):
+        assert ok.decrypt(gpu[i]) == tables[lut_of[i]][i % 16], f"block {i}"
+    pick = np.sort(np.random.default_rng(5).choice(B, 48, replace=False))
+    luts = np.stack([ok.make_lut(t) for t in tables])
+    ref = ok.pbs_batch(np.ascontiguousarray(cts[pick]), luts, lut_of[pick].astype(np.uint32))
+    for k, i in enumerate(pick):
+        assert np.array_equal(gpu[i], ref[k]), f"ciphertext {i} differs"
+
+
 def test_pbs_chained_and_large_batch(env):
     """Repeated bootstrapping keeps decrypting correctly (noise is refreshed), and a batch larger
     than the chip's workgroup capacity (4096 ciphertexts) is handled."""
