@@ -14,6 +14,8 @@
 //   C  regs (b5,b4)   idx = 64 (L>>2) + 16 r + 4 (L&3) + q     stages 4,5
 //   D  regs (b3,b2)   idx = 16 L + 4 r + q                     stages 6,7
 //   E  regs (b1,b0)   idx = 256 q + 4 L + r  (= the BSK layout R = 4q + r)  stages 8,9
+//      (classic: lane L of wave (p, q) holds polynomial L >> 5 at lane Lp = 32 p + (L & 31)'s points,
+//      so each point of each polynomial is transformed once; multi-bit: both polynomials at lane L's)
 // A<->B<->C<->D keep (b1,b0) = q fixed, so those exchanges are wave-private transposes of register
 // bits with lane bits: v_permlane32_swap / v_permlane16_swap for lane bits 5,4, bank-masked DPP
 // moves for lane bits 3,2, and a wave-private LDS region (no barrier, conflict-free XOR map) for lane
@@ -191,6 +193,8 @@ FHE_DEV void dif2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
     dif(x[0], x[1], tw2);
     dif(x[2], x[3], tw2);
 }
+// (A, B) -> ((A.lo, B.lo), (A.hi, B.hi)) over the lane halves: v_permlane32_swap per dword
+FHE_DEV void pair_swap32(cplx& A, cplx& B) { xpose_permlane<5>(A, B); }
 FHE_DEV void dit2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
     dit(x[0], x[1], conj_(tw2));
     dit(x[2], x[3], conj_(tw2));
@@ -240,12 +244,15 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk);  // key slices: per-step bases in SGPRs
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
 
+    // G = 1, phase E: lane L of wave (p, q) takes polynomial hL = L >> 5 at the points of lane
+    // Lp = 32 p + (L & 31) -- each point of each polynomial once in the workgroup (no recomputation)
+    const int hL = L >> 5, Lp = 32 * p + (L & 31), tE1 = 64 * q + Lp;
     // loop-invariant per-thread twiddles and twist factors (held in registers)
     cplx T[12], PS[4], ZT[10];
 #pragma unroll
     for (int s = 0; s < 12; ++s) T[s] = tw[s * 256 + t];
 #pragma unroll
-    for (int s = 0; s < 10; ++s) ZT[s] = zw[s * 256 + t];
+    for (int s = 0; s < 10; ++s) ZT[s] = zw[s * 256 + (G == 1 && s >= 8 ? tE1 : t)];
 #pragma unroll
     for (int r = 0; r < 4; ++r) PS[r] = make_double2(psiw[r * 256 + t].x * 0x1p-51, -psiw[r * 256 + t].y * 0x1p-51);
 
@@ -276,6 +283,10 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     const uint32_t j0 = __builtin_bitreverse32((uint32_t)(256 * q + 4 * L)) >> 22;
     const uint32_t c4 = 4u * (j0 & 63u) + 1u;
     const int fsel = (int)((j0 >> 6) & 3u);
+    const int xEp = fx(256 * q + 4 * Lp);  // G = 1: this lane's phase-E points
+    const int fselp = (int)(((__builtin_bitreverse32((uint32_t)(256 * q + 4 * Lp)) >> 22) >> 6) & 3u);
+    // G = 1: key slices at the points the MAC pairs take (rows 0, 1 of both columns; see phase E)
+    const uint32_t kvo = (uint32_t)(((4 * q + hL) * 64 + Lp) * 16);
 
     // modulus-switched mask of the current step and the next one (G = 1: a_i, a_i+1; G = 2: the pairs)
     uint32_t a_next = modswitch_2n(a_ct[0]);
@@ -351,17 +362,20 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         }
         a_next1 = modswitch_2n(a_ct[i + 2 <= n ? i + 2 : n]);
 
-        // BSK slice for this iteration (issued early; consumed after the forward FFT)
+        // BSK slice for this iteration (issued early; consumed after the forward FFT): for MAC pair
+        // k (points 2k, 2k + 1; this lane's point 2k + hL) the rows 0, 1 of column 0 (Kown[2k],
+        // Koth[2k]) and of column 1 (Kown[2k + 1], Koth[2k + 1])
         {
-            const bptr b0{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((i * 2 + p) * 2 + p) * 16 + 4 * q) * 1024u};  // own digit's row
-            const bptr b1{bsk_rs, 16u * (uint32_t)L, (uint32_t)(((i * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 1024u};  // other row
+            const bptr kb{bsk_rs, kvo, (uint32_t)i * 65536u};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                Kown[r] = b0[r * 64];
-                Koth[r] = b1[r * 64];
+            for (int k = 0; k < 2; ++k) {
+                Kown[2 * k] = kb[0 * 1024 + 128 * k];      // row 0, column 0
+                Koth[2 * k] = kb[2 * 1024 + 128 * k];      // row 1, column 0
+                Kown[2 * k + 1] = kb[3 * 1024 + 128 * k];  // row 1, column 1
+                Koth[2 * k + 1] = kb[1 * 1024 + 128 * k];  // row 0, column 1
             }
         }
-        e1 = cmul(s_mono[(i & 1) * 256 + q * 64 + L], s_monf[(i & 1) * 64 + fsel]);
+        e1 = cmul(s_mono[(i & 1) * 256 + q * 64 + Lp], s_monf[(i & 1) * 64 + fselp]);
         WSTAMP(1);
         WSTAMP(2);
         WSTAMP(3);
@@ -432,32 +446,50 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         if constexpr (G == 1) WSTAMP(4);
         __syncthreads();
         if constexpr (G == 1) WSTAMP(5);
-        // phase E reads both polynomials' regions: stages 8, 9 of the other polynomial's digits are
-        // recomputed here (identical operations to its own waves') instead of swapping the results
-        // through LDS -- one barrier and one exchange less per CMUX
-        cplx y[4];
-        {
+        // phase E reads both polynomials' regions, so the MAC needs no digit-swap exchange (one barrier
+        // less per CMUX).  Classic: each point of each polynomial is transformed by one lane (below);
+        // multi-bit: every wave transforms both polynomials at its points (the other polynomial's
+        // stages 8, 9 recomputed -- identical operations to its own waves')
+        if constexpr (G == 1) {
+            // phase E once per point and polynomial: lanes hL = 0 / 1 hold polynomial 0 / 1 at the
+            // points of lane Lp (stages 8, 9 on registers); v_permlane32_swap of registers 2k, 2k + 1
+            // then gives every lane both polynomials' digits at its point 2k + hL (A: polynomial 0,
+            // B: polynomial 1), the MAC forms both outputs there, the (e - 1) factor is shared (the
+            // upper half's point is i^(2a) = (-1)^a times the lower's), and a second swap restores
+            // the layout (register r = point r of polynomial hL)
+            const cplx* crw = s_cross[hL];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[r] = crw[xEp ^ fx(r)];
+            ct2_last(x, ZT[8], ZT[9]);
+            const uint32_t sg = (uint32_t)(hL & mB[0] & 1u) << 31;
+            const cplx el = make_double2(neg_if(e1.x, sg), neg_if(e1.y, sg));
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                cplx A = x[2 * k], B = x[2 * k + 1];
+                pair_swap32(A, B);
+                cplx o0 = mac2(A, Kown[2 * k], B, Koth[2 * k]);          // polynomial 0
+                cplx o1 = mac2(B, Kown[2 * k + 1], A, Koth[2 * k + 1]);  // polynomial 1
+                const cplx wv = k == 0 ? make_double2(el.x - 1.0, el.y) : turn_sel_m1(el, mB[0]);
+                o0 = cmul(o0, wv);
+                o1 = cmul(o1, wv);
+                pair_swap32(o0, o1);
+                x[2 * k] = o0;
+                x[2 * k + 1] = o1;
+            }
+        } else {
+            cplx y[4];
             const cplx* cross_other = s_cross[p ^ 1];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 x[r] = cross[xE ^ fx(r)];
                 y[r] = cross_other[xE ^ fx(r)];
             }
-        }
-        WP_A();
-        ct2_last(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
-        ct2_last(y, ZT[8], ZT[9]);
-
-        // ---- pointwise MAC (own digit x row p, then other digit x row 1 - p accumulated)
+            WP_A();
+            ct2_last(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
+            ct2_last(y, ZT[8], ZT[9]);
+            // ---- pointwise MAC (own digit x row p, then other digit x row 1 - p accumulated)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], Kown[r], y[r], Koth[r]);
-        if constexpr (G == 1) {  // (X^a - 1): point r = j0 + 256 bitrev2(r), e - 1 as in the multi-bit bundle
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const cplx wv = r == 0 ? make_double2(e1.x - 1.0, e1.y)
-                                       : turn_sel_m1(e1, (2 * (r & 1) + (r >> 1)) * mB[0]);
-                x[r] = cmul(x[r], wv);
-            }
+            for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], Kown[r], y[r], Koth[r]);
         }
         if constexpr (G == 1) WSTAMP(6);
 
@@ -472,8 +504,14 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         }
         // through a region of its own: the other polynomial's waves may still be reading `cross`
         cplx* inv = s_inv[p];
+        if constexpr (G == 1) {
+            cplx* invw = s_inv[hL];  // every wave holds points of both polynomials
 #pragma unroll
-        for (int r = 0; r < 4; ++r) inv[xE ^ fx(r)] = x[r];
+            for (int r = 0; r < 4; ++r) invw[xEp ^ fx(r)] = x[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) inv[xE ^ fx(r)] = x[r];
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the monomial DMA
         if constexpr (G == 1) WSTAMP(7);
         __syncthreads();
@@ -533,20 +571,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     }
 }
 
-// WIDE_INST: which instances this object holds.  The product build compiles this file twice
-// (Makefile): WIDE_INST = 1, the classic kernel alone, under the max-ilp machine scheduler
-// (-amdgpu-sched-strategy=max-ilp: B = 1 2.18 -> 2.10 ms, B = 256 2.52 -> 2.46 ms per level, same
-// box, profiles/r3/wide_sched_ab_r3m.txt), and WIDE_INST = 2, the multi-bit kernel under the default
-// one (max-ilp serialises its key-bundle loads: 1.60 -> 3.63 ms) plus the dispatcher.  0 (variant
-// and diagnostic builds): both in one object.
-#ifndef WIDE_INST
-#define WIDE_INST 0
-#endif
-hipError_t launch_blind_rotate_wide_g1(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
-                                       const uint64_t* luts, const double2* bsk, const double2* tw,
-                                       const double2* psiw, const double2* zw, const double2* mono, uint64_t* out,
-                                       int count, int n, hipStream_t s);
-
 #ifdef WIDE_STAMPS
 }  // namespace fhe
 extern "C" int fhe_debug_wide_stamps(uint64_t* out, size_t n) {
@@ -558,28 +582,18 @@ extern "C" int fhe_debug_wide_stamps(uint64_t* out, size_t n) {
 namespace fhe {
 #endif
 
-#if WIDE_INST != 2
-hipError_t launch_blind_rotate_wide_g1(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
-                                       const uint64_t* luts, const double2* bsk, const double2* tw,
-                                       const double2* psiw, const double2* zw, const double2* mono, uint64_t* out,
-                                       int count, int n, hipStream_t s) {
-    hipLaunchKernelGGL(k_blind_rotate_wide<1>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk,
-                       tw, psiw, zw, mono, out, n);
-    return hipGetLastError();
-}
-#endif
-#if WIDE_INST != 1
 hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const double2* bsk, const double2* tw, const double2* psiw,
                                     const double2* zw, const double2* mono, int grouping, uint64_t* out, int count,
                                     int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    if (grouping != 2)
-        return launch_blind_rotate_wide_g1(ms, ms_stride, desc, lut_idx, luts, bsk, tw, psiw, zw, mono, out, count, n, s);
-    hipLaunchKernelGGL(k_blind_rotate_wide<2>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk,
-                       tw, psiw, zw, mono, out, n);
+    if (grouping == 2)
+        hipLaunchKernelGGL(k_blind_rotate_wide<2>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts,
+                           bsk, tw, psiw, zw, mono, out, n);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_wide<1>, dim3(count), dim3(512), 0, s, ms, ms_stride, desc, lut_idx, luts,
+                           bsk, tw, psiw, zw, mono, out, n);
     return hipGetLastError();
 }
-#endif
 
 }  // namespace fhe

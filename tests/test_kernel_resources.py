@@ -16,11 +16,6 @@ CSRC = os.path.join(ROOT, "fhe-sign_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
-# the product build's per-object flags (fhe-sign_amd/Makefile: br_wide.hip is compiled twice)
-WIDE_G1 = ["-DWIDE_INST=1", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-WIDE_G2 = ["-DWIDE_INST=2"]
-
-
 def descriptors(src, tmp_path, flags=()):
     out = tmp_path / (os.path.basename(src) + ".s")
     subprocess.run([HIPCC, "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "--cuda-device-only",
@@ -36,8 +31,8 @@ def descriptors(src, tmp_path, flags=()):
 
 @pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src,flags,kernel,lds_per_cu_ok,max_regs,max_scratch", [
-    ("br_wide.hip", WIDE_G1, "k_blind_rotate_wideILi1", 1, 256, 0),  # one 8-wave workgroup per CU (classic)
-    ("br_wide.hip", WIDE_G2, "k_blind_rotate_wideILi2", 1, 256, 0),  # the same, multi-bit
+    ("br_wide.hip", (), "k_blind_rotate_wideILi1", 1, 256, 0),  # one 8-wave workgroup per CU (classic)
+    ("br_wide.hip", (), "k_blind_rotate_wideILi2", 1, 256, 0),  # the same, multi-bit
     ("br_quad.hip", (), "k_blind_rotate_quadILi1", 3, 168, 0),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
     ("br_quad.hip", (), "k_blind_rotate_quadILi2", 2, 256, 0),  # multi-bit: 2 per CU, 2 waves/SIMD, deeper BSK ring
 ])

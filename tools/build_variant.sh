@@ -22,8 +22,7 @@ cp "$SRC" $VS
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off ${EXTRA_FLAGS:-} -I$ROOT/include ${HDR:+-I$HDR} -I$PKG/csrc --offload-arch=gfx950 \
     -c -o $OUT/obj/$OBJ.o $VS
 rm -f $VS
-# a br_wide variant holds both latency-kernel instances (WIDE_INST = 0): drop the product's split object too
-OBJS=$(ls $PKG/build/*.o | grep -v "/$OBJ.o" | { [ $OBJ = br_wide ] && grep -v "/br_wide_g1.o" || cat; })
+OBJS=$(ls $PKG/build/*.o | grep -v "/$OBJ.o")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/lib/libfhe_rocm.so $OUT/obj/$OBJ.o $OBJS -lpthread -L/opt/rocm/lib -lrccl
 rm -rf $OUT/fhe_sign && cp -r $PKG/fhe_sign $OUT/fhe_sign
 echo "built $OUT"
