@@ -3,7 +3,7 @@ variant build: lane 0 of every wave records s_memtime at the phase boundaries of
 iterations.  usage (GPU box): python3 tools/wide_stamps.py [B ...]   (build: tools/wide_stamps.sh)
 Phases (stamp k -> k+1; factored CMUX, round 3): 0 top -> 1 digits (with the deferred reduction),
 monomial DMA, key loads issued, monomial factor -> (2, 3 empty) -> 4 forward A..D + cross store ->
-5 barrier X -> 6 phase E (both polynomials) + MAC + (X^a - 1) -> 7 inverse first stage + store ->
+5 barrier X -> 6 phase E (each point and polynomial once, paired swaps) + MAC + (X^a - 1) -> 7 inverse first stage + store ->
 8 barrier Y -> 9 inverse D..A + accumulate."""
 import ctypes as C
 import os
