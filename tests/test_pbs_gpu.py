@@ -135,6 +135,37 @@ def test_wide_and_quad_kernels_bit_identical(env):
     assert np.array_equal(wide[:6], ref)
 
 
+def test_zero_and_sparse_masks_both_kernels(env):
+    """Ciphertexts whose modulus-switched mask is 0 at every key bit (trivial encryptions: mask 0,
+    body m delta -- every CMUX is an a = 0 step, the kernels run it with e - 1 = 0 while the oracle
+    skips it, reducing on the same schedule) and at half of them (a random encryption with every
+    other mask word of the big LWE zeroed): both blind-rotate kernels equal the oracle word for word,
+    and the trivial ones decrypt to f(m)."""
+    _, _, ok, ctx = env
+    tables = _luts()
+    ids = np.array([ctx.lut(t) for t in tables], np.uint32)
+    luts = np.stack([ok.make_lut(t) for t in tables])
+    delta = ok.delta()
+    triv = np.zeros((16, 2049), np.uint64)
+    triv[:, 2048] = (np.arange(16, dtype=np.uint64) * np.uint64(delta))
+    r = ok.rng(4711)
+    sparse = np.stack([ok.encrypt(r, m) for m in range(8)])
+    sparse[:, 0:2048:2] = 0
+    cts = np.ascontiguousarray(np.concatenate([triv, sparse]))
+    lut_of = (np.arange(len(cts)) % len(tables)).astype(np.uint32)
+    ref = ok.pbs_batch(cts, luts, lut_of)
+    try:
+        for thr in (0, 1 << 30):  # throughput kernel, latency kernel
+            ctx.set_wide_threshold(thr)
+            got = ctx.pbs(cts, ids[lut_of])
+            bad = [i for i in range(len(cts)) if not np.array_equal(got[i], ref[i])]
+            assert not bad, f"threshold {thr}: ciphertexts {bad} differ from the oracle"
+    finally:
+        ctx.set_wide_threshold(256)
+    for m in range(16):
+        assert ok.decrypt(ref[m]) == tables[lut_of[m]][m]
+
+
 def test_quad_kernel_ragged_batches_and_retired_kernels(env):
     """The throughput kernel at ragged batches (1, 2, 3, 37) with every LUT gives the latency kernel's
     and the oracle's words; the retired blind-rotate kernels (0: round-1 2-wave, 2: the pair kernel)
