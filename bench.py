@@ -126,10 +126,10 @@ def cpu_baseline(seed, target_s, op_levels=None):
     ok.pbs_batch(pool, lut, np.zeros(count, np.uint32), threads)
     dt = time.perf_counter() - t0
     res = {"value": count / dt, "unit": "PBS/s", "cores": threads, "kind": "port", **info,
-           "simd": bool(oracle.load().fho_simd()),
+           "simd": {0: "scalar", 1: "avx2", 2: "avx512"}[int(oracle.load().fho_simd())],
            "sample": f"{count} PBS (KS+BR+SE, same params/keys shape) with the C oracle (bit-exact "
-                     f"restatement; its blind rotation and keyswitch loops in AVX2, bit-identical to "
-                     f"their scalar form -- not tfhe-rs's FFT), OpenMP {threads} threads = every CPU of "
+                     f"restatement; its blind rotation and keyswitch loops in AVX2 / AVX-512, bit-identical "
+                     f"to their scalar form -- not tfhe-rs's FFT), OpenMP {threads} threads = every CPU of "
                      f"this process's affinity/cgroup share, {dt:.1f} s"}
     t_round = dt / rounds  # one round = `threads` bootstraps in parallel
 

@@ -326,15 +326,31 @@ void fho_fourier_add_to_poly(double* f, double* acc) { fho_fourier_add_to_poly_r
  * bit-identical (tests/test_oracle.py::test_simd_paths_bit_identical runs both on the same inputs;
  * fho_set_simd(0) selects the scalar loops).  Two complex values per 256-bit register, interleaved
  * (re, im) as the arrays hold them.  Classic (grouping 1) blind rotation only. */
-static int g_simd = FHO_HAVE_SIMD;
-void fho_set_simd(int on) { g_simd = on && FHO_HAVE_SIMD; }
-int fho_simd(void) { return g_simd; }
+static int g_simd = -1; /* 0 scalar, 1 AVX2, 2 AVX-512 (f, dq) -- default: the best the CPU has */
+static int simd_max(void) {
+#if FHO_HAVE_SIMD && defined(__GNUC__)
+    __builtin_cpu_init();
+    return (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq")) ? 2 : 1;
+#else
+    return 0;
+#endif
+}
+static int simd_level(void) {
+    if (g_simd < 0) g_simd = simd_max();
+    return g_simd;
+}
+void fho_set_simd(int level) {
+    const int m = simd_max();
+    g_simd = level < 0 ? m : (level > m ? m : level);
+}
+int fho_simd(void) { return simd_level(); }
 
 #if FHO_HAVE_SIMD
 static double g_ur[1024], g_ui[1024]; /* untwist factors psi 2^-10, -psi.im 2^-10 (exact scalings) */
 static uint32_t g_brev10[1024];
 static int g_untwist_ready = 0;
 static void untwist_init(void) { /* called before the worker threads start (fho_pbs_batch) */
+    (void)simd_level();
     if (g_untwist_ready) return;
     fho_tables_init();
     const double inv = 0.0009765625;
@@ -359,11 +375,86 @@ static inline __m256d cmul_acc2(__m256d k, __m256d g, __m256d w) {
     return _mm256_fmadd_pd(_mm256_movedup_pd(g), w, inner);
 }
 
+/* AVX-512 forms (4 complex values per register) of the stages with spans of 4 or more points, the
+ * MAC and the keyswitch row update: the same lanes' operations again, so the same bits */
+#define FHO_T512 __attribute__((target("avx512f,avx512dq")))
+FHO_T512 static void fwd_stage512(double* x, int st) {
+    const int h = 512 >> st;
+    const __m512d two = _mm512_set1_pd(2.0);
+    for (int b = 0; b < (1 << st); ++b) {
+        const double* z = g_zeta + 2 * ((1 << st) + b);
+        const __m512d z0 = _mm512_set1_pd(z[0]);
+        const __m512d zs = _mm512_set_pd(z[1], -z[1], z[1], -z[1], z[1], -z[1], z[1], -z[1]);
+        for (int j = 0; j < h; j += 4) {
+            double* p = x + 2 * (2 * h * b + j);
+            double* q = p + 2 * h;
+            const __m512d a = _mm512_loadu_pd(p), c = _mm512_loadu_pd(q);
+            const __m512d pv = _mm512_fmadd_pd(z0, c, _mm512_fmadd_pd(zs, _mm512_permute_pd(c, 0x55), a));
+            _mm512_storeu_pd(p, pv);
+            _mm512_storeu_pd(q, _mm512_fmsub_pd(two, a, pv));
+        }
+    }
+}
+FHO_T512 static void inv_stage512(double* x, int s) {
+    const int h = 512 >> s;
+    const __m512d two = _mm512_set1_pd(2.0);
+    const __m512d neg_im = _mm512_set_pd(-0.0, 0.0, -0.0, 0.0, -0.0, 0.0, -0.0, 0.0);
+    for (int j = 0; j < h; j += 4) {
+        __m512d w = _mm512_castpd128_pd512(_mm_loadu_pd(g_tw + 2 * (j << s)));
+        w = _mm512_insertf64x2(w, _mm_loadu_pd(g_tw + 2 * ((j + 1) << s)), 1);
+        w = _mm512_insertf64x2(w, _mm_loadu_pd(g_tw + 2 * ((j + 2) << s)), 2);
+        w = _mm512_insertf64x2(w, _mm_loadu_pd(g_tw + 2 * ((j + 3) << s)), 3);
+        const __m512d ws = _mm512_xor_pd(_mm512_permute_pd(w, 0xFF), neg_im), w0 = _mm512_movedup_pd(w);
+        for (int b = 0; b < 1024; b += 2 * h) {
+            double* p = x + 2 * (b + j);
+            double* q = x + 2 * (b + j + h);
+            const __m512d a = _mm512_loadu_pd(p), c = _mm512_loadu_pd(q);
+            const __m512d pv = _mm512_fmadd_pd(w0, c, _mm512_fmadd_pd(ws, _mm512_permute_pd(c, 0x55), a));
+            _mm512_storeu_pd(p, pv);
+            _mm512_storeu_pd(q, _mm512_fmsub_pd(two, a, pv));
+        }
+    }
+}
+FHO_T512 static inline __m512d cmul4(__m512d x, __m512d w) {
+    const __m512d neg_re = _mm512_set_pd(0.0, -0.0, 0.0, -0.0, 0.0, -0.0, 0.0, -0.0);
+    const __m512d t = _mm512_mul_pd(_mm512_permute_pd(x, 0xFF), _mm512_permute_pd(w, 0x55));
+    return _mm512_fmadd_pd(_mm512_movedup_pd(x), w, _mm512_xor_pd(t, neg_re));
+}
+FHO_T512 static inline __m512d cmul_acc4(__m512d k, __m512d g, __m512d w) {
+    const __m512d neg_re = _mm512_set_pd(0.0, -0.0, 0.0, -0.0, 0.0, -0.0, 0.0, -0.0);
+    const __m512d inner = _mm512_fmadd_pd(_mm512_xor_pd(_mm512_permute_pd(g, 0xFF), neg_re), _mm512_permute_pd(w, 0x55), k);
+    return _mm512_fmadd_pd(_mm512_movedup_pd(g), w, inner);
+}
+/* O = cmul(cmul_acc(cmul(Dn, Bn), Dx, Bx), E) over the 1024 points (mac_own_first, then e - 1) */
+FHO_T512 static void mac_factor512(const double* Dn, const double* Bn, const double* Dx, const double* Bx,
+                                   const double* E, double* O) {
+    for (int q = 0; q < FHO_HALF; q += 4) {
+        const __m512d pv = cmul4(_mm512_loadu_pd(Dn + 2 * q), _mm512_loadu_pd(Bn + 2 * q));
+        const __m512d o = cmul_acc4(pv, _mm512_loadu_pd(Dx + 2 * q), _mm512_loadu_pd(Bx + 2 * q));
+        _mm512_storeu_pd(O + 2 * q, cmul4(o, _mm512_loadu_pd(E + 2 * q)));
+    }
+}
+/* out[t] -= d row[t] mod 2^64, t <= n (vpmullq: the low 64 bits of the product) */
+FHO_T512 static uint32_t ks_row512(uint64_t* out, const uint64_t* row, uint64_t d, uint32_t n1) {
+    const __m512i vd = _mm512_set1_epi64((long long)d);
+    uint32_t t = 0;
+    for (; t + 8 <= n1; t += 8) {
+        const __m512i m = _mm512_mullo_epi64(_mm512_loadu_si512((const void*)(row + t)), vd);
+        _mm512_storeu_si512((void*)(out + t), _mm512_sub_epi64(_mm512_loadu_si512((const void*)(out + t)), m));
+    }
+    return t;
+}
+
 static void fft_forward_twisted_simd(double* x) {
     fho_tables_init();
     const __m256d two = _mm256_set1_pd(2.0);
+    const int w512 = g_simd >= 2;
     for (int st = 0; st < 9; ++st) {
         const int h = 512 >> st;
+        if (w512 && h >= 4) {
+            fwd_stage512(x, st);
+            continue;
+        }
         for (int b = 0; b < (1 << st); ++b) {
             const double* z = g_zeta + 2 * ((1 << st) + b);
             const __m256d z0 = _mm256_set1_pd(z[0]), zs = _mm256_set_pd(z[1], -z[1], z[1], -z[1]);
@@ -398,8 +489,13 @@ static void fft_inverse_simd(double* x) {
         p[2] = ar - cr; p[3] = ai - ci;
     }
     const __m256d two = _mm256_set1_pd(2.0), neg_im = _mm256_set_pd(-0.0, 0.0, -0.0, 0.0);
+    const int w512 = g_simd >= 2;
     for (int s = 8; s >= 0; --s) {
         const int h = 512 >> s;
+        if (w512 && h >= 4) {
+            inv_stage512(x, s);
+            continue;
+        }
         /* j outer: the twiddle pair of (j, j + 1) is the same in every block of the stage */
         for (int j = 0; j < h; j += 2) {
             const __m256d w = _mm256_set_m128d(_mm_loadu_pd(g_tw + 2 * ((j + 1) << s)), _mm_loadu_pd(g_tw + 2 * (j << s)));
@@ -572,7 +668,9 @@ void fho_keyswitch(const fho_keys* k, const uint64_t* in, uint64_t* out) {
             uint64_t dd = (uint64_t)d[l];
             uint32_t t = 0;
 #if FHO_HAVE_SIMD
-            if (g_simd && d[l] >= -4 && d[l] <= 4) {
+            if (simd_level() >= 2) {
+                t = ks_row512(out, row, dd, n + 1);
+            } else if (simd_level() && d[l] >= -4 && d[l] <= 4) {
                 /* |d| <= 4 (base 8, balanced): |d| row by shifts and adds, exact mod 2^64 as dd * row */
                 const int64_t kd = d[l] < 0 ? -d[l] : d[l];
                 for (; t + 4 <= n + 1; t += 4) {
@@ -593,6 +691,7 @@ void fho_keyswitch(const fho_keys* k, const uint64_t* in, uint64_t* out) {
 }
 
 void fho_keyswitch_batch(const fho_keys* k, const uint64_t* in, size_t count, uint64_t* out, int threads) {
+    (void)fho_simd(); /* the SIMD level, before the worker threads read it */
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(static)
@@ -752,8 +851,8 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
             continue;
         }
 #if FHO_HAVE_SIMD
-        if (g_simd) {
-            /* the same CMUX through the AVX2 loops (bit-identical, see fourier_add_to_poly_simd) */
+        if (simd_level()) {
+            /* the same CMUX through the AVX2 / AVX-512 loops (bit-identical, see fourier_add_to_poly_simd) */
             for (int m = 0; m < 2; ++m) {
                 double* acc = m ? acc1 : acc0;
                 double* D = m ? D1 : D0;
@@ -799,10 +898,14 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
                 const double* Bx = bs + ((1 - w) * 2 + w) * FHO_HALF * 2; /* row 1 - w, poly w */
                 const double* Dn = w ? D1 : D0;
                 const double* Dx = w ? D0 : D1;
-                for (int q = 0; q < FHO_HALF; q += 2) {
-                    const __m256d pv = cmul2(_mm256_loadu_pd(Dn + 2 * q), _mm256_loadu_pd(Bn + 2 * q));
-                    const __m256d o = cmul_acc2(pv, _mm256_loadu_pd(Dx + 2 * q), _mm256_loadu_pd(Bx + 2 * q));
-                    _mm256_storeu_pd(O + 2 * q, cmul2(o, _mm256_loadu_pd(rot + 2 * q)));
+                if (g_simd >= 2) {
+                    mac_factor512(Dn, Bn, Dx, Bx, rot, O);
+                } else {
+                    for (int q = 0; q < FHO_HALF; q += 2) {
+                        const __m256d pv = cmul2(_mm256_loadu_pd(Dn + 2 * q), _mm256_loadu_pd(Bn + 2 * q));
+                        const __m256d o = cmul_acc2(pv, _mm256_loadu_pd(Dx + 2 * q), _mm256_loadu_pd(Bx + 2 * q));
+                        _mm256_storeu_pd(O + 2 * q, cmul2(o, _mm256_loadu_pd(rot + 2 * q)));
+                    }
                 }
                 fourier_add_to_poly_simd(O, w ? acc1 : acc0, reduce);
             }

@@ -141,9 +141,10 @@ void fho_pbs_batch(const fho_keys* k, const uint64_t* in, size_t count, const ui
 /* LUT: f given as a table of msg*carry values (f[i] in [0, msg*carry)) */
 void fho_make_lut(const fho_params* p, const uint32_t* f_table, uint64_t* lut /* N */);
 
-/* AVX2 forms of the classic blind rotation's loops (bit-identical to the scalar ones; on by default
- * when built for x86-64-v3): fho_set_simd(0) selects the scalar loops, fho_simd() reports the choice */
-void fho_set_simd(int on);
+/* SIMD forms of the classic blind rotation's loops and the keyswitch (bit-identical to the scalar
+ * ones): level 0 scalar, 1 AVX2, 2 AVX-512 (runtime-detected; the default is the best the CPU has,
+ * fho_set_simd(-1) restores it, larger requests are clamped); fho_simd() reports the level */
+void fho_set_simd(int level);
 int fho_simd(void);
 
 #ifdef __cplusplus

@@ -86,25 +86,31 @@ def test_pbs_identity_and_square_all_messages(okeys):
 
 
 def test_simd_paths_bit_identical(okeys):
-    """The AVX2 loops of the oracle's classic blind rotation and keyswitch (what bench.py's
-    cpu_baseline times) against its scalar restatement (fho_set_simd(0)): the same ciphertexts give
-    identical words, through every LUT-rotation and monomial pattern a random batch reaches."""
+    """The SIMD loops of the oracle's classic blind rotation and keyswitch (what bench.py's
+    cpu_baseline times: AVX2, and AVX-512 where the CPU has it) against its scalar restatement
+    (fho_set_simd(0)): the same ciphertexts give identical words at every level the CPU supports,
+    through every LUT-rotation and monomial pattern a random batch reaches."""
     lib = oracle.load()
-    if not lib.fho_simd():
+    top = lib.fho_simd()
+    if top == 0:
         pytest.skip("oracle built without AVX2/FMA")
     r = okeys.rng(11)
     cts = np.stack([okeys.encrypt(r, m % 16) for m in range(12)])
     luts = np.stack([okeys.make_lut([(m * 5 + k) % 16 for m in range(16)]) for k in range(3)])
     idx = (np.arange(12) % 3).astype(np.uint32)
+    res = {}
     try:
-        fast = okeys.pbs_batch(cts, luts, idx, 4), okeys.keyswitch_batch(cts, 4)
-        lib.fho_set_simd(0)
-        slow = okeys.pbs_batch(cts, luts, idx, 4), okeys.keyswitch_batch(cts, 4)
+        for level in range(top + 1):
+            lib.fho_set_simd(level)
+            assert lib.fho_simd() == level
+            res[level] = okeys.pbs_batch(cts, luts, idx, 4), okeys.keyswitch_batch(cts, 4)
     finally:
-        lib.fho_set_simd(1)
-    assert np.array_equal(fast[1], slow[1])
-    assert np.array_equal(fast[0], slow[0])
-    assert [okeys.decrypt(fast[0][i]) for i in range(12)] == [((i % 16) * 5 + i % 3) % 16 for i in range(12)]
+        lib.fho_set_simd(-1)
+    assert lib.fho_simd() == top
+    for level in range(1, top + 1):
+        assert np.array_equal(res[level][1], res[0][1]), f"keyswitch, level {level}"
+        assert np.array_equal(res[level][0], res[0][0]), f"PBS, level {level}"
+    assert [okeys.decrypt(res[top][0][i]) for i in range(12)] == [((i % 16) * 5 + i % 3) % 16 for i in range(12)]
 
 
 def test_keyswitch_preserves_message(okeys):
