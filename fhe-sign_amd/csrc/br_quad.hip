@@ -9,9 +9,12 @@
 //
 // FFT index bits b9..b0 per phase (thread t = 64 h + L, register r = 0..7, lane bits L5..L0):
 //   A  idx = 128 r + t                                   regs (b9 b8 b7), h = b6   DIF stages 0-2
-//   B  regs (b6 b5 b4), h = b9, lanes L5 L4 L3 = b3 b2 b1, L2 L1 = b8 b7, L0 = b0  stages 3-5
-//   C  regs (b3 b2 b1), h = b9, lanes L5 L4 L3 = b6 b5 b4, L2 L1 = b8 b7, L0 = b0  stages 6-8
-//   stage 9 pairs lanes L, L^1 (b0 = L0): DPP quad_perm, one signed add per value.
+//   B  regs (b6 b5 b4), h = b9, lanes L5 L4 L3 = b3 b2 b1, L2 = b0, L1 = b7, L0 = b8  stages 3-5
+//   C  regs (b3 b2 b1), h = b9, lanes L5 L4 L3 = b6 b5 b4, L2 = b0, L1 = b7, L0 = b8  stages 6-8
+//   MAC regs (b0 b2 b1), lane L2 = b3 (register bit 2 <-> lane bit 2 by bank-masked DPP): stage 9
+//   on register pairs (r, r + 4), and the inverse's stages 9, 8, 7 with per-register twiddles
+//   (classic kernel, S9; round 3 paired lanes L, L ^ 1 for stage 9 -- 6 f64 per lane and point
+//   instead of 4 per pair -- which the multi-bit kernel still does, with L2 = b8 and L0 = b0).
 // A<->B crosses the two waves of a polynomial (LDS + barrier).  B<->C swaps register bits (2,1,0)
 // with lane bits (5,4,3) inside the wave, in registers: v_permlane32_swap / v_permlane16_swap (one
 // instruction per dword pair) for lane bits 5,4 and a bank-masked DPP move for lane bit 3.  The
@@ -69,6 +72,9 @@ constexpr int QTW_SZ = 512 + 16;
 // zetas of stages 0-2 (read from global memory: Z[1], Z[2], Z[4], Z[6]).
 constexpr int QZ_LDS = 546, QZ_ONE = 544, QZ_MINUS_I = 545, QZ_UNIFORM = 546;
 FHE_DEV constexpr int tpos(int k) { return k + (k >> 5); }
+// LDS position of zeta entry k in the S9 layout: stages 6-9 (k >= 32) swap bit 2 by bit 4, so the 16
+// lanes of a read group (u = 16 b8 + 8 b7 + ..., b8 on lane bit 0) hit 16 different banks
+FHE_DEV constexpr int zsw(int k) { return k >= 32 ? k ^ (((k >> 4) & 1) << 2) : k; }
 
 // Inverse (DIT) stage on register bit K (pairs r, r | 2^K); lb = tpos(lane part of the twiddle index).
 // The twiddle index is lane part + step * (r mod 2^K), step 128 (K = 2) or 256 (K = 1), with lane
@@ -145,8 +151,11 @@ FHE_DEV void q_stage9(cplx (&x)[8], double sgn) {
 }
 // ---- B <-> C as register transposes (no LDS): register bits (2,1,0) <-> lane bits (5,4,3)
 // (lane bits 5, 4: qx_permlane<K> in device_math.h)
-// K = 3: lanes with lane bit 3 set are whole 4-lane DPP banks, one masked move per half
-FHE_DEV void qx_banked3(cplx& X, cplx& Y) {
+// K = 3, 2: lanes with lane bit K set are whole 4-lane DPP banks (banks 2, 3 for K = 3; 1, 3 for
+// K = 2), one masked row shift by 2^K per half
+template <int K>
+FHE_DEV void qx_banked(cplx& X, cplx& Y) {
+    constexpr int SH = 1 << K, HI = K == 3 ? 0xC : 0xA, LO = K == 3 ? 0x3 : 0x5;
     uint32_t x[4], y[4];
     qsplit(X.x, x[0], x[1]);
     qsplit(X.y, x[2], x[3]);
@@ -154,8 +163,8 @@ FHE_DEV void qx_banked3(cplx& X, cplx& Y) {
     qsplit(Y.y, y[2], y[3]);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)x[d], (int)y[d], 0x118, 0xF, 0xC, false);
-        const uint32_t ny = (uint32_t)__builtin_amdgcn_update_dpp((int)y[d], (int)x[d], 0x108, 0xF, 0x3, false);
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)x[d], (int)y[d], 0x110 + SH, 0xF, HI, false);
+        const uint32_t ny = (uint32_t)__builtin_amdgcn_update_dpp((int)y[d], (int)x[d], 0x100 + SH, 0xF, LO, false);
         x[d] = nx;
         y[d] = ny;
     }
@@ -169,7 +178,7 @@ FHE_DEV void q_xpose_bc(cplx (&x)[8]) {
     for (int r = 0; r < 8; ++r)
         if (!(r & 2)) qx_permlane<4>(x[r], x[r + 2]);  // reg bit 1 <-> lane bit 4
 #pragma unroll
-    for (int r = 0; r < 8; r += 2) qx_banked3(x[r], x[r + 1]);  // reg bit 0 <-> lane bit 3
+    for (int r = 0; r < 8; r += 2) qx_banked<3>(x[r], x[r + 1]);  // reg bit 0 <-> lane bit 3
 }
 }  // namespace
 
@@ -196,6 +205,9 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                                                               const cplx* __restrict__ zq,  // quad_zetas
                                                               const cplx* __restrict__ mono,  // E[4096] (G = 2)
                                                               uint64_t* __restrict__ out, int n) {
+    // S9 (classic): stage 9 in registers (see the layout table above); the multi-bit kernel keeps
+    // stage 9 across lane pairs
+    constexpr bool S9 = G == 1;
     // one LDS block (the kernel's only LDS object, so it starts at address 0): the polynomials'
     // exchange regions, the twiddles, the zetas (G = 2: the monomial lane factors)
     constexpr int QL_W = 2 * QX_SZ, QL_Z = QL_W + QTW_SZ, QL_M = QL_Z + QZ_LDS;
@@ -209,7 +221,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     // pattern, m = a_i: the factored CMUX)
     cplx* s_mono = s_lds + QL_M;
     for (int k = threadIdx.x; k < 512; k += 256) s_w[tpos(k)] = W[k];
-    for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[k] = zq[k];
+    for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[S9 ? zsw(k) : k] = zq[k];
     __syncthreads();
     const int ct = blockIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;  // w in an SGPR
@@ -218,17 +230,20 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     const cplx* other = s_x[p ^ 1];
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
     // lane bits of phases B and C (see the layout table above): L5 L4 L3 = (b3 b2 b1) in B, (b6 b5 b4)
-    // in C; L2 L1 = b8 b7 and L0 = b0 in both
+    // in C; L1 = b7 in both; b8, b0 on L0, L2 (S9) or L2, L0
     const int l0 = L & 1, l1 = (L >> 1) & 1, l2 = (L >> 2) & 1, l3 = (L >> 3) & 1, l4 = (L >> 4) & 1, l5 = (L >> 5) & 1;
-    const int u = 16 * l2 + 8 * l1 + 4 * l5 + 2 * l4 + l3;     // (b8 .. b4) in phase C
-    const int lowB = 8 * l5 + 4 * l4 + 2 * l3 + l0;              // (b3 .. b0) in phase B
-    const int B3 = 4 * h + 2 * l2 + l1, B6 = 32 * h + u;        // twisted-transform block bases of phases B, C
-    const int z9 = 288 + 32 * h + u;                             // stage-9 zeta of this lane (r2 = 0)
+    const int lb8 = S9 ? l0 : l2, lb0 = S9 ? l2 : l0;
+    const int u = 16 * lb8 + 8 * l1 + 4 * l5 + 2 * l4 + l3;    // (b8 .. b4) in phase C
+    const int lowB = 8 * l5 + 4 * l4 + 2 * l3 + lb0;             // (b3 .. b0) in phase B
+    const int B3 = 4 * h + 2 * lb8 + l1, B6 = 32 * h + u;       // twisted-transform block bases of phases B, C
+    // zeta-table positions of stages 6-9 (S9: swizzled, zsw)
+    const int zB6 = S9 ? (B6 ^ (4 * lb8)) : B6;
+    const int z9 = S9 ? 288 + 128 * l2 + zB6 : 288 + 32 * h + u;  // stage-9 zeta of this lane (S9: b2 = 0)
 
     // lane parts of the exchange addresses (register parts are compile-time constants)
     const int bA = fq(t);
-    const int bB = fq(512 * h + 256 * l2 + 128 * l1 + lowB);
-    const int bC = fq(512 * h + 16 * u + l0);
+    const int bB = fq(512 * h + 256 * lb8 + 128 * l1 + lowB);
+    const int bC = fq(512 * h + 16 * u + lb0);
 
     double acc[16];  // coefficients 128 r + t (f64 torus representatives)
     {
@@ -246,8 +261,8 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
     }
 
-    // 4 (j0 mod 64) + 1 of this lane's phase-C point r = 0 (idx 512 h + 16 u + L0, j0 = bitrev)
-    const uint32_t c4 = 4u * ((__builtin_bitreverse32((uint32_t)(512 * h + 16 * u + l0)) >> 22) & 63u) + 1u;
+    // 4 (j0 mod 64) + 1 of this lane's MAC points (j0 = bitrev(idx) mod 64: idx bits b9 .. b4, i.e. h, u)
+    const uint32_t c4 = 4u * ((__builtin_bitreverse32((uint32_t)(512 * h + 16 * u)) >> 22) & 63u) + 1u;
     uint32_t a_next = modswitch_2n(a_ct[0]);
     uint32_t a_next1 = modswitch_2n(a_ct[1]);  // G = 1: a of the step after next (two-deep pipeline)
     // G = 1: the wave-uniform pair factors E[256 k a], k = 1..3, of the next step, loaded one step
@@ -281,7 +296,6 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     __syncthreads();
     // key slices and untwist factors through buffer resources (bptr: per-step bases in SGPRs)
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
-    const double sgn9 = __longlong_as_double((long long)((uint64_t)(0x3FF00000u | ((uint32_t)L << 31)) << 32));  // +-1 by L0
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
     bool red_in = false;  // the previous update's reduction, deferred to this step's digits (red_digit_s)
     for (int i = 0; i < n / (G == 1 ? 1 : QMBDIV); ++i) {
@@ -359,9 +373,25 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             }
         }
         }
-        q_ct<2>(x, s_z[32 + B6], s_z[32 + B6]);
-        q_ct<1>(x, s_z[96 + B6], s_z[96 + B6]);
-        q_ct<0>(x, s_z[160 + B6], s_z[224 + B6]);
+        q_ct<2>(x, s_z[32 + zB6], s_z[32 + zB6]);
+        q_ct<1>(x, s_z[96 + zB6], s_z[96 + zB6]);
+        q_ct<0>(x, s_z[160 + zB6], s_z[224 + zB6]);
+        if constexpr (S9) {
+            // stage 9 in registers: register bit 2 <-> lane bit 2 (b3 <-> b0), then the pairs (r, r + 4)
+            // with t = zeta c (oracle: cmul, then a + t, a - t); registers r = 2 b2 + b1 < 4, zeta
+            // index 288 + 128 b3 + 64 b2 + 32 h + u, times i for b1 = 1
+#pragma unroll
+            for (int r = 0; r < 4; ++r) qx_banked<2>(x[r], x[r + 4]);
+            const cplx z0 = s_z[z9], z1 = s_z[z9 + 64];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const cplx zb = (r >> 1) ? z1 : z0;
+                const cplx tt = cmul(x[r + 4], (r & 1) ? mul_i(zb) : zb);
+                const cplx a = x[r];
+                x[r] = make_double2(a.x + tt.x, a.y + tt.y);
+                x[r + 4] = make_double2(a.x - tt.x, a.y - tt.y);
+            }
+        } else {
         // stage 9 across lane pairs: t = zeta c on the odd lane, the even lane keeps a (x 1, exact),
         // then (a + t, a - t) by the shared DPP step; odd registers use i zeta (1 on even lanes)
 #pragma unroll
@@ -371,7 +401,8 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             x[2 * r2] = cmul(x[2 * r2], s_z[ia]);
             x[2 * r2 + 1] = cmul(x[2 * r2 + 1], mul_i(s_z[ib]));
         }
-        q_stage9(x, G == 1 ? sgn9 : q_sgn9());
+        q_stage9(x, q_sgn9());
+        }
 
         // ---- swap Fourier digits with the other polynomial's wave of the same half, MAC with BSK
         wave_sync();
@@ -400,19 +431,18 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
         const cplx Eb = Ebn;
         Ebn = lane_factor(a_next);
-        cplx eb1, em1;
+        // MAC layout (S9): registers (b0 b2 b1), lane bit 2 = b3, i.e. j bits 9, 7, 8 and 6 of the
+        // point: e = i^((j8 + 2 j9) a) cmul(Eb, E[256 (j6 + 2 j7) a]), the pair factor picked per lane
+        const cplx Flo = l2 ? F[0] : make_double2(1.0, 0.0), Fhi = l2 ? F[2] : F[1];
+        cplx elo, ehi;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             x[r] = cmul_acc(x[r], other[bC + fq(2 * r)], Bq1[r]);
-            if (r == 0) {
-                const uint32_t sg = (uint32_t)(l0 & a) << 31;
-                eb1 = make_double2(neg_if(Eb.x, sg), neg_if(Eb.y, sg));
-            }
-            if (!(r & 1)) {
-                const uint32_t qk = ((r >> 2) & 1) + 2u * ((r >> 1) & 1);
-                em1 = qk == 0 ? eb1 : cmul(eb1, F[qk - 1]);
-            }
-            const cplx w = (r & 1) ? turn_sel_m1(em1, a) : make_double2(em1.x - 1.0, em1.y);
+            if (r == 0) elo = cmul(Eb, Flo);  // exact for Flo = 1
+            if (r == 2) ehi = cmul(Eb, Fhi);
+            const cplx em = (r & 2) ? ehi : elo;
+            const uint32_t tr = ((r & 1) ? a : 0u) + ((r & 4) ? 2u * a : 0u);
+            const cplx w = (r & 5) ? turn_sel_m1(em, tr) : make_double2(em.x - 1.0, em.y);
             x[r] = cmul(x[r], w);
         }
         } else {
@@ -458,10 +488,33 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
 
         // ---- inverse FFT: stage 9 and phase C in registers, then the region again
-        q_stage9(x, G == 1 ? sgn9 : q_sgn9());
-        q_dit<0>(x, s_w, tpos(256 * (L & 1)));
-        q_dit<1>(x, s_w, tpos(128 * (L & 1)));
-        q_dit<2>(x, s_w, tpos(64 * (L & 1)));
+        if constexpr (S9) {
+            // stages 9, 8, 7 in the MAC layout (registers b0 b2 b1), where their twiddles W[256 b0]
+            // and W[128 b0 + 256 b1] are per register: 1 and W[256] = i exact (p = a + t, t a move),
+            // W[128], W[384] = i W[128] wave-uniform; then register bit 2 <-> lane bit 2 back to the
+            // phase-C layout for stage 6
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // stage 9 (twiddle 1), pairs (r, r + 4)
+                const cplx a = x[r], c = x[r + 4];
+                x[r] = make_double2(a.x + c.x, a.y + c.y);
+                x[r + 4] = make_double2(a.x - c.x, a.y - c.y);
+            }
+#pragma unroll
+            for (int r = 0; r < 8; r += 2)  // stage 8 (b1 = register bit 0): conj(W) = 1, -i
+                dit_bfly_unit(x[r], x[r + 1], (r & 4) ? mul_negi(x[r + 1]) : x[r + 1]);
+            const cplx w128 = s_w[tpos(128)];
+            dit_bfly_unit(x[0], x[2], x[2]);  // stage 7 (b2 = register bit 1)
+            dit_bfly_unit(x[1], x[3], mul_negi(x[3]));
+            dit_bfly(x[4], x[6], conj_(w128));
+            dit_bfly(x[5], x[7], conj_(mul_i(w128)));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) qx_banked<2>(x[r], x[r + 4]);
+        } else {
+            q_stage9(x, q_sgn9());
+            q_dit<0>(x, s_w, tpos(256 * lb0));
+            q_dit<1>(x, s_w, tpos(128 * lb0));
+        }
+        q_dit<2>(x, s_w, tpos(64 * lb0));
         q_xpose_bc(x);
         __syncthreads();  // the other polynomial's waves have read this wave's digits
         if constexpr (G == 2)
@@ -518,15 +571,18 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
 }
 
 // Fourier BSK: blind-rotate layout (R = 4v + q, lane L' <-> idx = 4 (L' + 64 v) + q) -> quad layout
-// (h, r, L <-> idx = 512 h + 16 u + 2 r + L0 with u = (b8 .. b4) from the lane bits as in phase C),
-// one workgroup per polynomial.
-__global__ __launch_bounds__(256) void k_bsk_to_quad(const cplx* __restrict__ src, cplx* __restrict__ dst) {
+// of the MAC, one workgroup per polynomial: (h, r, L) <-> idx = 512 h + 16 u + 2 r + L0 with
+// u = (b8 .. b4) from the lane bits as in phase C (multi-bit), or (S9, classic) idx = 512 h + 16 u +
+// 8 L2 + 4 r1 + 2 r0 + r2 with u = 16 L0 + 8 L1 + 4 L5 + 2 L4 + L3.
+__global__ __launch_bounds__(256) void k_bsk_to_quad(const cplx* __restrict__ src, cplx* __restrict__ dst, int s9) {
     const cplx* s = src + (size_t)blockIdx.x * 1024;
     cplx* d = dst + (size_t)blockIdx.x * 1024;
     for (int k = threadIdx.x; k < 1024; k += 256) {
         const int hh = k >> 9, r = (k >> 6) & 7, L = k & 63;
-        const int u = 16 * ((L >> 2) & 1) + 8 * ((L >> 1) & 1) + 4 * ((L >> 5) & 1) + 2 * ((L >> 4) & 1) + ((L >> 3) & 1);
-        const int idx = 512 * hh + 16 * u + 2 * r + (L & 1);
+        const int lb8 = s9 ? (L & 1) : ((L >> 2) & 1);
+        const int u = 16 * lb8 + 8 * ((L >> 1) & 1) + 4 * ((L >> 5) & 1) + 2 * ((L >> 4) & 1) + ((L >> 3) & 1);
+        const int idx = s9 ? 512 * hh + 16 * u + 8 * ((L >> 2) & 1) + 4 * ((r >> 1) & 1) + 2 * (r & 1) + (r >> 2)
+                           : 512 * hh + 16 * u + 2 * r + (L & 1);
         const int q = idx & 3, Lp = (idx >> 2) & 63, v = idx >> 8;
         d[k] = s[(4 * v + q) * 64 + Lp];
     }
@@ -546,8 +602,8 @@ hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const Pbs
     return hipGetLastError();
 }
 
-hipError_t launch_bsk_to_quad(const cplx* bsk, int npoly, cplx* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_bsk_to_quad, dim3(npoly), dim3(256), 0, s, bsk, out);
+hipError_t launch_bsk_to_quad(const cplx* bsk, int npoly, int grouping, cplx* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_bsk_to_quad, dim3(npoly), dim3(256), 0, s, bsk, out, grouping == 1 ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """LDS cycle census of one CMUX of the 4-wave blind rotation (br_quad.hip, classic), per wave.
-(Models the round-2 kernel, whose CMUX still had the rotation exchange; the factored CMUX of round 3
-has no rotation writes/reads -- DESIGN.md 3.)
+Layout "r3" is the round-3 kernel (stage 9 across lane pairs, b0 = L0, b8 = L2); "s9" has b0 on
+lane bit 2 and b8 on L0, with stage 9 in registers after a register-bit-2 <-> lane-bit-2 transpose
+(two zeta reads instead of eight; the digit swap in that MAC layout).  The rotation sites of the
+round-2 kernel are gone with the factored CMUX.
 
 Every LDS instruction of the loop with its per-lane byte addresses, costed by the gfx950 rules of
 MI355X_MICROARCH.md's LDS table: lane groups per instruction, one LDS-array cycle per group when
 conflict-free, +1 per extra distinct address on a bank within a group; stores also pay their
 data transfer (2 cycles per source dword per wave-instruction: b64 6, b128 13), so a store costs
 max(transfer, array cycles).  Prints per site the array cycles, the conflict-free minimum and the
-charged cycles, then the totals.  usage: python3 tools/lds_census_quad.py [rotation a]
+charged cycles, then the totals.  usage: python3 tools/lds_census_quad.py [r3|s9]
 """
 import sys
 
@@ -58,7 +60,8 @@ def cycles(kind, addr):
 
 
 def main():
-    a = int(sys.argv[1]) if len(sys.argv) > 1 else 1234
+    lay = sys.argv[1] if len(sys.argv) > 1 else "r3"
+    s9 = lay == "s9"
     sites = []  # (name, kind, [addr per lane]) per wave-instruction; averaged over the 4 waves
     for w in range(4):
         p, h = w >> 1, w & 1
@@ -66,20 +69,23 @@ def main():
         L = list(range(64))
         t = [64 * h + l for l in L]
         bit = lambda l, k: (l >> k) & 1
-        u = [16 * bit(l, 2) + 8 * bit(l, 1) + 4 * bit(l, 5) + 2 * bit(l, 4) + bit(l, 3) for l in L]
-        lowB = [8 * bit(l, 5) + 4 * bit(l, 4) + 2 * bit(l, 3) + bit(l, 0) for l in L]
-        B3 = [4 * h + 2 * bit(l, 2) + bit(l, 1) for l in L]
+        b8 = (lambda l: bit(l, 0)) if s9 else (lambda l: bit(l, 2))
+        b0 = (lambda l: bit(l, 2)) if s9 else (lambda l: bit(l, 0))
+        u = [16 * b8(l) + 8 * bit(l, 1) + 4 * bit(l, 5) + 2 * bit(l, 4) + bit(l, 3) for l in L]
+        lowB = [8 * bit(l, 5) + 4 * bit(l, 4) + 2 * bit(l, 3) + b0(l) for l in L]
+        B3 = [4 * h + 2 * b8(l) + bit(l, 1) for l in L]
         B6 = [32 * h + uu for uu in u]
         z9 = [288 + 32 * h + uu for uu in u]
         bA = [fq(tt) for tt in t]
-        bB = [fq(512 * h + 256 * bit(l, 2) + 128 * bit(l, 1) + lowB[l]) for l in L]
-        bC = [fq(512 * h + 16 * u[l] + bit(l, 0)) for l in L]
+        bB = [fq(512 * h + 256 * b8(l) + 128 * bit(l, 1) + lowB[l]) for l in L]
+        if s9:  # MAC layout: regs (b0 b2 b1), lane bit 2 = b3
+            bC = [fq(512 * h + 16 * u[l] + 8 * bit(l, 2)) for l in L]
+            regC = [fq(4 * ((r >> 1) & 1) + 2 * (r & 1) + (r >> 2)) for r in range(8)]
+        else:
+            bC = [fq(512 * h + 16 * u[l] + bit(l, 0)) for l in L]
+            regC = [fq(2 * r) for r in range(8)]
         cpl = lambda idx: [16 * i for i in idx]
         S = lambda name, kind, ad: sites.append((name, kind, ad))
-        for r in range(16):
-            S("rotation write", "w64", [region + 8 * (128 * r + tt) for tt in t])
-        for r in range(16):
-            S("rotation read", "r64", [region + ((((tt - a) & 4095) << 3) + 1024 * r & 0x3FFF) for tt in t])
         for r in range(8):
             S("A->B write", "w128", [region + 16 * (b + fq(128 * r)) for b in bA])
         for r in range(8):
@@ -88,16 +94,20 @@ def main():
             S("zeta B", "r128", cpl([QL_Z + off + b for b in B3]))
         for off in (32, 96, 160, 224):
             S("zeta C", "r128", cpl([QL_Z + off + b for b in B6]))
-        for r2 in range(4):
-            ia = [z9[l] + 64 * r2 if l & 1 else QZ_ONE for l in L]
-            ib = [ia[l] if l & 1 else QZ_MINUS_I for l in L]
-            S("zeta 9", "r128", cpl([QL_Z + i for i in ia]))
-            S("zeta 9", "r128", cpl([QL_Z + i for i in ib]))
+        if s9:
+            for b2 in range(2):
+                S("zeta 9", "r128", cpl([QL_Z + z9[l] + 128 * bit(l, 2) + 64 * b2 for l in L]))
+        else:
+            for r2 in range(4):
+                ia = [z9[l] + 64 * r2 if l & 1 else QZ_ONE for l in L]
+                ib = [ia[l] if l & 1 else QZ_MINUS_I for l in L]
+                S("zeta 9", "r128", cpl([QL_Z + i for i in ia]))
+                S("zeta 9", "r128", cpl([QL_Z + i for i in ib]))
         for r in range(8):
-            S("digit swap write", "w128", [region + 16 * (b + fq(2 * r)) for b in bC])
+            S("digit swap write", "w128", [region + 16 * (b + regC[r]) for b in bC])
         oreg = (1 - p) * QX_SZ * 16
         for r in range(8):
-            S("digit swap read", "r128", [oreg + 16 * (b + fq(2 * r)) for b in bC])
+            S("digit swap read", "r128", [oreg + 16 * (b + regC[r]) for b in bC])
         # inverse twiddles: q_dit<K> reads sw[lb] (and sw[lb + 132] for K = 2)
         def tw(name, lane_part):
             for K, lp in zip((0, 1, 2), lane_part):
@@ -105,7 +115,7 @@ def main():
                 S(name, "r128", cpl([QL_W + x for x in lb]))
                 if K == 2:
                     S(name, "r128", cpl([QL_W + x + 132 for x in lb]))
-        tw("twiddle C", ([256 * (l & 1) for l in L], [128 * (l & 1) for l in L], [64 * (l & 1) for l in L]))
+        tw("twiddle C", ([256 * b0(l) for l in L], [128 * b0(l) for l in L], [64 * b0(l) for l in L]))
         tw("twiddle B", ([32 * x for x in lowB], [16 * x for x in lowB], [8 * x for x in lowB]))
         for r in range(8):
             S("B->A write", "w128", [region + 16 * (b + fq(16 * r)) for b in bB])
@@ -121,7 +131,7 @@ def main():
         e[3] += base
         e[4] += ch
     tot = [0, 0, 0]
-    print(f"{'site':18s} {'kind':5s} {'instr':>5s} {'array':>7s} {'min':>7s} {'charged':>8s}   (per wave, a = {a})")
+    print(f"{'site':18s} {'kind':5s} {'instr':>5s} {'array':>7s} {'min':>7s} {'charged':>8s}   (per wave, layout {lay})")
     for name, (kind, n, arr, base, ch) in agg.items():
         print(f"{name:18s} {kind:5s} {n / 4:5.0f} {arr / 4:7.1f} {base / 4:7.1f} {ch / 4:8.1f}")
         tot[0] += arr / 4
