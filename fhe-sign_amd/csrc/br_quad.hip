@@ -243,7 +243,10 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     // lane parts of the exchange addresses (register parts are compile-time constants)
     const int bA = fq(t);
     const int bB = fq(512 * h + 256 * lb8 + 128 * l1 + lowB);
-    const int bC = fq(512 * h + 16 * u + lb0);
+    // digit swap: any map onto this half's region positions works (both polynomials' waves use it);
+    // S9 takes lane bits 5..0 -> idx bits 5..0, registers -> bits 8..6 (conflict-free reads and writes)
+    const int bC = S9 ? fq(512 * h + L) : fq(512 * h + 16 * u + lb0);
+    constexpr int DSW = S9 ? 64 : 2;  // register part fq(DSW r)
 
     double acc[16];  // coefficients 128 r + t (f64 torus representatives)
     {
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         // ---- swap Fourier digits with the other polynomial's wave of the same half, MAC with BSK
         wave_sync();
 #pragma unroll
-        for (int r = 0; r < 8; ++r) reg[bC + fq(2 * r)] = x[r];
+        for (int r = 0; r < 8; ++r) reg[bC + fq(DSW * r)] = x[r];
         // G = 1: mac2 = own digit x row p (the rounded product), then other digit x row 1 - p
         // accumulated into it, split around the barrier; the other row's loads go out as the own
         // row's registers free up
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         cplx elo, ehi;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            x[r] = cmul_acc(x[r], other[bC + fq(2 * r)], Bq1[r]);
+            x[r] = cmul_acc(x[r], other[bC + fq(DSW * r)], Bq1[r]);
             if (r == 0) elo = cmul(Eb, Flo);  // exact for Flo = 1
             if (r == 2) ehi = cmul(Eb, Fhi);
             const cplx em = (r & 2) ? ehi : elo;
@@ -483,7 +486,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                 Ko = cmul_acc(Ko, Bm, w);
                 Kt = cmul_acc(Kt, Bo, w);
             }
-            x[r] = mac2(x[r], Ko, other[bC + fq(2 * r)], Kt);
+            x[r] = mac2(x[r], Ko, other[bC + fq(DSW * r)], Kt);
         }
         }
 

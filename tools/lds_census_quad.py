@@ -2,7 +2,7 @@
 """LDS cycle census of one CMUX of the 4-wave blind rotation (br_quad.hip, classic), per wave.
 Layout "r3" is the round-3 kernel (stage 9 across lane pairs, b0 = L0, b8 = L2); "s9" has b0 on
 lane bit 2 and b8 on L0, with stage 9 in registers after a register-bit-2 <-> lane-bit-2 transpose
-(two zeta reads instead of eight; the digit swap in that MAC layout).  The rotation sites of the
+(two zeta reads instead of eight, the zeta table swizzled, the digit swap on a lane-linear map).  The rotation sites of the
 round-2 kernel are gone with the factored CMUX.
 
 Every LDS instruction of the loop with its per-lane byte addresses, costed by the gfx950 rules of
@@ -62,6 +62,8 @@ def cycles(kind, addr):
 def main():
     lay = sys.argv[1] if len(sys.argv) > 1 else "r3"
     s9 = lay == "s9"
+    # zeta-table swizzle of the S9 kernel (br_quad.hip zsw)
+    zs = (lambda k: k ^ (((k >> 4) & 1) << 2) if k >= 32 else k) if s9 else (lambda k: k)
     sites = []  # (name, kind, [addr per lane]) per wave-instruction; averaged over the 4 waves
     for w in range(4):
         p, h = w >> 1, w & 1
@@ -78,9 +80,9 @@ def main():
         z9 = [288 + 32 * h + uu for uu in u]
         bA = [fq(tt) for tt in t]
         bB = [fq(512 * h + 256 * b8(l) + 128 * bit(l, 1) + lowB[l]) for l in L]
-        if s9:  # MAC layout: regs (b0 b2 b1), lane bit 2 = b3
-            bC = [fq(512 * h + 16 * u[l] + 8 * bit(l, 2)) for l in L]
-            regC = [fq(4 * ((r >> 1) & 1) + 2 * (r & 1) + (r >> 2)) for r in range(8)]
+        if s9:  # digit swap: lane bits -> idx bits 5..0, registers -> 8..6
+            bC = [fq(512 * h + l) for l in L]
+            regC = [fq(64 * r) for r in range(8)]
         else:
             bC = [fq(512 * h + 16 * u[l] + bit(l, 0)) for l in L]
             regC = [fq(2 * r) for r in range(8)]
@@ -91,12 +93,12 @@ def main():
         for r in range(8):
             S("A->B read", "r128", [region + 16 * (b + fq(16 * r)) for b in bB])
         for off in (0, 8, 16, 24):
-            S("zeta B", "r128", cpl([QL_Z + off + b for b in B3]))
+            S("zeta B", "r128", cpl([QL_Z + zs(off + b) for b in B3]))
         for off in (32, 96, 160, 224):
-            S("zeta C", "r128", cpl([QL_Z + off + b for b in B6]))
+            S("zeta C", "r128", cpl([QL_Z + zs(off + b) for b in B6]))
         if s9:
             for b2 in range(2):
-                S("zeta 9", "r128", cpl([QL_Z + z9[l] + 128 * bit(l, 2) + 64 * b2 for l in L]))
+                S("zeta 9", "r128", cpl([QL_Z + zs(z9[l] + 128 * bit(l, 2) + 64 * b2) for l in L]))
         else:
             for r2 in range(4):
                 ia = [z9[l] + 64 * r2 if l & 1 else QZ_ONE for l in L]
