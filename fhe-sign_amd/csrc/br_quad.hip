@@ -12,9 +12,9 @@
 //   B  regs (b6 b5 b4), h = b9, lanes L5 L4 L3 = b3 b2 b1, L2 = b0, L1 = b7, L0 = b8  stages 3-5
 //   C  regs (b3 b2 b1), h = b9, lanes L5 L4 L3 = b6 b5 b4, L2 = b0, L1 = b7, L0 = b8  stages 6-8
 //   MAC regs (b0 b2 b1), lane L2 = b3 (register bit 2 <-> lane bit 2 by bank-masked DPP): stage 9
-//   on register pairs (r, r + 4), and the inverse's stages 9, 8, 7 with per-register twiddles
-//   (classic kernel, S9; round 3 paired lanes L, L ^ 1 for stage 9 -- 6 f64 per lane and point
-//   instead of 4 per pair -- which the multi-bit kernel still does, with L2 = b8 and L0 = b0).
+//   on register pairs (r, r + 4), and the inverse's stages 9, 8, 7 with per-register twiddles.
+//   (Until round 3 stage 9 paired lanes L, L ^ 1 by DPP -- 6 f64 per lane and point instead of 4 per
+//   pair -- with L2 = b8 and L0 = b0.)
 // A<->B crosses the two waves of a polynomial (LDS + barrier).  B<->C swaps register bits (2,1,0)
 // with lane bits (5,4,3) inside the wave, in registers: v_permlane32_swap / v_permlane16_swap (one
 // instruction per dword pair) for lane bits 5,4 and a bank-masked DPP move for lane bit 3.  The
@@ -70,9 +70,11 @@ constexpr int QTW_SZ = 512 + 16;
 // 8 [160 + 64j + B6], 9 [288 + 64 r2 + 32 h + u] (B3 = 4h + (b8 b7), B6 = 32h + u, u = (b8 .. b4), even
 // blocks only: odd ones are i times them), then 1 and -i (stage 9, lanes L0 = 0) and the uniform
 // zetas of stages 0-2 (read from global memory: Z[1], Z[2], Z[4], Z[6]).
-constexpr int QZ_LDS = 546, QZ_ONE = 544, QZ_MINUS_I = 545, QZ_UNIFORM = 546;
+constexpr int QZ_LDS = 546, QZ_UNIFORM = 546;
+// G = 2: MAC register order (j7 = 0 registers first)
+constexpr int QMB_ORD[8] = {0, 1, 4, 5, 2, 3, 6, 7};
 FHE_DEV constexpr int tpos(int k) { return k + (k >> 5); }
-// LDS position of zeta entry k in the S9 layout: stages 6-9 (k >= 32) swap bit 2 by bit 4, so the 16
+// LDS position of zeta entry k: stages 6-9 (k >= 32) swap bit 2 by bit 4, so the 16
 // lanes of a read group (u = 16 b8 + 8 b7 + ..., b8 on lane bit 0) hit 16 different banks
 FHE_DEV constexpr int zsw(int k) { return k >= 32 ? k ^ (((k >> 4) & 1) << 2) : k; }
 
@@ -124,31 +126,6 @@ FHE_DEV void q_ct(cplx (&x)[8], cplx za, cplx zb) {
     }
 }
 
-// stage 9 (twiddle 1, forward and inverse alike): lane L0 = 0 keeps a + c, L0 = 1 keeps a - c,
-// with (a, c) the (L0 = 0, L0 = 1) pair: x' = partner + (L0 ? -x : x).
-FHE_DEV double dpp_swap1(double v) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, 0xB1, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), 0xB1, 0xF, 0xF, false);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-// partner + sgn * x with sgn = +1 (L0 = 0) or -1 (L0 = 1): one exact-product fma, identical to the
-// add of +-x.  The classic kernel builds sgn once and holds it; the multi-bit kernel rebuilds it from
-// the lane id at each use (volatile: not hoisted -- held across its loop it cost 13 % per batch).
-FHE_DEV double q_sgn9() {
-    uint32_t lane;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    const uint32_t hi = 0x3FF00000u | (lane << 31);
-    return __longlong_as_double((long long)((uint64_t)hi << 32));
-}
-// The accumulator is kept in units of 2^41 (device_math.h: tor_red_s, tor_digit_s).
-FHE_DEV void q_stage9(cplx (&x)[8], double sgn) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const cplx p = make_double2(dpp_swap1(x[r].x), dpp_swap1(x[r].y));
-        x[r] = make_double2(__fma_rn(sgn, x[r].x, p.x), __fma_rn(sgn, x[r].y, p.y));
-    }
-}
 // ---- B <-> C as register transposes (no LDS): register bits (2,1,0) <-> lane bits (5,4,3)
 // (lane bits 5, 4: qx_permlane<K> in device_math.h)
 // K = 3, 2: lanes with lane bit K set are whole 4-lane DPP banks (banks 2, 3 for K = 3; 1, 3 for
@@ -190,10 +167,10 @@ FHE_DEV void q_xpose_bc(cplx (&x)[8]) {
 // fho_blind_rotate: digits of acc itself, the MAC output times e - 1 per point); G = 2 multi-bit --
 // the digits of acc itself, and at the MAC the key bundle
 // K_rc = sum_B (e_B(j) - 1) G_B,rc per point, e_B(j) = zeta^((4j+1) m_B) as the oracle forms it:
-// i^((j >> 8) m) cmul(E[(4 (j mod 64) + 1) m], E[256 ((j >> 6) mod 4) m]).  A lane's phase-C points
-// are j = j0 + 256 (r & 1) + 128 ((r >> 1) & 1) + 64 (r >> 2), j0 = (h + 2 u') + 512 L0: the first
-// factor is one value per lane and pattern for the whole group (its sign (-1)^(L0 m) taken out), the
-// second is wave-uniform per register pair (scalar loads), and registers r, r + 1 differ by i^m.
+// i^((j >> 8) m) cmul(E[(4 (j mod 64) + 1) m], E[256 ((j >> 6) mod 4) m]).  A lane's MAC points are
+// j = j0 + 64 L2 + 128 ((r >> 1) & 1) + 256 (r & 1) + 512 (r >> 2), j0 = bitrev(idx) mod 64 from h and
+// u: the first factor is one value per lane and pattern for the whole group, the second one of the
+// wave-uniform E[256 k m] picked per lane, and the quarter turns i^((j >> 8) m) are per register.
 template <int G>
 __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_quad(const uint64_t* __restrict__ ms, int ms_stride,
                                                               const PbsDesc* __restrict__ desc,
@@ -205,9 +182,6 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
                                                               const cplx* __restrict__ zq,  // quad_zetas
                                                               const cplx* __restrict__ mono,  // E[4096] (G = 2)
                                                               uint64_t* __restrict__ out, int n) {
-    // S9 (classic): stage 9 in registers (see the layout table above); the multi-bit kernel keeps
-    // stage 9 across lane pairs
-    constexpr bool S9 = G == 1;
     // one LDS block (the kernel's only LDS object, so it starts at address 0): the polynomials'
     // exchange regions, the twiddles, the zetas (G = 2: the monomial lane factors)
     constexpr int QL_W = 2 * QX_SZ, QL_Z = QL_W + QTW_SZ, QL_M = QL_Z + QZ_LDS;
@@ -221,7 +195,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     // pattern, m = a_i: the factored CMUX)
     cplx* s_mono = s_lds + QL_M;
     for (int k = threadIdx.x; k < 512; k += 256) s_w[tpos(k)] = W[k];
-    for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[S9 ? zsw(k) : k] = zq[k];
+    for (int k = threadIdx.x; k < QZ_LDS; k += 256) s_z[zsw(k)] = zq[k];
     __syncthreads();
     const int ct = blockIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;  // w in an SGPR
@@ -230,23 +204,22 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
     const cplx* other = s_x[p ^ 1];
     const uint64_t* a_ct = ms + (size_t)ct * ms_stride;
     // lane bits of phases B and C (see the layout table above): L5 L4 L3 = (b3 b2 b1) in B, (b6 b5 b4)
-    // in C; L1 = b7 in both; b8, b0 on L0, L2 (S9) or L2, L0
+    // in C; L2 = b0, L1 = b7, L0 = b8 in both
     const int l0 = L & 1, l1 = (L >> 1) & 1, l2 = (L >> 2) & 1, l3 = (L >> 3) & 1, l4 = (L >> 4) & 1, l5 = (L >> 5) & 1;
-    const int lb8 = S9 ? l0 : l2, lb0 = S9 ? l2 : l0;
-    const int u = 16 * lb8 + 8 * l1 + 4 * l5 + 2 * l4 + l3;    // (b8 .. b4) in phase C
-    const int lowB = 8 * l5 + 4 * l4 + 2 * l3 + lb0;             // (b3 .. b0) in phase B
-    const int B3 = 4 * h + 2 * lb8 + l1, B6 = 32 * h + u;       // twisted-transform block bases of phases B, C
-    // zeta-table positions of stages 6-9 (S9: swizzled, zsw)
-    const int zB6 = S9 ? (B6 ^ (4 * lb8)) : B6;
-    const int z9 = S9 ? 288 + 128 * l2 + zB6 : 288 + 32 * h + u;  // stage-9 zeta of this lane (S9: b2 = 0)
+    const int u = 16 * l0 + 8 * l1 + 4 * l5 + 2 * l4 + l3;     // (b8 .. b4) in phase C
+    const int lowB = 8 * l5 + 4 * l4 + 2 * l3 + l2;              // (b3 .. b0) in phase B
+    const int B3 = 4 * h + 2 * l0 + l1, B6 = 32 * h + u;        // twisted-transform block bases of phases B, C
+    // zeta-table positions of stages 6-9 (swizzled, zsw); stage 9 in the MAC layout (L2 = b3, b2 = 0)
+    const int zB6 = B6 ^ (4 * l0);
+    const int z9 = 288 + 128 * l2 + zB6;
 
     // lane parts of the exchange addresses (register parts are compile-time constants)
     const int bA = fq(t);
-    const int bB = fq(512 * h + 256 * lb8 + 128 * l1 + lowB);
+    const int bB = fq(512 * h + 256 * l0 + 128 * l1 + lowB);
     // digit swap: any map onto this half's region positions works (both polynomials' waves use it);
-    // S9 takes lane bits 5..0 -> idx bits 5..0, registers -> bits 8..6 (conflict-free reads and writes)
-    const int bC = S9 ? fq(512 * h + L) : fq(512 * h + 16 * u + lb0);
-    constexpr int DSW = S9 ? 64 : 2;  // register part fq(DSW r)
+    // lane bits 5..0 -> idx bits 5..0, registers -> bits 8..6 (conflict-free reads and writes)
+    const int bC = fq(512 * h + L);
+    constexpr int DSW = 64;  // register part fq(DSW r)
 
     double acc[16];  // coefficients 128 r + t (f64 torus representatives)
     {
@@ -361,7 +334,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         // BSK ring head, in flight across phase C and the digit swap (G = 1: the whole own-row slice)
         constexpr int QR = G == 1 ? 8 : QMB_D;
         cplx Bq0[G == 1 ? 8 : QMBP * QR], Bq1[G == 1 ? 8 : QMBP * QR];
-        cplx em[G == 2 ? 3 : 1];  // G = 2: monomials of the current register pair, per pattern
+        cplx em[G == 2 ? 3 : 1];  // G = 2: monomials of the current registers (j7), per pattern
         cplx eb[G == 2 ? 3 : 1];  // G = 2: lane factors of the group, per pattern
         if constexpr (G == 1) {
 #pragma unroll
@@ -371,40 +344,26 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         for (int B = 0; B < QMBP; ++B) {
 #pragma unroll
             for (int d = 0; d < QR; ++d) {
-                Bq0[QMBP * d + B] = bm[B * 4 * 1024 + d * 64];
-                Bq1[QMBP * d + B] = bo[B * 4 * 1024 + d * 64];
+                Bq0[QMBP * d + B] = bm[B * 4 * 1024 + QMB_ORD[d] * 64];
+                Bq1[QMBP * d + B] = bo[B * 4 * 1024 + QMB_ORD[d] * 64];
             }
         }
         }
         q_ct<2>(x, s_z[32 + zB6], s_z[32 + zB6]);
         q_ct<1>(x, s_z[96 + zB6], s_z[96 + zB6]);
         q_ct<0>(x, s_z[160 + zB6], s_z[224 + zB6]);
-        if constexpr (S9) {
-            // stage 9 in registers: register bit 2 <-> lane bit 2 (b3 <-> b0), then the pairs (r, r + 4)
-            // with t = zeta c (oracle: cmul, then a + t, a - t); registers r = 2 b2 + b1 < 4, zeta
-            // index 288 + 128 b3 + 64 b2 + 32 h + u, times i for b1 = 1
+        {
+            // stage 9 in registers: register bit 2 <-> lane bit 2 (b3 <-> b0), then the fused
+            // butterflies of the pairs (r, r + 4); registers r = 2 b2 + b1 < 4, zeta index
+            // 288 + 128 b3 + 64 b2 + 32 h + u, times i for b1 = 1
 #pragma unroll
             for (int r = 0; r < 4; ++r) qx_banked<2>(x[r], x[r + 4]);
             const cplx z0 = s_z[z9], z1 = s_z[z9 + 64];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const cplx zb = (r >> 1) ? z1 : z0;
-                const cplx tt = cmul(x[r + 4], (r & 1) ? mul_i(zb) : zb);
-                const cplx a = x[r];
-                x[r] = make_double2(a.x + tt.x, a.y + tt.y);
-                x[r + 4] = make_double2(a.x - tt.x, a.y - tt.y);
+                dit_bfly(x[r], x[r + 4], (r & 1) ? mul_i(zb) : zb);
             }
-        } else {
-        // stage 9 across lane pairs: t = zeta c on the odd lane, the even lane keeps a (x 1, exact),
-        // then (a + t, a - t) by the shared DPP step; odd registers use i zeta (1 on even lanes)
-#pragma unroll
-        for (int r2 = 0; r2 < 4; ++r2) {
-            const int ia = (L & 1) ? z9 + 64 * r2 : QZ_ONE;
-            const int ib = (L & 1) ? ia : QZ_MINUS_I;
-            x[2 * r2] = cmul(x[2 * r2], s_z[ia]);
-            x[2 * r2 + 1] = cmul(x[2 * r2 + 1], mul_i(s_z[ib]));
-        }
-        q_stage9(x, q_sgn9());
         }
 
         // ---- swap Fourier digits with the other polynomial's wave of the same half, MAC with BSK
@@ -434,7 +393,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
         const cplx Eb = Ebn;
         Ebn = lane_factor(a_next);
-        // MAC layout (S9): registers (b0 b2 b1), lane bit 2 = b3, i.e. j bits 9, 7, 8 and 6 of the
+        // MAC layout: registers (b0 b2 b1), lane bit 2 = b3, i.e. j bits 9, 7, 8 and 6 of the
         // point: e = i^((j8 + 2 j9) a) cmul(Eb, E[256 (j6 + 2 j7) a]), the pair factor picked per lane
         const cplx Flo = l2 ? F[0] : make_double2(1.0, 0.0), Fhi = l2 ? F[2] : F[1];
         cplx elo, ehi;
@@ -449,39 +408,44 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             x[r] = cmul(x[r], w);
         }
         } else {
-        // key bundle per point (oracle cmul_acc, patterns in order), then the MAC; the slice of the
-        // next registers stream in behind (QR registers ahead), the monomials per register pair
+        // key bundle per point (oracle cmul_acc, patterns in order), then the MAC.  The monomials as
+        // in the classic MAC above: e_B = i^((j8 + 2 j9) m_B) cmul(E[(4 (j mod 64) + 1) m_B],
+        // E[256 (j6 + 2 j7) m_B]) with the pair factor (scalar loads) picked per lane; registers in the
+        // order QMB_ORD (j7 = 0, then 1: two monomials per pattern), the key slices streaming in QR
+        // registers ahead in that order
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int k = 0; k < 8; ++k) {
+            const int r = QMB_ORD[k];
             cplx Ko = make_double2(0.0, 0.0), Kt = make_double2(0.0, 0.0);
-            if (r == 0) {  // lane factors with the sign (-1)^(L0 m) of (j >> 8) m taken out
+            if (k == 0) {
 #pragma unroll
-                for (int B = 0; B < 3; ++B) {
-                    const cplx b = s_mono[(B * 2 + h) * 64 + L];
-                    const uint32_t sg = (uint32_t)(l0 & mB[B]) << 31;
-                    eb[B] = make_double2(neg_if(b.x, sg), neg_if(b.y, sg));
-                }
+                for (int B = 0; B < 3; ++B) eb[B] = s_mono[(B * 2 + h) * 64 + L];
             }
-            if (!(r & 1)) {  // pair r / 2 = 2 b1 + b2: natural bits 6, 7 of j are (b2, b1)
-                const uint32_t qk = ((r >> 2) & 1) + 2u * ((r >> 1) & 1);
+            if (k == 0 || k == 4) {
 #pragma unroll
                 for (int B = 0; B < 3; ++B) {
-                    if (qk == 0) {
-                        em[B] = eb[B];
+                    const uint32_t m = mB[B];
+                    cplx f;
+                    if (k == 0) {
+                        const cplx f1 = sload(mono, (256u * m) & 4095u);
+                        f = l2 ? f1 : make_double2(1.0, 0.0);
                     } else {
-                        em[B] = cmul(eb[B], sload(mono, (256u * qk * mB[B]) & 4095u));
+                        const cplx f2 = sload(mono, (512u * m) & 4095u), f3 = sload(mono, (768u * m) & 4095u);
+                        f = l2 ? f3 : f2;
                     }
+                    em[B] = cmul(eb[B], f);  // exact for f = 1
                 }
             }
 #pragma unroll
             for (int B = 0; B < QMBP; ++B) {
                 const int b3 = B % 3;
-                const cplx w = (r & 1) ? turn_sel_m1(em[b3], mB[b3]) : make_double2(em[b3].x - 1.0, em[b3].y);
-                const int sl = QMBP * (r % QR) + B;
+                const uint32_t tr = ((r & 1) ? mB[b3] : 0u) + ((r & 4) ? 2u * mB[b3] : 0u);
+                const cplx w = (r & 5) ? turn_sel_m1(em[b3], tr) : make_double2(em[b3].x - 1.0, em[b3].y);
+                const int sl = QMBP * (k % QR) + B;
                 const cplx Bm = Bq0[sl], Bo = Bq1[sl];
-                if (r + QR < 8) {
-                    Bq0[sl] = bm[B * 4 * 1024 + (r + QR) * 64];
-                    Bq1[sl] = bo[B * 4 * 1024 + (r + QR) * 64];
+                if (k + QR < 8) {
+                    Bq0[sl] = bm[B * 4 * 1024 + QMB_ORD[k + QR] * 64];
+                    Bq1[sl] = bo[B * 4 * 1024 + QMB_ORD[k + QR] * 64];
                 }
                 Ko = cmul_acc(Ko, Bm, w);
                 Kt = cmul_acc(Kt, Bo, w);
@@ -491,7 +455,7 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         }
 
         // ---- inverse FFT: stage 9 and phase C in registers, then the region again
-        if constexpr (S9) {
+        {
             // stages 9, 8, 7 in the MAC layout (registers b0 b2 b1), where their twiddles W[256 b0]
             // and W[128 b0 + 256 b1] are per register: 1 and W[256] = i exact (p = a + t, t a move),
             // W[128], W[384] = i W[128] wave-uniform; then register bit 2 <-> lane bit 2 back to the
@@ -512,12 +476,8 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
             dit_bfly(x[5], x[7], conj_(mul_i(w128)));
 #pragma unroll
             for (int r = 0; r < 4; ++r) qx_banked<2>(x[r], x[r + 4]);
-        } else {
-            q_stage9(x, q_sgn9());
-            q_dit<0>(x, s_w, tpos(256 * lb0));
-            q_dit<1>(x, s_w, tpos(128 * lb0));
         }
-        q_dit<2>(x, s_w, tpos(64 * lb0));
+        q_dit<2>(x, s_w, tpos(64 * l2));
         q_xpose_bc(x);
         __syncthreads();  // the other polynomial's waves have read this wave's digits
         if constexpr (G == 2)
@@ -574,18 +534,15 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
 }
 
 // Fourier BSK: blind-rotate layout (R = 4v + q, lane L' <-> idx = 4 (L' + 64 v) + q) -> quad layout
-// of the MAC, one workgroup per polynomial: (h, r, L) <-> idx = 512 h + 16 u + 2 r + L0 with
-// u = (b8 .. b4) from the lane bits as in phase C (multi-bit), or (S9, classic) idx = 512 h + 16 u +
-// 8 L2 + 4 r1 + 2 r0 + r2 with u = 16 L0 + 8 L1 + 4 L5 + 2 L4 + L3.
-__global__ __launch_bounds__(256) void k_bsk_to_quad(const cplx* __restrict__ src, cplx* __restrict__ dst, int s9) {
+// of the MAC, one workgroup per polynomial: (h, r, L) <-> idx = 512 h + 16 u + 8 L2 + 4 r1 + 2 r0 + r2
+// with u = (b8 .. b4) = 16 L0 + 8 L1 + 4 L5 + 2 L4 + L3 as in phase C.
+__global__ __launch_bounds__(256) void k_bsk_to_quad(const cplx* __restrict__ src, cplx* __restrict__ dst) {
     const cplx* s = src + (size_t)blockIdx.x * 1024;
     cplx* d = dst + (size_t)blockIdx.x * 1024;
     for (int k = threadIdx.x; k < 1024; k += 256) {
         const int hh = k >> 9, r = (k >> 6) & 7, L = k & 63;
-        const int lb8 = s9 ? (L & 1) : ((L >> 2) & 1);
-        const int u = 16 * lb8 + 8 * ((L >> 1) & 1) + 4 * ((L >> 5) & 1) + 2 * ((L >> 4) & 1) + ((L >> 3) & 1);
-        const int idx = s9 ? 512 * hh + 16 * u + 8 * ((L >> 2) & 1) + 4 * ((r >> 1) & 1) + 2 * (r & 1) + (r >> 2)
-                           : 512 * hh + 16 * u + 2 * r + (L & 1);
+        const int u = 16 * (L & 1) + 8 * ((L >> 1) & 1) + 4 * ((L >> 5) & 1) + 2 * ((L >> 4) & 1) + ((L >> 3) & 1);
+        const int idx = 512 * hh + 16 * u + 8 * ((L >> 2) & 1) + 4 * ((r >> 1) & 1) + 2 * (r & 1) + (r >> 2);
         const int q = idx & 3, Lp = (idx >> 2) & 63, v = idx >> 8;
         d[k] = s[(4 * v + q) * 64 + Lp];
     }
@@ -605,8 +562,8 @@ hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const Pbs
     return hipGetLastError();
 }
 
-hipError_t launch_bsk_to_quad(const cplx* bsk, int npoly, int grouping, cplx* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_bsk_to_quad, dim3(npoly), dim3(256), 0, s, bsk, out, grouping == 1 ? 1 : 0);
+hipError_t launch_bsk_to_quad(const cplx* bsk, int npoly, cplx* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_bsk_to_quad, dim3(npoly), dim3(256), 0, s, bsk, out);
     return hipGetLastError();
 }
 

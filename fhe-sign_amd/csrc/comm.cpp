@@ -493,7 +493,7 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
         return rc;
     }
     rc = launch_ksk_to_planes(n_ksk, (int)p.n, n_planes, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
-    if (!rc) rc = launch_bsk_to_quad(n_bsk, npoly, (int)p.grouping, n_quad, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = launch_bsk_to_quad(n_bsk, npoly, n_quad, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (rc) {
         drop_new();

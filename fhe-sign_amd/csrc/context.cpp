@@ -596,7 +596,7 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     FHE_HIP_CHECK(hipMemcpyAsync(d_std, sk->bsk.data(), sk->bsk.size() * 8, hipMemcpyHostToDevice, c->stream));
     FHE_HIP_CHECK(launch_bsk_to_fourier(d_std, npoly, c->d_W, c->d_psi, c->d_bsk, c->stream));
     FHE_HIP_CHECK(hipMalloc(&c->d_bsk_quad, (size_t)npoly * 1024 * sizeof(double2)));
-    FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, (int)p.grouping, c->d_bsk_quad, c->stream));
+    FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, c->d_bsk_quad, c->stream));
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
     FHE_HIP_CHECK(hipFree(d_std));
     if (!c->has_key || !(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {

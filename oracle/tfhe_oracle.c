@@ -200,8 +200,8 @@ void fho_fft_forward(double* x) {
  * negacyclic split X^1024 - i -> (X^512 - z)(X^512 + z) -> ..., i.e. radix-2 Cooley-Tukey stages
  * s = 0..9 on natural-order input, block b of stage s using zeta(s, b); output in the same
  * bit-reversed order and the same mathematical values as twist + fho_fft_forward.  Butterfly
- * (a, c) -> (p, m), p = a + z c with two fmas per component, m = 2a - p; the last stage (span 1)
- * is t = z c (cmul), (a + t, a - t). */
+ * (a, c) -> (p, m), p = a + z c with two fmas per component, m = 2a - p, in every stage (round 3
+ * and before, the last stage was t = z c (cmul), (a + t, a - t)). */
 void fho_fft_forward_twisted(double* x) {
     fho_tables_init();
     for (int st = 0; st < 10; ++st) {
@@ -212,13 +212,6 @@ void fho_fft_forward_twisted(double* x) {
                 double* p = x + 2 * (2 * h * b + j);
                 double* q = p + 2 * h;
                 const double ar = p[0], ai = p[1], cr = q[0], ci = q[1];
-                if (st == 9) {
-                    double tr, ti;
-                    cmul(cr, ci, z[0], z[1], &tr, &ti);
-                    p[0] = ar + tr; p[1] = ai + ti;
-                    q[0] = ar - tr; q[1] = ai - ti;
-                    continue;
-                }
                 const double pr = fma(z[0], cr, fma(-z[1], ci, ar));
                 const double pi = fma(z[0], ci, fma(z[1], cr, ai));
                 p[0] = pr; p[1] = pi;
@@ -469,14 +462,14 @@ static void fft_forward_twisted_simd(double* x) {
             }
         }
     }
-    for (int b = 0; b < 512; ++b) { /* stage 9 (span 1): t = z c, (a + t, a - t) */
+    for (int b = 0; b < 512; ++b) { /* stage 9 (span 1), the same fused butterfly */
         const double* z = g_zeta + 2 * (512 + b);
         double* p = x + 4 * b;
-        double tr, ti;
-        cmul(p[2], p[3], z[0], z[1], &tr, &ti);
-        const double ar = p[0], ai = p[1];
-        p[0] = ar + tr; p[1] = ai + ti;
-        p[2] = ar - tr; p[3] = ai - ti;
+        const double ar = p[0], ai = p[1], cr = p[2], ci = p[3];
+        const double pr = fma(z[0], cr, fma(-z[1], ci, ar));
+        const double pi = fma(z[0], ci, fma(z[1], cr, ai));
+        p[0] = pr; p[1] = pi;
+        p[2] = fma(2.0, ar, -pr); p[3] = fma(2.0, ai, -pi);
     }
 }
 
