@@ -353,16 +353,25 @@ __global__ __launch_bounds__(256, G == 1 ? QCL_W : QMB_W) void k_blind_rotate_qu
         q_ct<1>(x, s_z[96 + zB6], s_z[96 + zB6]);
         q_ct<0>(x, s_z[160 + zB6], s_z[224 + zB6]);
         {
-            // stage 9 in registers: register bit 2 <-> lane bit 2 (b3 <-> b0), then the fused
-            // butterflies of the pairs (r, r + 4); registers r = 2 b2 + b1 < 4, zeta index
-            // 288 + 128 b3 + 64 b2 + 32 h + u, times i for b1 = 1
+            // stage 9 in registers: register bit 2 <-> lane bit 2 (b3 <-> b0), then the butterflies of
+            // the pairs (r, r + 4); registers r = 2 b2 + b1 < 4, zeta index 288 + 128 b3 + 64 b2 +
+            // 32 h + u, times i for b1 = 1.  Classic: the fused butterfly; multi-bit: t = zeta c,
+            // (a + t, a - t) (oracle forward_twisted: the fused form costs this kernel 11-15 %)
 #pragma unroll
             for (int r = 0; r < 4; ++r) qx_banked<2>(x[r], x[r + 4]);
             const cplx z0 = s_z[z9], z1 = s_z[z9 + 64];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const cplx zb = (r >> 1) ? z1 : z0;
-                dit_bfly(x[r], x[r + 4], (r & 1) ? mul_i(zb) : zb);
+                const cplx zr = (r & 1) ? mul_i(zb) : zb;
+                if constexpr (G == 1) {
+                    dit_bfly(x[r], x[r + 4], zr);
+                } else {
+                    const cplx tt = cmul(x[r + 4], zr);
+                    const cplx a = x[r];
+                    x[r] = make_double2(a.x + tt.x, a.y + tt.y);
+                    x[r + 4] = make_double2(a.x - tt.x, a.y - tt.y);
+                }
             }
         }
 

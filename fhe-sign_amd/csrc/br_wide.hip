@@ -174,6 +174,18 @@ FHE_DEV void ct2(cplx (&x)[4], cplx z0, cplx z1) {
     dit_bfly(x[0], x[1], z1);
     dit_bfly(x[2], x[3], mul_i(z1));
 }
+// the multi-bit kernel's last two stages (phase E): stage 8 fused, stage 9 as t = z c, (a + t, a - t)
+// (oracle forward_twisted; the classic kernel's stage 9 is fused like the others)
+FHE_DEV void ct2_last_mb(cplx (&x)[4], cplx z0, cplx z1) {
+    dit_bfly(x[0], x[2], z0);
+    dit_bfly(x[1], x[3], z0);
+    const cplx t0 = cmul(x[1], z1), t1 = cmul(x[3], mul_i(z1));
+    const cplx a0 = x[0], a1 = x[2];
+    x[0] = cadd(a0, t0);
+    x[1] = csub(a0, t0);
+    x[2] = cadd(a1, t1);
+    x[3] = csub(a1, t1);
+}
 
 // two DIF stages on regs (r,r+2) then (r,r+1) with twiddles tw0 (r=0), tw1 (r=1), tw2
 FHE_DEV void dif2(cplx (&x)[4], cplx tw0, cplx tw1, cplx tw2) {
@@ -474,8 +486,8 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 y[r] = cross_other[xE ^ fx(r)];
             }
             WP_A();
-            ct2(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
-            ct2(y, ZT[8], ZT[9]);
+            ct2_last_mb(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
+            ct2_last_mb(y, ZT[8], ZT[9]);
             // ---- pointwise MAC (own digit x row p, then other digit x row 1 - p accumulated)
 #pragma unroll
             for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], Kown[r], y[r], Koth[r]);

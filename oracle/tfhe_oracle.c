@@ -200,9 +200,11 @@ void fho_fft_forward(double* x) {
  * negacyclic split X^1024 - i -> (X^512 - z)(X^512 + z) -> ..., i.e. radix-2 Cooley-Tukey stages
  * s = 0..9 on natural-order input, block b of stage s using zeta(s, b); output in the same
  * bit-reversed order and the same mathematical values as twist + fho_fft_forward.  Butterfly
- * (a, c) -> (p, m), p = a + z c with two fmas per component, m = 2a - p, in every stage (round 3
- * and before, the last stage was t = z c (cmul), (a + t, a - t)). */
-void fho_fft_forward_twisted(double* x) {
+ * (a, c) -> (p, m), p = a + z c with two fmas per component, m = 2a - p.  The last stage (span 1)
+ * is that fused butterfly for the classic blind rotation (fused9) and t = z c (cmul), (a + t, a - t)
+ * for the multi-bit one: the multi-bit throughput kernel runs 11-15 % slower with the fused form
+ * (same-box A/B, profiles/r3/quad_s9e_ab_r3al.txt), the classic kernels 0.5-1 % faster. */
+static void forward_twisted(double* x, int fused9) {
     fho_tables_init();
     for (int st = 0; st < 10; ++st) {
         const int h = 512 >> st;
@@ -212,6 +214,13 @@ void fho_fft_forward_twisted(double* x) {
                 double* p = x + 2 * (2 * h * b + j);
                 double* q = p + 2 * h;
                 const double ar = p[0], ai = p[1], cr = q[0], ci = q[1];
+                if (st == 9 && !fused9) {
+                    double tr, ti;
+                    cmul(cr, ci, z[0], z[1], &tr, &ti);
+                    p[0] = ar + tr; p[1] = ai + ti;
+                    q[0] = ar - tr; q[1] = ai - ti;
+                    continue;
+                }
                 const double pr = fma(z[0], cr, fma(-z[1], ci, ar));
                 const double pi = fma(z[0], ci, fma(z[1], cr, ai));
                 p[0] = pr; p[1] = pi;
@@ -258,14 +267,17 @@ void fho_poly_to_fourier(const uint64_t* poly, double* out) {
     fho_fft_forward(out);
 }
 
-/* digit polynomial (integer-valued doubles) -> Fourier, twisted forward transform */
-void fho_dpoly_to_fourier(const double* poly, double* out) {
+void fho_fft_forward_twisted(double* x) { forward_twisted(x, 1); }
+
+/* digit polynomial (integer-valued doubles) -> Fourier, twisted forward transform (classic form) */
+static void dpoly_to_fourier(const double* poly, double* out, int fused9) {
     for (int j = 0; j < 1024; ++j) {
         out[2 * j] = poly[j];
         out[2 * j + 1] = poly[j + 1024];
     }
-    fho_fft_forward_twisted(out);
+    forward_twisted(out, fused9);
 }
+void fho_dpoly_to_fourier(const double* poly, double* out) { dpoly_to_fourier(poly, out, 1); }
 
 /* round(x) mod 2^64, x finite.  rint = IEEE round-half-even (GPU: v_rndne_f64). */
 uint64_t fho_f64_to_torus(double x) {
@@ -794,7 +806,7 @@ void fho_blind_rotate(const fho_keys* k, const uint64_t* ct_small, const uint64_
             for (int mm = 0; mm < 2; ++mm) {
                 double* acc = mm ? acc1 : acc0;
                 for (int j = 0; j < FHO_N; ++j) dig[j] = tor_digit(acc[j], down, base, ibase);
-                fho_dpoly_to_fourier(dig, mm ? D1 : D0);
+                dpoly_to_fourier(dig, mm ? D1 : D0, 0);  /* multi-bit: cmul-form stage 9 */
             }
             const double* gi = k->bsk_f + (size_t)(3 * i) * 4 * FHO_HALF * 2;
             for (int w = 0; w < 2; ++w) {
