@@ -54,29 +54,6 @@ __device__ uint64_t g_wide_stamps[WS_CT][8][WS_IT][WS_N];
     } while (0)
 #endif
 
-// Wave priorities (s_setprio) of the two waves a SIMD holds (polynomial p = 0 and p = 1 of the same
-// q): with equal priority the older wave (p = 0) wins every issue conflict and the p = 1 waves are
-// the critical path (WIDE_STAMPS: they arrive ~900 cycles late at each barrier).  WIDE_PRIO
-// selects a schedule that hands the priority to the other polynomial's waves mid-phase.
-#ifndef WIDE_PRIO
-#define WIDE_PRIO 0
-#endif
-#define WP(a, b)                                 \
-    do {                                         \
-        if (p) __builtin_amdgcn_s_setprio(b);    \
-        else __builtin_amdgcn_s_setprio(a);      \
-    } while (0)
-#if WIDE_PRIO == 2
-#define WP_A() WP(0, 1)
-#define WP_B() WP(1, 0)
-#elif WIDE_PRIO == 3
-#define WP_A() WP(1, 0)
-#define WP_B() WP(0, 1)
-#else
-#define WP_A() do {} while (0)
-#define WP_B() do {} while (0)
-#endif
-
 namespace {
 // cross-wave regions: an XOR swizzle pos = A idx over GF(2) (bijective, no padding) under which the
 // D-side stores/loads and E-side loads/stores are all conflict-free by the gfx950 lane-group rules
@@ -323,9 +300,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     __syncthreads();
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
     bool red_in = false;  // the previous update's reduction, deferred to this step's digits (red_digit_s)
-#if WIDE_PRIO == 1
-    WP(0, 1);
-#endif
     for (int i = 0; i < n / (G == 1 ? 1 : WMBDIV); ++i) {  // n / G in the product build
         cplx x[4];
         cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
@@ -433,7 +407,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         ct2(x, ZT[0], ZT[1]);
         xpose_AB(x);                 // A -> B: regs <-> lane bits 5,4
         ct2(x, ZT[2], ZT[3]);
-        WP_B();
         xpose_dpp32(x);              // B -> C: regs <-> lane bits 3,2
         ct2(x, ZT[4], ZT[5]);
 #pragma unroll
@@ -485,7 +458,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 x[r] = cross[xE ^ fx(r)];
                 y[r] = cross_other[xE ^ fx(r)];
             }
-            WP_A();
             ct2_last_mb(x, ZT[8], ZT[9]);  // phase E: stages 8, 9
             ct2_last_mb(y, ZT[8], ZT[9]);
             // ---- pointwise MAC (own digit x row p, then other digit x row 1 - p accumulated)
@@ -495,7 +467,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         if constexpr (G == 1) WSTAMP(6);
 
         // ---- inverse FFT: E -> D (cross-wave) -> C -> B -> A (wave-private)
-        WP_B();
         {
             cplx a0 = x[0], c0 = x[1], a1 = x[2], c1 = x[3];
             x[0] = cadd(a0, c0); x[1] = csub(a0, c0);
@@ -519,7 +490,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         if constexpr (G == 1) WSTAMP(8);
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = inv[xD ^ fx(4 * r)];
-        WP_A();
         dit2(x, T[9], T[10], T[11]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) cd[cdpos(gL, r, aL)] = x[r];  // D -> C
@@ -527,7 +497,6 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = cd[cdpos(gL, aL, r)];
         dit2(x, T[6], T[7], T[8]);
-        WP_B();
         xpose_dpp32(x);              // C -> B
         dit2(x, T[3], T[4], T[5]);
         xpose_AB(x);                 // B -> A
