@@ -337,14 +337,52 @@ std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<
 }
 
 void Engine::flush() {
-    const size_t N = pending_.size();
-    if (N == 0) return;
+    if (pending_.empty()) return;
     const auto f0 = std::chrono::steady_clock::now();
     if (trace_) {
         fprintf(stderr, "[host] %zu run() calls, %.3f ms inside run() since the last flush\n", run_calls_, run_ns_ * 1e-6);
         run_ns_ = 0.0;
         run_calls_ = 0;
     }
+    // Dead nodes: an output slot referenced by nothing but its own node (no later node reads it, no
+    // block of the program holds it -- e.g. a carry-chain state whose every consumer folded to a
+    // constant on the host) can never be read, so the node is dropped; newest first, so dropping a
+    // node releases its inputs and can make their producers dead in turn.
+    {
+        const size_t N0 = pending_.size();
+        std::vector<int32_t> remap(N0, -1);
+        std::vector<char> dead(N0, 0);
+        for (size_t k = N0; k-- > 0;)
+            if (pending_[k].hold[0].use_count() == 1) {
+                dead[k] = 1;
+                pending_[k].hold.clear();
+            }
+        size_t live = 0;
+        for (size_t k = 0; k < N0; ++k)
+            if (!dead[k]) remap[k] = (int32_t)live++;
+        if (live < N0) {
+            dead_nodes += N0 - live;
+            std::vector<Pending> kept;
+            kept.reserve(live);
+            for (size_t k = 0; k < N0; ++k) {
+                if (dead[k]) continue;
+                Pending& n = pending_[k];
+                for (int32_t& d : n.deps) {
+                    engine_check(remap[d] >= 0, "live node reads a dropped node");
+                    d = remap[d];
+                }
+                n.hold[0]->node = remap[k];
+                kept.push_back(std::move(n));
+            }
+            pending_.swap(kept);
+        }
+        if (pending_.empty()) {
+            pending_dependent_ = 0;
+            eager_ok_ = true;
+            return;
+        }
+    }
+    const size_t N = pending_.size();
     std::vector<std::vector<int32_t>> deps(N);
     for (size_t k = 0; k < N; ++k) deps[k] = pending_[k].deps;
     // a fanned-out level's round is one latency-kernel round on every rank
@@ -387,7 +425,8 @@ void Engine::flush() {
     hip_check(hipMemcpyAsync(dev, h, ndesc * sizeof(PbsDesc), hipMemcpyHostToDevice, ctx_->stream), "desc copy");
     hip_check(hipEventRecord(desc_ev_[desc_turn_], ctx_->stream), "desc event");
     if (trace_)
-        fprintf(stderr, "[flush] %zu nodes, %zu levels, scheduled in %.3f ms\n", N, lv.size(),
+        fprintf(stderr, "[flush] %zu nodes (%llu dropped so far), %zu levels, scheduled in %.3f ms\n", N,
+                (unsigned long long)dead_nodes, lv.size(),
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count());
     for (size_t li = 0; li < lv.size(); ++li) {
         const size_t G = lv[li].size();

@@ -128,6 +128,7 @@ public:
     bool eager_head_ok() const { return eager_ok_ && pending_.empty(); }
     // statistics
     uint64_t pbs_count = 0, levels = 0, fanout_levels = 0;
+    uint64_t dead_nodes = 0;  // recorded bootstraps dropped at flush: nothing could read their outputs
     // bootstraps per launched level, in launch order (fhe_ctx_level_log; the bench's CPU replay)
     std::vector<uint32_t> level_log;
     static constexpr size_t kLevelLogCap = 1u << 20;
