@@ -179,17 +179,19 @@ __global__ __launch_bounds__(256) void k_ks_mfma(const int8_t* __restrict__ digi
 
 int ks_plane_tiles(int n) { return (n + 1 + 15) / 16; }
 size_t ks_planes_bytes(int n) { return (size_t)8 * ks_plane_tiles(n) * KS_KT * 1024; }
-#ifndef KS_CW
-#define KS_CW 2  // ciphertext tiles per wave
-#endif
+// ciphertext tiles per wave: 4 for large batches (each plane fragment feeds 4 MFMAs: 3.8 -> 3.2 ms
+// per 32768, profiles/r3/ks_cw4_ab_r3aq.txt; 296 registers, one wave per SIMD), 2 for latency
+// levels (3 workgroups per CU; CW = 4 there: 40 -> 60 us per 256)
+constexpr int KS_CW_BIG = 4, KS_CW_SMALL = 2, KS_CW_BIG_FROM = 4096;
 #ifndef KS_MAX_SPLITS
 #define KS_MAX_SPLITS 16  // contraction splits for small batches (KS_KT / 16 = 10 k-tiles each)
 #endif
 static_assert(KS_KT % KS_MAX_SPLITS == 0 && KS_KT / KS_MAX_SPLITS >= 2, "split k-tile spans");
-// k_ks_mfma reads the digit fragments of every tile its grid covers (64 KS_CW ciphertexts per
-// workgroup column, 4 KS_CW 16-row tiles), including tiles past the batch: size for whole columns
+// k_ks_mfma reads the digit fragments of every tile its grid covers (64 CW ciphertexts per
+// workgroup column, 4 CW 16-row tiles), including tiles past the batch: size for whole columns of
+// the larger CW
 size_t ks_digits_bytes(int count) {
-    return (size_t)((count + 64 * KS_CW - 1) / (64 * KS_CW)) * 4 * KS_CW * KS_KT * 1024;
+    return (size_t)((count + 64 * KS_CW_BIG - 1) / (64 * KS_CW_BIG)) * 4 * KS_CW_BIG * KS_KT * 1024;
 }
 
 hipError_t launch_ksk_to_planes(const uint64_t* ksk, int n, int8_t* planes, hipStream_t s) {
@@ -201,7 +203,8 @@ hipError_t launch_ksk_to_planes(const uint64_t* ksk, int n, int8_t* planes, hipS
 hipError_t launch_keyswitch_mfma(const uint64_t* in, const PbsDesc* desc, int count, const int8_t* planes,
                                  int8_t* digits, uint64_t* body, uint64_t* small, int stride, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    const int tiles = ks_plane_tiles(n), xb = (count + 64 * KS_CW - 1) / (64 * KS_CW);
+    const int cw = count >= KS_CW_BIG_FROM ? KS_CW_BIG : KS_CW_SMALL;
+    const int tiles = ks_plane_tiles(n), xb = (count + 64 * cw - 1) / (64 * cw);
     // contraction splits: the fewest (of 1, 2, 4, 8, 16; 160 k-tiles) that give >= 768 workgroups
     // (3 per CU)
     int splits = 1;
@@ -211,8 +214,12 @@ hipError_t launch_keyswitch_mfma(const uint64_t* in, const PbsDesc* desc, int co
         hipLaunchKernelGGL(k_ks_digits<true>, dim3(count), dim3(256), 0, s, nullptr, desc, digits, body, init, stride, n);
     else
         hipLaunchKernelGGL(k_ks_digits<false>, dim3(count), dim3(256), 0, s, in, nullptr, digits, body, init, stride, n);
-    hipLaunchKernelGGL(k_ks_mfma<KS_CW>, dim3(xb, tiles, splits), dim3(256), 0, s, digits, body, planes, tiles, count,
-                       n, small, stride, KS_KT / splits);
+    if (cw == KS_CW_BIG)
+        hipLaunchKernelGGL(k_ks_mfma<KS_CW_BIG>, dim3(xb, tiles, splits), dim3(256), 0, s, digits, body, planes, tiles,
+                           count, n, small, stride, KS_KT / splits);
+    else
+        hipLaunchKernelGGL(k_ks_mfma<KS_CW_SMALL>, dim3(xb, tiles, splits), dim3(256), 0, s, digits, body, planes, tiles,
+                           count, n, small, stride, KS_KT / splits);
     return hipGetLastError();
 }
 

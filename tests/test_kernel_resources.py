@@ -1,4 +1,4 @@
-"""Occupancy guard for the blind-rotate kernels (CPU: compiles device code, reads the code-object
+"""Occupancy guard for the blind-rotate and keyswitch kernels (CPU: compiles device code, reads the code-object
 descriptors).  Each kernel is designed for a fixed occupancy: a register total
 (arch VGPR + AGPR) above 256 silently halves occupancy -- it happened once through a VGPR->AGPR
 spill (next_free_vgpr 258) and cost 50% of throughput -- and scratch spills in the CMUX loop
@@ -35,6 +35,8 @@ def descriptors(src, tmp_path, flags=()):
     ("br_wide.hip", (), "k_blind_rotate_wideILi2", 1, 256, 0),  # the same, multi-bit
     ("br_quad.hip", (), "k_blind_rotate_quadILi1", 3, 168, 0),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
     ("br_quad.hip", (), "k_blind_rotate_quadILi2", 2, 256, 0),  # multi-bit: 2 per CU, 2 waves/SIMD, deeper BSK ring
+    ("ks_mfma.hip", (), "k_ks_mfmaILi2", 3, 168, 0),  # keyswitch, latency levels: 3 workgroups per CU
+    ("ks_mfma.hip", (), "k_ks_mfmaILi4", 2, 512, 0),  # keyswitch, large batches: one wave per SIMD, no spill
 ])
 def test_blind_rotate_occupancy(tmp_path, src, flags, kernel, lds_per_cu_ok, max_regs, max_scratch):
     d = descriptors(os.path.join(CSRC, src), tmp_path, flags)
