@@ -68,9 +68,30 @@ __global__ __launch_bounds__(256) void k_ks_digits(const uint64_t* __restrict__ 
                                                    uint64_t* __restrict__ init, int stride, int n) {
     __shared__ int8_t sd[KS_K];
     const int ct = blockIdx.x;
-    for (int j = threadIdx.x; j < 2048; j += 256) {
-        const uint64_t a = ks_input<DESC>(in, desc, ct, j);
-        uint64_t v = (((a >> (63 - 15)) + 1) >> 1) & 0x7fffull;  // round to the top 15 bits
+    // the 8 mask words of this thread (j = threadIdx.x + 256 it), every term's loads issued together
+    // (ks_input's per-word term loop waited for each word's loads in turn: 18 us per latency level)
+    uint64_t av[8];
+    if constexpr (DESC) {
+        const PbsDesc& d = desc[ct];
+#pragma unroll
+        for (int it = 0; it < 8; ++it) av[it] = 0ull;
+#pragma unroll
+        for (int tm = 0; tm < kMaxTerms; ++tm) {
+            if (tm < (int)d.nterms) {  // uniform
+                const uint64_t* src = d.src[tm];
+                const uint64_t c = (uint64_t)(int64_t)d.coef[tm];
+#pragma unroll
+                for (int it = 0; it < 8; ++it) av[it] += c * src[threadIdx.x + 256 * it];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) av[it] = in[(size_t)ct * 2049 + threadIdx.x + 256 * it];
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int j = threadIdx.x + 256 * it;
+        uint64_t v = (((av[it] >> (63 - 15)) + 1) >> 1) & 0x7fffull;  // round to the top 15 bits
 #pragma unroll
         for (int l = 4; l >= 0; --l) {
             int d = (int)(v & 7u);
