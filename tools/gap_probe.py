@@ -22,6 +22,13 @@ if sys.argv[1:2] == ["--analyze"]:
             last = max(last, e)
         span = sel[-1][1] - sel[0][0]
         big = sorted(gaps)[-5:]
+        if os.environ.get("GAP_DETAIL"):  # where the gaps sit: (offset from t0, gap, kernel after it)
+            last = sel[0][0]
+            for s, e, n in sel:
+                if s - last > 200_000:
+                    print(f"   gap {(s - last) / 1e6:.2f} ms at +{(s - t0) / 1e6:.2f} ms before {n.split('(')[0][:40]}")
+                last = max(last, e)
+            print(f"   last kernel ends at +{(sel[-1][1] - t0) / 1e6:.2f} ms of {(t1 - t0) / 1e6:.2f}")
         print(f"{name}: wall {(t1 - t0) / 1e6:.1f} ms, first kernel at +{(sel[0][0] - t0) / 1e6:.1f} ms, kernel span "
               f"{span / 1e6:.1f} ms, busy {busy / 1e6:.1f} ms, idle gaps {sum(gaps) / 1e6:.1f} ms over {len(gaps)} "
               f"(largest {[round(g / 1e6, 2) for g in big]}), {len(sel)} kernels")
@@ -39,8 +46,9 @@ marks = []
 def mark(name, fn):
     ctx.sync()
     t0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
-    fn(); ctx.sync()
+    r = fn(); ctx.sync()  # r held across the sync: the engine drops bootstraps nothing can read
     t1 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
+    del r
     marks.append((name, t0, t1))
     print(name, (t1 - t0) / 1e6, "ms", flush=True)
 for _ in range(2):
