@@ -99,7 +99,7 @@ def host_cores():
 
 # ops whose launched levels are replayed through the C restatement (measured), and ops whose CPU time
 # is projected from the measured per-PBS time level by level (too long to replay in a default run)
-CPU_REPLAY_OPS = ("biguint256_add_fast", "sign_fhe_with_k0_v0_compat")
+CPU_REPLAY_OPS = ("biguint256_add_fast", "sign_fhe_with_k0_v0_compat", "sub256", "shr256_encrypted", "and256")
 CPU_PROJECT_OPS = ("biguint256_mul_compat", "biguint256_mul_fast", "sign_fhe_v0_compat", "div256_by_u32")
 
 
@@ -228,6 +228,18 @@ def ops_legs(ck, ctx, seed):
     D256 = FheUint256.try_encrypt(du128, ck)
     leg("div256_by_encrypted", lambda: A256.div_rem(D256),
         lambda r: (r[0].decrypt(ck), r[1].decrypt(ck)) == (a // du128, a % du128))
+    # north_star's other 256-bit ops (sub, encrypted shift, and; the reference applies them at 32 bits,
+    # src/perf_test.rs:36,48; shift amount mod the width, src/biguint.rs:494-498)
+    B256 = FheUint256.try_encrypt(b, ck)
+    m256 = (1 << 256) - 1
+    sh = rng.randrange(256)
+    S256 = FheUint256.try_encrypt(sh, ck)
+    cl256 = rng.getrandbits(256)
+    leg("sub256", lambda: A256 - B256, lambda r: r.decrypt(ck) == (a - b) & m256)
+    leg("shr256_encrypted", lambda: A256 >> S256, lambda r: r.decrypt(ck) == a >> sh)
+    leg("shl256_encrypted", lambda: A256 << S256, lambda r: r.decrypt(ck) == (a << sh) & m256)
+    leg("and256", lambda: A256 & B256, lambda r: r.decrypt(ck) == a & b)
+    leg("and256_clear", lambda: A256 & cl256, lambda r: r.decrypt(ck) == a & cl256)
     X32 = FheUint32.try_encrypt(1344, ck)  # src/perf_test.rs:14-15,54 (README.md:114: 1121 s on CPU)
     leg("fheuint32_div5", lambda: X32 / 5, lambda r: r.decrypt(ck) == 268)
     leg("fheuint32_add", lambda: X32 + FheUint32.try_encrypt(5, ck), lambda r: r.decrypt(ck) == 1349)
@@ -382,9 +394,8 @@ def pbs_leg(a, kind, dist, rank, world, device):
     lid = ctx.lut([(m + 1) % 16 for m in range(16)])
     B = a.batch
     ck.seed_encryption(a.seed + rank, 100)
-    base = np.stack([ck.encrypt_block(m % 16) for m in range(256)])
-    reps = (B + 255) // 256
-    cts = np.ascontiguousarray(np.concatenate([base] * reps)[:B])
+    # B distinct encryptions (distinct masks, hence distinct monomial-table gathers per step)
+    cts = ck.encrypt_blocks(np.arange(B) % 16)
     d_in = ctx.alloc(cts.nbytes)
     d_out = ctx.alloc(cts.nbytes)
     d_lut = ctx.alloc(B * 4)
@@ -426,7 +437,7 @@ def pbs_leg(a, kind, dist, rank, world, device):
     # correctness spot check of the last step (decrypt a sample)
     out = np.zeros_like(cts)
     ctx.d2h(out, d_out)
-    ok = all(ck.decrypt_block(out[i]) == (i % 256 % 16 + 1) % 16 for i in range(0, B, max(1, B // 64)))
+    ok = all(ck.decrypt_block(out[i]) == (i % 16 + 1) % 16 for i in range(0, B, max(1, B // 64)))
     if not ok:
         raise SystemExit(f"bench: decryption check failed ({kind})")
     for d in (d_in, d_out, d_lut):
@@ -438,7 +449,9 @@ def pbs_leg(a, kind, dist, rank, world, device):
     achieved = B * flops_pbs / (br_ms * 1e-3) / 1e12
     ggsw = n if kind == "classic" else n // 2 * 3
     bsk_bytes = ggsw * 4 * 1024 * 16
-    hbm_bytes = bsk_bytes + B * ((n + 1) * 2 + 2049 * 8 + 4)
+    # algorithmic HBM bytes of one blind-rotate launch: the Fourier BSK once, per PBS the keyswitched
+    # LWE u64[n + 1] in, the big LWE u64[2049] out and its u32 LUT index
+    hbm_bytes = bsk_bytes + B * ((n + 1) * 8 + 2049 * 8 + 4)
     # every workgroup streams the whole Fourier BSK from L2 (one ciphertext per workgroup): the bytes
     # the blind rotate moves L2 -> CU per launch, and their rate against the L2 peak
     l2_bytes = B * bsk_bytes

@@ -25,6 +25,9 @@ template <class F>
 int guarded(F&& f) {
     try {
         return f();
+    } catch (const EngineError& e) {  // carries its status (FHE_ERR_TIMEOUT, FHE_ERR_HIP)
+        set_error(e.what());
+        return e.code;
     } catch (const std::exception& e) {
         set_error(e.what());
         return FHE_ERR_INVALID;
@@ -394,7 +397,7 @@ int fhe_ctx_level_log(fhe_ctx* c, uint32_t* sizes, size_t cap, size_t* n, int re
     }
     const std::vector<uint32_t>& log = c->engine->level_log;
     *n = log.size();
-    std::memcpy(sizes, log.data(), std::min(cap, log.size()) * 4);
+    if (cap && !log.empty()) std::memcpy(sizes, log.data(), std::min(cap, log.size()) * 4);
     if (reset) c->engine->level_log.clear();
     return FHE_OK;
 }

@@ -49,10 +49,19 @@ int nccl_settle(ncclComm_t comm, ncclResult_t r, const char* what, uint32_t time
 // communicator is aborted and detached (a peer that died after the enqueue cannot hang this rank).
 int comm_wait_impl(fhe_ctx* c, const char* what) {
     ncclComm_t cm = (ncclComm_t)c->comm;
-    const auto t0 = std::chrono::steady_clock::now();
+    auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         const hipError_t q = hipStreamQuery(c->stream);
-        if (q == hipSuccess) return FHE_OK;
+        if (q == hipSuccess) {
+            c->prog_done = c->prog_rec;
+            return FHE_OK;
+        }
+        // the deadline counts time without progress: a completed level mark restarts it
+        while (c->prog_done < c->prog_rec &&
+               hipEventQuery(c->prog_ev[c->prog_done % fhe_ctx::kProgRing]) == hipSuccess) {
+            ++c->prog_done;
+            t0 = std::chrono::steady_clock::now();
+        }
         if (q != hipErrorNotReady) {
             set_error(std::string(what) + ": " + hipGetErrorString(q));
             return FHE_ERR_HIP;
@@ -71,8 +80,8 @@ int comm_wait_impl(fhe_ctx* c, const char* what) {
             c->comm = nullptr;
             c->nranks = 1;
             c->rank = 0;
-            set_error(std::string(what) + ": collective did not complete within " + std::to_string(c->comm_timeout_ms) +
-                      " ms (communicator aborted)");
+            set_error(std::string(what) + ": no progress within " + std::to_string(c->comm_timeout_ms) +
+                      " ms (a collective did not complete; communicator aborted)");
             return FHE_ERR_TIMEOUT;
         }
         std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -140,12 +149,41 @@ int fhe_ctx::allgather(uint64_t* buf, size_t words) {
                        "ncclAllGather", comm_timeout_ms, false);
 }
 
+void fhe_ctx::mark_progress() {
+    if (!comm) return;
+    if (!prog_ev[0])
+        for (auto& e : prog_ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    if (!prog_ev[kProgRing - 1]) return;
+    // a full ring re-records the newest mark (marks complete in stream order, so it still stands for
+    // "everything up to here")
+    const uint64_t slot = prog_rec - prog_done < (uint64_t)kProgRing ? prog_rec++ : prog_rec - 1;
+    (void)hipEventRecord(prog_ev[slot % kProgRing], stream);
+}
+
+int fhe_ctx::allreduce_min_u8(uint8_t* flags, size_t n) {
+    if (!comm || n == 0) return FHE_OK;
+    uint8_t* d = nullptr;
+    FHE_HIP_CHECK(hipMalloc(&d, n));
+    ncclComm_t cm = (ncclComm_t)comm;
+    int rc = hipMemcpyAsync(d, flags, n, hipMemcpyHostToDevice, stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc)
+        rc = nccl_settle(cm, ncclAllReduce(d, d, n, ncclUint8, ncclMin, cm, stream), "ncclAllReduce (dead nodes)",
+                         comm_timeout_ms, false);
+    if (!rc) rc = hipMemcpyAsync(flags, d, n, hipMemcpyDeviceToHost, stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = comm_wait_impl(this, "ncclAllReduce (dead nodes)");
+    if (comm) (void)hipStreamSynchronize(stream);
+    (void)hipFree(d);
+    return rc;
+}
+
 void fhe_ctx::release_comm() {
     if (comm) {
         (void)hipStreamSynchronize(stream);
         (void)ncclCommDestroy((ncclComm_t)comm);
         comm = nullptr;
     }
+    prog_rec = prog_done = 0;
     nranks = 1;
     rank = 0;
 }
@@ -382,6 +420,16 @@ int fhe_ctx_attach_comm_timeout(fhe_ctx* c, const uint8_t id[FHE_COMM_ID_BYTES],
 
 int fhe_ctx_attach_comm(fhe_ctx* c, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank) {
     return fhe_ctx_attach_comm_timeout(c, id, nranks, rank, FHE_COMM_DEFAULT_TIMEOUT_MS);
+}
+
+int fhe_ctx_set_comm_timeout(fhe_ctx* c, uint32_t timeout_ms) {
+    if (!c || timeout_ms == 0) return FHE_ERR_INVALID;
+    if (!c->comm) {
+        set_error("no communicator attached");
+        return FHE_ERR_INVALID;
+    }
+    c->comm_timeout_ms = timeout_ms;
+    return FHE_OK;
 }
 
 int fhe_ctx_detach_comm(fhe_ctx* c) {

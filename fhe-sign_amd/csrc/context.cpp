@@ -565,6 +565,8 @@ void fhe_ctx_destroy(fhe_ctx* c) {
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto ev : c->prog_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -650,8 +652,9 @@ int fhe_ctx_sync(fhe_ctx* c) {
             return FHE_ERR_HIP;
         }
     }
-    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
-    return FHE_OK;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    // bounded while a communicator is attached (fhe_ctx::wait_stream): FHE_ERR_TIMEOUT, not a hang
+    return c->wait_stream("fhe_ctx_sync");
 }
 
 int fhe_lut_register(fhe_ctx* c, const uint32_t* table, uint32_t table_len, uint32_t* id) {

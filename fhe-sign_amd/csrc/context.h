@@ -103,9 +103,19 @@ struct fhe_ctx {
     // in-place all-gather of nranks segments of `words` u64 each (segment `rank` is local)
     int allgather(uint64_t* buf, size_t words);
     void release_comm();
-    // wait for the stream; with a communicator attached, bounded by comm_timeout_ms (a collective
-    // whose peer died is aborted instead of hanging this rank)
+    // wait for the stream; with a communicator attached, bounded by comm_timeout_ms WITHOUT PROGRESS
+    // (a collective whose peer died is aborted instead of hanging this rank; a long but healthy
+    // flush keeps completing progress marks and is never cut off)
     int wait_stream(const char* what);
+    // progress marks: an event recorded on the stream after every launched level while a
+    // communicator is attached; wait_stream restarts its deadline whenever one completes
+    static constexpr int kProgRing = 32;
+    hipEvent_t prog_ev[kProgRing] = {};
+    uint64_t prog_rec = 0, prog_done = 0;
+    void mark_progress();
+    // *flags (one byte per entry) = min over the ranks, in place (one all-reduce; a no-op without a
+    // communicator).  The engine's dead-node agreement.
+    int allreduce_min_u8(uint8_t* flags, size_t n);
 
     int ensure_ms(size_t count);
     int ensure_ks(size_t count);

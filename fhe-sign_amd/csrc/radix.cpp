@@ -29,7 +29,12 @@ void engine_check(bool ok, const char* what) {
 }
 
 static void hip_check(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+    if (e != hipSuccess) throw EngineError(FHE_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static void wait_check(fhe_ctx* c, const char* what) {
+    const int rc = c->wait_stream(what);
+    if (rc != FHE_OK) throw EngineError(rc, last_error());
 }
 
 // ============================================================================ block pool
@@ -348,15 +353,32 @@ void Engine::flush() {
     // block of the program holds it -- e.g. a carry-chain state whose every consumer folded to a
     // constant on the host) can never be read, so the node is dropped; newest first, so dropping a
     // node releases its inputs and can make their producers dead in turn.
+    // The output counts come from host reference counts, i.e. from how long the caller keeps its
+    // handles: under a real communicator the ranks could disagree (one rank still holding an
+    // intermediate), and every rank must schedule the same levels (the split, the chunk and the
+    // all-gather size all follow from them).  So the ranks agree first: a node is dropped only if it
+    // is dead on EVERY rank (one byte-wise min all-reduce).  The result is closed under the cascade --
+    // a node kept on some rank keeps its producers' outputs referenced on that rank.
     {
         const size_t N0 = pending_.size();
         std::vector<int32_t> remap(N0, -1);
-        std::vector<char> dead(N0, 0);
-        for (size_t k = N0; k-- > 0;)
-            if (pending_[k].hold[0].use_count() == 1) {
+        std::vector<uint8_t> dead(N0, 0);
+        {
+            // count the references without releasing any: refs[k] = holders of node k's output slot
+            std::vector<long> refs(N0);
+            for (size_t k = 0; k < N0; ++k) refs[k] = pending_[k].hold[0].use_count();
+            for (size_t k = N0; k-- > 0;) {
+                if (refs[k] != 1) continue;
                 dead[k] = 1;
-                pending_[k].hold.clear();
+                for (size_t h = 1; h < pending_[k].hold.size(); ++h) {
+                    const int64_t prod = pending_[k].hold[h]->node;
+                    if (prod >= 0) --refs[prod];
+                }
             }
+        }
+        if (ctx_->comm) engine_check(ctx_->allreduce_min_u8(dead.data(), N0) == FHE_OK, "dead-node agreement");
+        for (size_t k = N0; k-- > 0;)
+            if (dead[k]) pending_[k].hold.clear();
         size_t live = 0;
         for (size_t k = 0; k < N0; ++k)
             if (!dead[k]) remap[k] = (int32_t)live++;
@@ -451,6 +473,7 @@ void Engine::flush() {
                       "scatter");
             fanout_levels += 1;
         }
+        ctx_->mark_progress();
         pbs_count += G;
         levels += 1;
         if (level_log.size() < kLevelLogCap) level_log.push_back((uint32_t)G);
@@ -546,7 +569,7 @@ void Engine::download(const Block& b, uint64_t* ct) {
     engine_check(!b.trivial() && !b.lazy(), "download of a trivial or lazy block");
     flush();
     hip_check(hipMemcpyAsync(ct, b.slot->p, kBigCt * 8, hipMemcpyDeviceToHost, ctx_->stream), "download");
-    if (ctx_->wait_stream("download") != FHE_OK) throw std::runtime_error(last_error());
+    wait_check(ctx_, "download");
 }
 
 void Engine::download_many(const std::vector<const Block*>& blocks, uint64_t* cts) {
@@ -570,12 +593,12 @@ void Engine::download_many(const std::vector<const Block*>& blocks, uint64_t* ct
     hip_check(hipMemcpyAsync(d_src, src.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice, ctx_->stream), "download");
     hip_check(launch_gather_blocks(d_src, d_up_, (int)n, ctx_->stream), "download gather");
     hip_check(hipMemcpyAsync(cts, d_up_, n * kBigCt * 8, hipMemcpyDeviceToHost, ctx_->stream), "download");
-    if (ctx_->wait_stream("download") != FHE_OK) throw std::runtime_error(last_error());
+    wait_check(ctx_, "download");
 }
 
 void Engine::sync() {
     flush();
-    if (ctx_->wait_stream("sync") != FHE_OK) throw std::runtime_error(last_error());
+    wait_check(ctx_, "sync");
 }
 
 Blocks Engine::adopt_device(const uint64_t* d_cts, size_t n) {

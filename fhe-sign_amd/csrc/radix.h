@@ -14,6 +14,8 @@
 #include <cstdint>
 #include <functional>
 #include <memory>
+#include <stdexcept>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -163,6 +165,12 @@ private:
 };
 
 void engine_check(bool ok, const char* what);
+// An engine failure that carries its C-ABI status (e.g. FHE_ERR_TIMEOUT from a bounded stream wait):
+// the C entry points return `code` instead of the generic FHE_ERR_INVALID.
+struct EngineError : std::runtime_error {
+    int code;
+    EngineError(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
 // The Engine's level scheduler (deps[i]: earlier nodes node i reads; mode 0 backward, 1 forward).
 std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<int32_t>>& deps, int mode,
                                                   size_t round = 256);

@@ -72,6 +72,7 @@ _SIGNATURES = [
     ("fhe_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("fhe_ctx_attach_comm", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     ("fhe_ctx_attach_comm_timeout", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_uint32]),
+    ("fhe_ctx_set_comm_timeout", C.c_int, [C.c_void_p, C.c_uint32]),
     ("fhe_ctx_broadcast_server_key", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_ctx_broadcast_radix", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int]),
     ("fhe_ctx_broadcast_biguint", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int]),
@@ -154,7 +155,14 @@ _lib = None
 
 
 class FheError(RuntimeError):
-    pass
+    """a negative status of the C ABI; `code` is the FHE_ERR_* value"""
+
+    def __init__(self, msg: str, code: int = 0):
+        super().__init__(msg)
+        self.code = code
+
+
+FHE_ERR_TIMEOUT = -6
 
 
 def load() -> C.CDLL:
@@ -179,7 +187,7 @@ def declared_symbols() -> list[str]:
 def check(rc: int) -> None:
     if rc != 0:
         msg = load().fhe_last_error()
-        raise FheError(f"fhe error {rc}: {msg.decode() if msg else ''}")
+        raise FheError(f"fhe error {rc}: {msg.decode() if msg else ''}", rc)
 
 
 def ptr(arr, ctype=C.c_uint64):

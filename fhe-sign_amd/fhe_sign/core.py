@@ -230,6 +230,10 @@ class Context:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         check(load().fhe_ctx_attach_comm_timeout(self._h, buf, nranks, rank, int(timeout_ms)))
 
+    def set_comm_timeout(self, timeout_ms: int) -> None:
+        """the attached communicator's deadline: time a bounded wait may pass without progress"""
+        check(load().fhe_ctx_set_comm_timeout(self._h, int(timeout_ms)))
+
     def ready(self) -> bool:
         """the context exists and its device is usable (checked before any collective is entered)"""
         return bool(getattr(self, "_h", None)) and load().fhe_ctx_sync(self._h) == 0

@@ -178,11 +178,16 @@ int fhe_comm_unique_id(uint8_t id[FHE_COMM_ID_BYTES]);
  * ranks that did -- no rank is left waiting inside the library.  The same deadline bounds the
  * enqueue of every later collective (all-gather, key and operand broadcasts) and, while a
  * communicator is attached, every wait for the engine's stream (fhe_ctx_sync, downloads,
- * decryption): a peer that dies after a collective was enqueued gives FHE_ERR_TIMEOUT (or the
- * communicator's error) and an aborted, detached communicator instead of a hang.  Callers should still agree out of
- * band that every rank is ready before attaching (fhe_sign/dist.py: attach_fanout). */
+ * decryption): a stream that makes no progress for the deadline -- no launched level completes, e.g.
+ * a peer died after a collective was enqueued -- gives FHE_ERR_TIMEOUT (or the communicator's error)
+ * and an aborted, detached communicator instead of a hang; a long flush whose levels keep completing
+ * is never cut off.  Callers should still agree out of band that every rank is ready before
+ * attaching (fhe_sign/dist.py: attach_fanout).  All ranks must issue the same radix program and the
+ * same host reads (downloads, syncs) in the same order, since every flush schedules collectively. */
 int fhe_ctx_attach_comm_timeout(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank,
                                 uint32_t timeout_ms);
+/* change the attached communicator's deadline (ms, > 0); FHE_ERR_INVALID without a communicator */
+int fhe_ctx_set_comm_timeout(fhe_ctx* ctx, uint32_t timeout_ms);
 /* the same with FHE_COMM_DEFAULT_TIMEOUT_MS */
 int fhe_ctx_attach_comm(fhe_ctx* ctx, const uint8_t id[FHE_COMM_ID_BYTES], int nranks, int rank);
 /* Collective over the attached communicator: rank `root` (which has a server key installed)

@@ -233,6 +233,14 @@ def u_add(a, b, bits):
     return (a + b) % (1 << bits)
 
 
+def u_sub(a, b, bits):
+    return (a - b) % (1 << bits)
+
+
+def u_and(a, b, bits):
+    return (a & b) % (1 << bits)
+
+
 def u_mul(a, b, bits):
     return (a * b) % (1 << bits)
 

@@ -254,3 +254,61 @@ def test_config5_emulated_ranks_production_split(keys, config5_ref, ranks):
     assert world == ranks and split > 0  # the compat mul's wide product levels were split
     set_server_key(None)
     ctx.close()
+
+
+def test_rccl_world1_sync_is_bounded(keys):
+    """While a communicator is attached, fhe_ctx_sync waits through the bounded path
+    (fhe_ctx::wait_stream), whose deadline counts time WITHOUT PROGRESS: (a) a compat 256-bit mul
+    (~0.6 s over 151 levels, no level above ~0.25 s) completes under a 400 ms deadline, since every
+    completed level restarts it, and its dead-node agreement (a byte-wise min all-reduce) runs at
+    every flush; (b) one raw 8192-PBS launch (one kernel, ~60 ms, no level marks) under a 2 ms
+    deadline returns FHE_ERR_TIMEOUT with the communicator aborted and detached, and the context
+    keeps computing afterwards."""
+    from fhe_sign._lib import FHE_ERR_TIMEOUT, FheError
+    ck, sk = keys
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    with pytest.raises(FheError):
+        ctx.set_comm_timeout(100)  # no communicator
+    ctx.attach_comm(comm_unique_id(), 1, 0)
+    set_server_key(ctx)
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "biguint_vectors.json")))["mul"][0]
+    val = lambda limbs: sum(int(x) << (32 * i) for i, x in enumerate(limbs))  # noqa: E731
+    A, B = BigUintFHE.new(val(g["a"]), ck), BigUintFHE.new(val(g["b"]), ck)
+    ctx.set_comm_timeout(400)
+    out = A.mul(B, COMPAT)
+    ctx.sync()
+    assert out.decrypt_limbs(ck) == _limbs(g["out"])
+    assert ctx.fanout_info()[1] == 1 and load_comm_attached(ctx)
+    # (b) no progress for longer than the deadline
+    n = 8192
+    lid = ctx.lut([(m + 1) % 16 for m in range(16)])
+    cts = ck.encrypt_blocks(np.arange(n) % 16)
+    d_in, d_out, d_lut = ctx.alloc(cts.nbytes), ctx.alloc(cts.nbytes), ctx.alloc(n * 4)
+    ctx.h2d(d_in, cts)
+    ctx.h2d(d_lut, np.full(n, lid, np.uint32))
+    ctx.sync()
+    ctx.set_comm_timeout(2)
+    ctx.pbs_device(d_in, n, d_lut, d_out)
+    with pytest.raises(FheError) as e:
+        ctx.sync()
+    assert e.value.code == FHE_ERR_TIMEOUT
+    assert not load_comm_attached(ctx)  # aborted and detached
+    ctx.sync()  # no communicator: a plain stream wait
+    got = np.zeros_like(cts)
+    ctx.d2h(got, d_out)
+    assert all(ck.decrypt_block(got[i]) == (i % 16 + 1) % 16 for i in range(0, n, 97))
+    for p in (d_in, d_out, d_lut):
+        ctx.free(p)
+    set_server_key(None)
+    ctx.close()
+
+
+def load_comm_attached(ctx) -> bool:
+    """a communicator is attached (fhe_ctx_set_comm_timeout refuses otherwise)"""
+    from fhe_sign._lib import FheError
+    try:
+        ctx.set_comm_timeout(120000)
+        return True
+    except FheError:
+        return False
