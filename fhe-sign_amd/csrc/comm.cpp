@@ -496,22 +496,24 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     // usable until every collective and conversion has succeeded, then the two are swapped.
     uint64_t* n_ksk = nullptr;
     int8_t* n_planes = nullptr;
-    double2 *n_bsk = nullptr, *n_quad = nullptr;
+    double2 *n_bsk = nullptr, *n_quad = nullptr, *n_qx = nullptr;
     auto drop_new = [&] {
         (void)hipStreamSynchronize(c->stream);
         if (n_ksk) (void)hipFree(n_ksk);
         if (n_planes) (void)hipFree(n_planes);
         if (n_bsk) (void)hipFree(n_bsk);
         if (n_quad) (void)hipFree(n_quad);
+        if (n_qx) (void)hipFree(n_qx);
         n_ksk = nullptr;
         n_planes = nullptr;
-        n_bsk = n_quad = nullptr;
+        n_bsk = n_quad = n_qx = nullptr;
     };
     if (!is_root && local_ok) {
         hipError_t he = hipMalloc(&n_ksk, ksk_words * 8);
         if (he == hipSuccess) he = hipMalloc(&n_planes, fhe::ks_planes_bytes((int)p.n));
         if (he == hipSuccess) he = hipMalloc(&n_bsk, bsk_doubles * 8);
         if (he == hipSuccess) he = hipMalloc(&n_quad, bsk_doubles * 8);
+        if (he == hipSuccess && p.grouping == 1) he = hipMalloc(&n_qx, bsk_doubles * 8);
         if (he != hipSuccess) {
             drop_new();
             local_ok = 0;
@@ -542,6 +544,7 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     }
     rc = launch_ksk_to_planes(n_ksk, (int)p.n, n_planes, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = launch_bsk_to_quad(n_bsk, npoly, n_quad, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc && n_qx) rc = launch_bsk_to_qx(n_bsk, npoly, n_qx, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (rc) {
         drop_new();
@@ -561,6 +564,7 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     std::swap(c->d_ksk_planes, n_planes);
     std::swap(c->d_bsk, n_bsk);
     std::swap(c->d_bsk_quad, n_quad);
+    std::swap(c->d_bsk_qx, n_qx);
     drop_new();  // frees the previous key's buffers (null when there was none)
     if (!(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
         c->lut_ids.clear();
@@ -576,6 +580,12 @@ int fhe_ctx_set_fanout(fhe_ctx* c, uint32_t min_level, int emulate_ranks) {
     if (!c || emulate_ranks < 0) return FHE_ERR_INVALID;
     c->fanout_min = min_level;
     c->fanout_emulate = emulate_ranks;
+    return FHE_OK;
+}
+
+int fhe_ctx_rank_pbs(const fhe_ctx* c, uint64_t* pbs) {
+    if (!c || !pbs) return FHE_ERR_INVALID;
+    *pbs = c->engine ? c->engine->rank_pbs : 0;
     return FHE_OK;
 }
 

@@ -279,6 +279,9 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     if ((int)count <= wide_threshold)
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
+    if (p.grouping == 1 && br_kernel == FHE_BR_QX && d_bsk_qx)
+        return launch_blind_rotate_qx(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
+                                      d_zeta_full, d_mono, out, (int)count, (int)p.n, stream);
     return launch_blind_rotate_quad(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_quad, d_tw_quad, d_psi_quad,
                                     d_zeta_quad, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
 }
@@ -526,6 +529,8 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
     wide_zetas(Z, &zw);
     FHE_HIP_CHECK(hipMalloc(&c->d_zeta_wide, zw.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_zeta_wide, zw.data(), zw.size() * sizeof(double2), hipMemcpyHostToDevice));
+    FHE_HIP_CHECK(hipMalloc(&c->d_zeta_full, Z.size() * sizeof(double2)));
+    FHE_HIP_CHECK(hipMemcpy(c->d_zeta_full, Z.data(), Z.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMalloc(&c->d_zeta_quad, zq.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_zeta_quad, zq.data(), zq.size() * sizeof(double2), hipMemcpyHostToDevice));
     lane_twiddles(W0, &W);
@@ -560,7 +565,7 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     c->engine = nullptr;
     c->release_comm();
     void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
-                    c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_mono, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
+                    c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_mono, c->d_bsk_qx, c->d_zeta_full, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)
@@ -580,11 +585,13 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
         FHE_HIP_CHECK(hipFree(c->d_ksk));
         FHE_HIP_CHECK(hipFree(c->d_bsk));
         FHE_HIP_CHECK(hipFree(c->d_bsk_quad));
+        if (c->d_bsk_qx) FHE_HIP_CHECK(hipFree(c->d_bsk_qx));
         FHE_HIP_CHECK(hipFree(c->d_ksk_planes));
         c->d_ksk_planes = nullptr;
         c->d_ksk = nullptr;
         c->d_bsk = nullptr;
         c->d_bsk_quad = nullptr;
+        c->d_bsk_qx = nullptr;
         c->has_key = false;
     }
     FHE_HIP_CHECK(hipMalloc(&c->d_ksk, sk->ksk.size() * 8));
@@ -599,6 +606,10 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     FHE_HIP_CHECK(launch_bsk_to_fourier(d_std, npoly, c->d_W, c->d_psi, c->d_bsk, c->stream));
     FHE_HIP_CHECK(hipMalloc(&c->d_bsk_quad, (size_t)npoly * 1024 * sizeof(double2)));
     FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, c->d_bsk_quad, c->stream));
+    if (p.grouping == 1) {  // the classic throughput kernel's layout (br_qx.hip)
+        FHE_HIP_CHECK(hipMalloc(&c->d_bsk_qx, (size_t)npoly * 1024 * sizeof(double2)));
+        FHE_HIP_CHECK(launch_bsk_to_qx(c->d_bsk, npoly, c->d_bsk_qx, c->stream));
+    }
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
     FHE_HIP_CHECK(hipFree(d_std));
     if (!c->has_key || !(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
@@ -748,7 +759,7 @@ int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
                   "FHE_BR_QUAD is the throughput kernel");
         return FHE_ERR_INVALID;
     }
-    if (kind != FHE_BR_QUAD) return FHE_ERR_INVALID;
+    if (kind != FHE_BR_QUAD && kind != FHE_BR_QX) return FHE_ERR_INVALID;
     c->br_kernel = kind;
     return FHE_OK;
 }

@@ -52,12 +52,14 @@ struct fhe_ctx {
     double2* d_tw_wide = nullptr;   // [12][256]
     double2* d_psi_wide = nullptr;  // [4][256]
     double2* d_bsk_quad = nullptr;  // Fourier BSK in the 4-wave kernel's layout (br_quad.hip)
+    double2* d_bsk_qx = nullptr;    // classic Fourier BSK in br_qx.hip's E layout (grouping 1 only)
+    double2* d_zeta_full = nullptr; // zeta(s, b) at [2^s + b], 1024 entries (br_qx.hip)
     double2* d_tw_quad = nullptr;   // W[0..512)
     double2* d_psi_quad = nullptr;  // [2][8][128]: twist (unused since the twisted forward), untwist
     double2* d_zeta_quad = nullptr; // br_quad.hip zeta layout (context.cpp:quad_zetas)
     double2* d_zeta_wide = nullptr; // [10][256] (context.cpp:wide_zetas)
     double2* d_mono = nullptr;      // monomial table E[4096] of the multi-bit blind rotation (mono_table)
-    int br_kernel = FHE_BR_QUAD;    // throughput kernel for levels above wide_threshold
+    int br_kernel = FHE_BR_QX;      // throughput kernel for levels above wide_threshold (classic; multi-bit: quad)
     int8_t* d_ksk_planes = nullptr; // KSK as balanced signed-byte planes (ks_mfma.hip)
     int ks_kernel = FHE_KS_MFMA;
     int8_t* d_ks_digits = nullptr;  // keyswitch digits workspace

@@ -56,6 +56,13 @@ hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const Pbs
                                     const double2* zq, const double2* mono, int grouping, uint64_t* out, int count,
                                     int n, hipStream_t s);
 hipError_t launch_bsk_to_quad(const double2* bsk, int npoly, double2* out, hipStream_t s);
+// classic throughput kernel with the round-4 layouts (br_qx.hip): no DPP transposes; bsk_qx from
+// launch_bsk_to_qx, zfull = the zeta table zeta(s, b) at [2^s + b] (context.cpp zeta_table)
+hipError_t launch_blind_rotate_qx(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
+                                  const uint64_t* luts, const double2* bsk_qx, const double2* tw, const double2* ps,
+                                  const double2* zfull, const double2* mono, uint64_t* out, int count, int n,
+                                  hipStream_t s);
+hipError_t launch_bsk_to_qx(const double2* bsk, int npoly, double2* out, hipStream_t s);
 // dst[i][0..2049) = src[i * 2049 ..] for i < count (all-gathered level outputs -> block slots)
 hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s);
 // the reverse: block slots -> contiguous [count][2049] (operand broadcast, comm.cpp)

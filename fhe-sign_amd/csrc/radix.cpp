@@ -476,7 +476,10 @@ void Engine::flush() {
         ctx_->mark_progress();
         pbs_count += G;
         levels += 1;
-        if (level_log.size() < kLevelLogCap) level_log.push_back((uint32_t)G);
+        // this rank's bootstraps: its slice of a fanned-out level (rank 0's when ranks are emulated), else all
+        const size_t r0 = ctx_->comm ? (size_t)ctx_->rank : 0;
+        rank_pbs += split ? std::min(G, (r0 + 1) * chunk) - std::min(G, r0 * chunk) : G;
+        if (level_log.size() < kLevelLogCap) level_log.push_back((uint32_t)G | (split ? kLevelSplit : 0u));
         if (trace_) {
             hip_check(hipStreamSynchronize(ctx_->stream), "trace sync");
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -131,8 +131,11 @@ public:
     // statistics
     uint64_t pbs_count = 0, levels = 0, fanout_levels = 0;
     uint64_t dead_nodes = 0;  // recorded bootstraps dropped at flush: nothing could read their outputs
-    // bootstraps per launched level, in launch order (fhe_ctx_level_log; the bench's CPU replay)
+    // bootstraps per launched level, in launch order (fhe_ctx_level_log; the bench's CPU replay);
+    // kLevelSplit marks a level fanned out over the ranks (fan-out only, never at world size 1)
     std::vector<uint32_t> level_log;
+    static constexpr uint32_t kLevelSplit = 1u << 31;
+    uint64_t rank_pbs = 0;  // bootstraps this rank ran itself (fanned-out levels: its slice)
     static constexpr size_t kLevelLogCap = 1u << 20;
 
 private:

@@ -12,5 +12,5 @@ from .core import (ClientKey, Context, ServerKey, comm_unique_id, default_params
                    multi_bit_params)
 from .integer import (  # noqa: F401,E402
     COMPAT, FAST, PUBLIC, BigUintFHE, FheBool, FheUint, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, set_server_key,
-    level_log, stats, to_u32_digits)
+    LEVEL_SPLIT, level_log, rank_pbs, stats, to_u32_digits)
 from .schnorr import Schnorr, compute_nonce, public_key_x  # noqa: F401,E402

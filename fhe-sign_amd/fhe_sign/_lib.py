@@ -126,6 +126,7 @@ _SIGNATURES = [
     ("fhe_radix_bitand", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("fhe_ctx_stats", C.c_int, [C.c_void_p, u64p, u64p]),
     ("fhe_ctx_level_log", C.c_int, [C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_size_t), C.c_int]),
+    ("fhe_ctx_rank_pbs", C.c_int, [C.c_void_p, u64p]),
     ("fhe_schedule_levels", C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_size_t, C.c_int,
                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("fhe_biguint_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_void_p)]),

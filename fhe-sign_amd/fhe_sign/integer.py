@@ -385,8 +385,19 @@ class BigUintFHE:
     __mul__ = mul
 
 
+LEVEL_SPLIT = 1 << 31  # FHE_LEVEL_SPLIT: the level was fanned out over the ranks
+
+
+def rank_pbs(ctx) -> int:
+    """bootstraps this rank ran itself (fhe_ctx_rank_pbs; emulated ranks: rank 0's share)"""
+    v = C.c_uint64()
+    check(load().fhe_ctx_rank_pbs(ctx.handle, C.byref(v)))
+    return int(v.value)
+
+
 def level_log(ctx, reset: bool = True) -> list[int]:
-    """bootstraps per launched level since the last reset (fhe_ctx_level_log)"""
+    """bootstraps per launched level since the last reset (fhe_ctx_level_log); under fan-out an
+    entry carries LEVEL_SPLIT when the level was split over the ranks"""
     n = C.c_size_t()
     check(load().fhe_ctx_level_log(ctx.handle, None, 0, C.byref(n), 0))
     buf = np.zeros(max(1, n.value), np.uint32)

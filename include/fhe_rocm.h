@@ -151,13 +151,16 @@ int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
-/* Throughput blind-rotate kernel for levels above the threshold: 4 waves per ciphertext
- * (FHE_BR_QUAD, the only one).  The retired kernels -- FHE_BR_NARROW (2 waves per ciphertext, round
- * 1) and FHE_BR_PAIR (two ciphertexts per 4-wave workgroup, rounds 2-3: at parity, never default) --
- * are refused with FHE_ERR_INVALID.  Both blind-rotate kernels produce identical bits. */
+/* Throughput blind-rotate kernel for levels above the threshold, 4 waves per ciphertext:
+ * FHE_BR_QX (default; classic parameters: the round-4 layouts without DPP transposes, br_qx.hip) or
+ * FHE_BR_QUAD (br_quad.hip; always used for the multi-bit blind rotation).  The retired kernels --
+ * FHE_BR_NARROW (2 waves per ciphertext, round 1) and FHE_BR_PAIR (two ciphertexts per 4-wave
+ * workgroup, rounds 2-3) -- are refused with FHE_ERR_INVALID.  All blind-rotate kernels produce
+ * identical bits. */
 #define FHE_BR_NARROW 0
 #define FHE_BR_QUAD 1
 #define FHE_BR_PAIR 2
+#define FHE_BR_QX 3
 int fhe_ctx_set_br_kernel(fhe_ctx* ctx, int kind);
 /* Keyswitch: int8 matrix-core contraction against the KSK's byte planes (FHE_KS_MFMA, default) or
  * the 64-bit VALU kernel (FHE_KS_VALU).  Both are exact: identical small LWE words. */
@@ -288,6 +291,12 @@ int fhe_ctx_stats(fhe_ctx* ctx, uint64_t* pbs_count, uint64_t* levels);
  * record, at most 2^20 levels): *n = the number recorded, min(cap, *n) written to sizes; reset != 0
  * clears the record.  bench.py replays these level sizes through the CPU restatement. */
 int fhe_ctx_level_log(fhe_ctx* ctx, uint32_t* sizes, size_t cap, size_t* n, int reset);
+/* Bit 31 of a level_log entry: the level was fanned out over the ranks (split + all-gather); the
+ * low bits are its bootstrap count.  Only set while ranks are attached or emulated. */
+#define FHE_LEVEL_SPLIT 0x80000000u
+/* Bootstraps this rank ran itself since context creation: its slice of every fanned-out level plus
+ * every level it ran redundantly (with emulated ranks: rank 0's share). */
+int fhe_ctx_rank_pbs(const fhe_ctx* ctx, uint64_t* pbs);
 /* The engine's level scheduler on an explicit dependency graph (host only, no GPU): node i reads
  * nodes deps[dep_offsets[i] .. dep_offsets[i+1]) (all < i).  Writes each node's launch level
  * (1-based) to level_of[i] and the level count (= the critical path) to *nlevels.  mode 0: backward

@@ -166,32 +166,60 @@ def test_zero_and_sparse_masks_both_kernels(env):
         assert ok.decrypt(ref[m]) == tables[lut_of[m]][m]
 
 
-def test_quad_kernel_ragged_batches_and_retired_kernels(env):
-    """The throughput kernel at ragged batches (1, 2, 3, 37) with every LUT gives the latency kernel's
-    and the oracle's words; the retired blind-rotate kernels (0: round-1 2-wave, 2: the pair kernel)
-    are refused."""
+@pytest.mark.parametrize("kind", [3, 1])  # FHE_BR_QX (classic default, br_qx.hip), FHE_BR_QUAD (br_quad.hip)
+def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
+    """Both throughput kernels at ragged batches (1, 2, 3, 37, 259) with every LUT give the latency
+    kernel's and the oracle's words (multi-bit parameters always run br_quad.hip); the retired
+    blind-rotate kernels (0: round-1 2-wave, 2: the pair kernel) are refused."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = [ctx.lut(t) for t in tables]
     r = ok.rng(991)
-    cts = np.stack([ok.encrypt(r, (3 * i + 1) % 16) for i in range(37)])
-    lut_ids = np.array([ids[i % len(ids)] for i in range(37)], np.uint32)
+    cts = np.stack([ok.encrypt(r, (3 * i + 1) % 16) for i in range(259)])
+    lut_ids = np.array([ids[i % len(ids)] for i in range(259)], np.uint32)
     try:
         ctx.set_wide_threshold(1 << 30)
         wide = ctx.pbs(cts, lut_ids)
+        ctx.set_br_kernel(kind)
         ctx.set_wide_threshold(0)
-        quad = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 2, 3, 37)}
+        thr = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 2, 3, 37, 259)}
     finally:
         ctx.set_wide_threshold(256)
-    for c, out in quad.items():
+        ctx.set_br_kernel(3)
+    for c, out in thr.items():
         bad = [i for i in range(c) if not np.array_equal(out[i], wide[i])]
-        assert not bad, f"batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
+        assert not bad, f"kernel {kind}, batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
-    assert np.array_equal(quad[37][:6], ref)
-    for kind in (0, 2):
+    assert np.array_equal(thr[37][:6], ref)
+    for bad_kind in (0, 2, 4):
         with pytest.raises(Exception):
-            ctx.set_br_kernel(kind)
-    ctx.set_br_kernel(1)
+            ctx.set_br_kernel(bad_kind)
+
+
+def test_throughput_kernels_identical_at_full_batch(env):
+    """br_qx.hip and br_quad.hip on the same 4096 distinct encryptions (16 rounds of 256 CUs): every
+    output word identical, a seeded sample of 8 equal to the oracle."""
+    _, _, ok, ctx = env
+    tables = _luts()
+    ids = np.array([ctx.lut(t) for t in tables], np.uint32)
+    B = 4096
+    r = ok.rng(31337)
+    cts = np.stack([ok.encrypt(r, i % 16) for i in range(B)])
+    lut_of = np.arange(B) % len(tables)
+    try:
+        ctx.set_br_kernel(1)
+        quad = ctx.pbs(cts, ids[lut_of])
+        ctx.set_br_kernel(3)
+        qx = ctx.pbs(cts, ids[lut_of])
+    finally:
+        ctx.set_br_kernel(3)
+    bad = np.flatnonzero((quad != qx).any(axis=1))
+    assert bad.size == 0, f"{bad.size} ciphertexts differ between the throughput kernels, first {bad[:5]}"
+    pick = np.array([0, 1, 513, 1024, 2047, 2048, 3333, 4095])
+    ref = ok.pbs_batch(np.ascontiguousarray(cts[pick]), np.stack([ok.make_lut(t) for t in tables]),
+                       lut_of[pick].astype(np.uint32))
+    for k, i in enumerate(pick):
+        assert np.array_equal(qx[i], ref[k]), f"ciphertext {i} differs from the oracle"
 
 
 def test_keyswitch_kernels_identical(env):

@@ -1,0 +1,96 @@
+"""Config 5 (one op fanned over N GPUs) projected from one GPU: the engine runs the op with N emulated
+ranks at the production split (levels of >= 257 bootstraps split, fhe_ctx_set_fanout), the level log
+records every level's size and whether it was split, and rank 0's share of each level is then
+REPLAYED on this GPU as raw bootstrap launches (keyswitch + blind rotate of that many ciphertexts,
+each level synchronised), which is what one rank of a real N-GPU run computes.  All-gathers are not
+included (estimated separately: ~16 KB per bootstrap of a split level).  Also reported: the host
+graph build alone (the op call without a sync, no trace) and the per-rank bootstrap count.
+usage: python3 tools/fanout_projection.py [ranks...]   (default 1 2 4 8)"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
+import numpy as np  # noqa: E402
+
+from fhe_sign import (COMPAT, FAST, LEVEL_SPLIT, BigUintFHE, Context, Schnorr, compute_nonce,  # noqa: E402
+                      generate_keys, level_log, rank_pbs, set_server_key)
+
+ranks_list = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8]
+g = json.load(open(os.path.join(ROOT, "tests", "golden", "biguint_vectors.json")))["mul"][0]
+val = lambda limbs: sum(int(x) << (32 * i) for i, x in enumerate(limbs))  # noqa: E731
+a, b = val(g["a"]), val(g["b"])
+ck, sk = generate_keys(seed=0xFA11)
+ctx = Context(0)
+ctx.set_server_key(sk)
+set_server_key(ctx)
+lid = ctx.lut([(m + 1) % 16 for m in range(16)])
+MAXB = 32768
+cts = ck.encrypt_blocks(np.arange(MAXB) % 16)
+d_in, d_out, d_lut = ctx.alloc(cts.nbytes), ctx.alloc(cts.nbytes), ctx.alloc(MAXB * 4)
+ctx.h2d(d_in, cts)
+ctx.h2d(d_lut, np.full(MAXB, lid, np.uint32))
+
+
+def replay(sizes):
+    """wall time of launching these level sizes back to back, each level synchronised"""
+    ctx.pbs_device(d_in, 256, d_lut, d_out)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for k in sizes:
+        if k:
+            ctx.pbs_device(d_in, min(k, MAXB), d_lut, d_out)
+            ctx.sync()
+    return time.perf_counter() - t0
+
+
+A, B = BigUintFHE.new(a, ck), BigUintFHE.new(b, ck)
+d, msg = 3, bytes(32)
+k0 = compute_nonce(d, msg, bytes(32))
+dF = BigUintFHE.new(d, ck)
+s = Schnorr()
+ops = {
+    "biguint256_mul_compat": lambda: A.mul(B, COMPAT),
+    "biguint256_mul_fast": lambda: A.mul(B, FAST),
+    "sign_fhe_with_k0_v0_compat": lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT),
+}
+ref = {"biguint256_mul_compat": [int(x) for x in g["out"]], "biguint256_mul_fast": a * b,
+       "sign_fhe_with_k0_v0_compat": s.sign_with_k0(msg, k0, d)}
+rows = []
+for W in ranks_list:
+    ctx.set_fanout(min_level=257, emulate_ranks=W if W > 1 else 0)
+    for name, fn in ops.items():
+        fn()  # warm-up (pools, LUTs)
+        ctx.sync()
+        level_log(ctx)
+        p0 = rank_pbs(ctx)
+        t0 = time.perf_counter()
+        r = fn() if name.startswith("sign") else fn()
+        t_call = time.perf_counter() - t0  # sign: includes its own host reads; mul: the graph build
+        ctx.sync()
+        t_op = time.perf_counter() - t0
+        log = level_log(ctx)
+        p1 = rank_pbs(ctx)
+        if name == "biguint256_mul_compat":
+            assert r.decrypt_limbs(ck) == ref[name]
+        elif name == "biguint256_mul_fast":
+            assert r.to_biguint(ck) == ref[name]
+        else:
+            assert r == ref[name]
+        share = []
+        for e in log:
+            G, split = e & ~LEVEL_SPLIT, bool(e & LEVEL_SPLIT)
+            share.append((G + W - 1) // W if split else G)
+        t_rank = replay(share)
+        split_pbs = sum(e & ~LEVEL_SPLIT for e in log if e & LEVEL_SPLIT)
+        row = {"op": name, "ranks": W, "levels": len(log), "split_levels": sum(1 for e in log if e & LEVEL_SPLIT),
+               "pbs": sum(e & ~LEVEL_SPLIT for e in log), "rank_pbs": p1 - p0,
+               "redundant_levels": sum(1 for e in log if not e & LEVEL_SPLIT),
+               "allgather_mb": round(split_pbs * 2049 * 8 / 1e6, 1),
+               "rank_replay_s": round(t_rank, 4), "host_call_s": round(t_call, 4),
+               "emulated_wall_s": round(t_op, 4)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+ctx.close()

@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""LDS map search for the throughput blind rotate's exchange layouts (br_quad.hip, round 4).
+
+Four layouts of a 1024-point polynomial region, each written and read through ds_*_b128:
+  A  wave bit b6 = h, registers (b9 b8 b7), lanes (b5..b0)
+  B  wave bit b9 = h, registers (b6 b5 b4), lane bits 5, 4 = (b3, b2), lane bits 3..0 = perm of (b8 b7 b1 b0)
+  B' B after the register-bit (2, 1) <-> lane-bit (5, 4) permlane swaps: registers (b3 b2 b4),
+     lane bits 5, 4 = (b6, b5), lane bits 3..0 as in B
+  E  wave = (b3, b2), registers (poly, b1, b0), lanes = perm of (b9..b4)
+Exchanges: A -> B and B -> A (forward / inverse), B' -> E and E -> B'.  An ADDITIVE map
+pos = sum_k w_k b_k (injective, padded region; additive so that the register part of every access is a
+ds_* immediate offset on a per-lane base, no per-access VALU) is scored by the gfx950 lane-group rules of MI355X_MICROARCH.md
+LDS: ds_read_b128 four 16-lane groups over 16 slots of 16 B (pos mod 16), ds_write_b128 eight
+8-lane groups over 8 slots (pos mod 8, transfer-bound at ~13 cycles, so array cycles up to 13 are free).
+usage: python3 tools/lds_layout_qx.py [trials]"""
+import itertools
+import random
+import sys
+
+RG = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+      list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+RG += [[l + 32 for l in g] for g in RG]
+WG = [list(range(i, i + 8)) for i in range(0, 64, 8)]
+
+
+def bits_to_idx(assign):
+    """assign: {index bit: value bit} -> idx"""
+    return sum(v << k for k, v in assign.items())
+
+
+def layout_A(h, L, r):
+    return 128 * r + 64 * h + L
+
+
+def make_B(perm):  # perm: index bits held by lane bits 3, 2, 1, 0
+    def f(h, L, r):
+        a = {9: h, 6: r >> 2 & 1, 5: r >> 1 & 1, 4: r & 1, 3: L >> 5 & 1, 2: L >> 4 & 1}
+        for lb, ib in zip((3, 2, 1, 0), perm):
+            a[ib] = L >> lb & 1
+        return bits_to_idx(a)
+    return f
+
+
+def make_Bp(perm):
+    def f(h, L, r):
+        a = {9: h, 3: r >> 2 & 1, 2: r >> 1 & 1, 4: r & 1, 6: L >> 5 & 1, 5: L >> 4 & 1}
+        for lb, ib in zip((3, 2, 1, 0), perm):
+            a[ib] = L >> lb & 1
+        return bits_to_idx(a)
+    return f
+
+
+def make_E(lperm, wswap):  # lperm: index bits held by lane bits 5..0; region = r >> 2 (poly)
+    def f(e, L, r):
+        a = {1: r >> 1 & 1, 0: r & 1}
+        if wswap:
+            a[2], a[3] = e >> 1 & 1, e & 1
+        else:
+            a[3], a[2] = e >> 1 & 1, e & 1
+        for lb, ib in zip((5, 4, 3, 2, 1, 0), lperm):
+            a[ib] = L >> lb & 1
+        return bits_to_idx(a)
+    return f
+
+
+def apply(M, idx):
+    return sum(M[k] for k in range(10) if idx >> k & 1)
+
+
+MAXPOS = 1100  # region size bound (complex entries)
+
+
+def valid(M):
+    ad = {apply(M, i) for i in range(1024)}
+    return len(ad) == 1024 and max(ad) < MAXPOS
+
+
+def rd_cycles(pos):
+    t = 0
+    for g in RG:
+        cnt = {}
+        for l in g:
+            cnt.setdefault(pos[l] % 16, set()).add(pos[l])
+        t += max(len(v) for v in cnt.values())
+    return t
+
+
+def wr_cycles(pos):
+    t = 0
+    for g in WG:
+        cnt = {}
+        for l in g:
+            cnt.setdefault(pos[l] % 8, set()).add(pos[l])
+        t += max(len(v) for v in cnt.values())
+    return t
+
+
+def score(M, layouts):
+    """average cycles per instruction: reads (ideal 4) + writes (max(13, array cycles))"""
+    rd = wr = 0.0
+    n = 0
+    for lay, waves in layouts:
+        for w in waves:
+            for r in range(8):
+                pos = [apply(M, lay(w, L, r)) for L in range(64)]
+                rd += rd_cycles(pos)
+                wr += max(13, wr_cycles(pos))
+                n += 1
+    return rd / n, wr / n
+
+
+def rand_invertible():
+    while True:
+        M = [random.randrange(1, 1024) for _ in range(10)]
+        # rank check
+        rows = list(M)
+        rank = 0
+        for bit in range(10):
+            piv = next((i for i in range(rank, 10) if rows[i] >> bit & 1), None)
+            if piv is None:
+                continue
+            rows[rank], rows[piv] = rows[piv], rows[rank]
+            for i in range(10):
+                if i != rank and rows[i] >> bit & 1:
+                    rows[i] ^= rows[rank]
+            rank += 1
+        if rank == 10:
+            return M
+
+
+def invertible(M):
+    rows = list(M)
+    rank = 0
+    for bit in range(10):
+        piv = next((i for i in range(rank, 10) if rows[i] >> bit & 1), None)
+        if piv is None:
+            continue
+        rows[rank], rows[piv] = rows[piv], rows[rank]
+        for i in range(10):
+            if i != rank and rows[i] >> bit & 1:
+                rows[i] ^= rows[rank]
+        rank += 1
+    return rank == 10
+
+
+def search(trials, seed=1):
+    random.seed(seed)
+    best = None
+    perms = list(itertools.permutations((8, 7, 1, 0)))
+    lperms = list(itertools.permutations((9, 8, 7, 6, 5, 4)))
+    for t in range(trials):
+        perm = random.choice(perms)
+        lperm = random.choice(lperms)
+        wswap = random.random() < 0.5
+        lays = [(layout_A, (0, 1)), (make_B(perm), (0, 1)), (make_Bp(perm), (0, 1)), (make_E(lperm, wswap), (0, 1, 2, 3))]
+        M = [1 << k for k in range(10)]
+        rd, wr = score(M, lays)
+        cur = rd + wr
+        # hill-climb: nudge one weight
+        for _ in range(400):
+            k = random.randrange(10)
+            M2 = list(M)
+            M2[k] = max(1, M2[k] + random.choice((-8, -4, -2, -1, 1, 2, 4, 8, 16, 32)))
+            if not valid(M2):
+                continue
+            r2, w2 = score(M2, lays)
+            if r2 + w2 <= cur:
+                M, rd, wr, cur = M2, r2, w2, r2 + w2
+        if best is None or cur < best[0]:
+            best = (cur, rd, wr, perm, lperm, wswap, M, max(apply(M, i) for i in range(1024)))
+            print(best, flush=True)
+    return best
+
+
+
+# ---- vectorised search (numpy): the same score, ~100x faster
+def search_np(trials, iters=3000, seed=1):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    RGa = np.array(RG)
+    WGa = np.array(WG)
+    perms = list(itertools.permutations((8, 7, 1, 0)))
+    lperms = list(itertools.permutations((9, 8, 7, 6, 5, 4)))
+    best = None
+    for t in range(trials):
+        perm = perms[rng.integers(len(perms))]
+        lperm = lperms[rng.integers(len(lperms))]
+        wswap = bool(rng.integers(2))
+        lays = [(layout_A, (0, 1)), (make_B(perm), (0, 1)), (make_Bp(perm), (0, 1)), (make_E(lperm, wswap), (0, 1, 2, 3))]
+        idx = np.array([[lay(w, L, r) for L in range(64)] for lay, waves in lays for w in waves for r in range(8)])
+        bits = ((idx[..., None] >> np.arange(10)) & 1).astype(np.int64)  # [80][64][10]
+        allbits = ((np.arange(1024)[:, None] >> np.arange(10)) & 1).astype(np.int64)
+
+        def sc(M):
+            pos = bits @ M  # [80][64]
+            s16 = pos[:, RGa] % 16  # [80][4][16]
+            rd = np.zeros(s16.shape[:2], np.int64)
+            for v in range(16):
+                rd = np.maximum(rd, (s16 == v).sum(-1))
+            s8 = pos[:, WGa] % 8
+            wr = np.zeros(s8.shape[:2], np.int64)
+            for v in range(8):
+                wr = np.maximum(wr, (s8 == v).sum(-1))
+            return rd.sum(1).mean(), np.maximum(13, wr.sum(1)).mean()
+
+        def ok(M):
+            a = allbits @ M
+            return a.max() < MAXPOS and len(np.unique(a)) == 1024
+
+        M = np.array([1 << k for k in range(10)], np.int64)
+        rd, wr = sc(M)
+        cur = rd + wr
+        steps = np.array((-16, -8, -4, -2, -1, 1, 2, 4, 8, 16, 32))
+        for _ in range(iters):
+            M2 = M.copy()
+            k = rng.integers(10)
+            M2[k] = max(1, M2[k] + steps[rng.integers(len(steps))])
+            if rng.integers(4) == 0:
+                k2 = rng.integers(10)
+                M2[k2] = max(1, M2[k2] + steps[rng.integers(len(steps))])
+            if not ok(M2):
+                continue
+            r2, w2 = sc(M2)
+            if r2 + w2 <= cur:
+                M, rd, wr, cur = M2, r2, w2, r2 + w2
+        if best is None or cur < best[0]:
+            best = (cur, rd, wr, perm, lperm, wswap, [int(x) for x in M], int((allbits @ M).max()))
+            print(best, flush=True)
+    return best
+
+
+if __name__ == "__main__":
+    search_np(int(sys.argv[1]) if len(sys.argv) > 1 else 50)
