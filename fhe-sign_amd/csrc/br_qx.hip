@@ -33,10 +33,12 @@ namespace fhe {
 
 namespace {
 // ---- layout parameters (tools/lds_layout_qx.py)
-constexpr int XW[10] = {1, 4, 16, 8, 2, 32, 65, 136, 266, 548};  // additive weights of index bits b0..b9
-constexpr int QB[4] = {7, 1, 0, 8};                                 // index bits on lane bits 3, 2, 1, 0 (B, B')
-constexpr int QE[6] = {8, 5, 7, 4, 6, 9};                           // index bits on lane bits 5..0 (E)
-constexpr int QW1 = 3, QW0 = 2;                                      // E wave bit 1 -> b3, wave bit 0 -> b2
+// (conflict-free for every read and write of the four layouts except the phase-B reads, 2-way; the
+// A-layout writes of the first choice were 2-way instead, PMC r4c: 2x the bank-conflict cycles of quad)
+constexpr int XW[10] = {2, 1, 4, 8, 16, 32, 65, 132, 264, 534};  // additive weights of index bits b0..b9
+constexpr int QB[4] = {8, 1, 0, 7};                                 // index bits on lane bits 3, 2, 1, 0 (B, B')
+constexpr int QE[6] = {5, 4, 8, 7, 6, 9};                           // index bits on lane bits 5..0 (E)
+constexpr int QW1 = 2, QW0 = 3;                                      // E wave bit 1 -> b2, wave bit 0 -> b3
 
 FHE_DEV constexpr int xq(int idx) {
     int p = 0;

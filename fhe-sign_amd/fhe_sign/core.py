@@ -212,8 +212,8 @@ class Context:
         check(load().fhe_ctx_sync(self._h))
 
     def set_br_kernel(self, kind: int) -> None:
-        """1 = 4 waves per ciphertext (the throughput kernel, the only one); 0 and 2, the retired
-        2-wave and pair kernels, are refused (FHE_ERR_INVALID)."""
+        """3 = br_qx.hip (classic default), 1 = br_quad.hip (always used for multi-bit); 0 and 2, the
+        retired 2-wave and pair kernels, are refused (FHE_ERR_INVALID)."""
         check(load().fhe_ctx_set_br_kernel(self._h, int(kind)))
 
     def set_ks_kernel(self, kind: int) -> None:

@@ -162,6 +162,7 @@ int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
 #define FHE_BR_PAIR 2
 #define FHE_BR_QX 3
 int fhe_ctx_set_br_kernel(fhe_ctx* ctx, int kind);
+
 /* Keyswitch: int8 matrix-core contraction against the KSK's byte planes (FHE_KS_MFMA, default) or
  * the 64-bit VALU kernel (FHE_KS_VALU).  Both are exact: identical small LWE words. */
 #define FHE_KS_VALU 0
