@@ -19,7 +19,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <queue>
+#include <string>
 #include <stdexcept>
 
 namespace fhe {
@@ -70,6 +72,7 @@ Engine::Engine(fhe_ctx* ctx) : ctx_(ctx) {
     // FHE_TRACE_LEVELS=1: synchronize after every level and print its size and wall time (stderr);
     // a diagnostic for schedule work, never set by the bench or the tests.
     if (const char* t = getenv("FHE_TRACE_LEVELS")) trace_ = atoi(t) != 0;
+    if (const char* t = getenv("FHE_GRAPH_STATS")) gstats_ = atoi(t) != 0;
     // FHE_SCHED=1: forward (deadline-driven) list scheduling instead of the default backward one
     if (const char* t = getenv("FHE_SCHED")) sched_ = atoi(t);
     // FHE_ROUND: level fill granule in bootstraps per GPU (schedule experiments; default 256)
@@ -242,6 +245,17 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         d.nterms = nt;
         d.lut = lut;
         d.cst = (uint64_t)dcst * delta;
+        if (gstats_) {
+            std::vector<std::pair<const uint64_t*, int32_t>> tk;
+            for (uint32_t u = 0; u < nt; ++u) tk.push_back({d.src[u], d.coef[u]});
+            std::sort(tk.begin(), tk.end());
+            std::string key(reinterpret_cast<const char*>(tk.data()), tk.size() * sizeof(tk[0]));
+            key.append(reinterpret_cast<const char*>(&dcst), sizeof dcst);
+            in_key_.push_back(std::move(key));
+            bool okr;
+            const uint64_t rr = reachable(live[i], csts[i], &okr);
+            in_deg_.push_back((uint8_t)(63 - __builtin_clzll(rr | 1)));
+        }
         d.dst = out[i].slot->p;
         out[i].slot->node = (int64_t)pending_.size();
         if (!n.deps.empty()) ++pending_dependent_;
@@ -386,6 +400,16 @@ void Engine::flush() {
             dead_nodes += N0 - live;
             std::vector<Pending> kept;
             kept.reserve(live);
+            if (gstats_ && in_key_.size() == N0) {
+                size_t o = 0;
+                for (size_t k = 0; k < N0; ++k)
+                    if (!dead[k]) {
+                        in_key_[o] = std::move(in_key_[k]);
+                        in_deg_[o++] = in_deg_[k];
+                    }
+                in_key_.resize(o);
+                in_deg_.resize(o);
+            }
             for (size_t k = 0; k < N0; ++k) {
                 if (dead[k]) continue;
                 Pending& n = pending_[k];
@@ -407,6 +431,7 @@ void Engine::flush() {
     const size_t N = pending_.size();
     std::vector<std::vector<int32_t>> deps(N);
     for (size_t k = 0; k < N; ++k) deps[k] = pending_[k].deps;
+    if (gstats_) graph_stats(deps);
     // a fanned-out level's round is one latency-kernel round on every rank
     const size_t round = (size_t)round_ * (size_t)std::max(1, ctx_->fanout_world());
     std::vector<std::vector<int32_t>> lv = schedule_levels(deps, sched_, round);
@@ -490,6 +515,56 @@ void Engine::flush() {
     pending_.clear();  // the stream orders any later reuse of the held slots behind these launches
     pending_dependent_ = 0;
     eager_ok_ = true;
+}
+
+// FHE_GRAPH_STATS: critical-path width (nodes with zero slack, asap == alap) and two-output candidates
+// (bootstraps whose input -- the same blocks, coefficients and constant -- another one also has, with
+// input degree <= 7, so that a half-box LUT pair could serve both from one blind rotation)
+void Engine::graph_stats(const std::vector<std::vector<int32_t>>& deps) {
+    const size_t N = deps.size();
+    if (in_key_.size() != N) {  // dropped dead nodes: their keys are gone from the count
+        fprintf(stderr, "[graph] %zu nodes (key bookkeeping skipped after dead-node removal)\n", N);
+        in_key_.clear();
+        in_deg_.clear();
+        return;
+    }
+    std::vector<int32_t> asap(N, 1), alap(N);
+    std::vector<std::vector<int32_t>> users(N);
+    int32_t L = 0;
+    for (size_t i = 0; i < N; ++i) {
+        for (int32_t d : deps[i]) {
+            asap[i] = std::max(asap[i], asap[d] + 1);
+            users[d].push_back((int32_t)i);
+        }
+        L = std::max(L, asap[i]);
+    }
+    std::vector<size_t> crit(L + 1, 0);
+    for (size_t k = N; k-- > 0;) {
+        alap[k] = L;
+        for (int32_t u : users[k]) alap[k] = std::min(alap[k], alap[u] - 1);
+        if (alap[k] == asap[k]) ++crit[asap[k]];
+    }
+    size_t ncrit = 0, maxc = 0;
+    for (size_t c : crit) {
+        ncrit += c;
+        maxc = std::max(maxc, c);
+    }
+    std::map<std::string, std::pair<size_t, size_t>> groups;  // key -> (count, count with degree <= 7)
+    for (size_t k = 0; k < N; ++k) {
+        auto& g = groups[in_key_[k]];
+        ++g.first;
+        if (in_deg_[k] <= 7) ++g.second;
+    }
+    size_t shared = 0, pairs7 = 0;
+    for (auto& kv : groups) {
+        if (kv.second.first > 1) shared += kv.second.first;
+        pairs7 += kv.second.second / 2;
+    }
+    fprintf(stderr, "[graph] %zu nodes, %d levels, critical %zu (max %zu per level), shared-input nodes %zu, "
+                    "degree<=7 pairs %zu (%.1f %% of the nodes saved by two-output blind rotations)\n",
+            N, L, ncrit, maxc, shared, pairs7, 100.0 * pairs7 / std::max<size_t>(1, N));
+    in_key_.clear();
+    in_deg_.clear();
 }
 
 Block Engine::lincomb(const std::vector<Term>& terms, uint32_t cst) {

@@ -144,6 +144,11 @@ private:
     uint64_t* d_up_ = nullptr;  // upload staging: n big LWEs, then n destination pointers
     size_t up_cap_ = 0;
     bool trace_ = false;
+    // FHE_GRAPH_STATS=1: per flush, the critical-path width and the bootstraps that share their exact
+    // input with another one at input degree <= 7 (two-output blind rotation candidates); stderr
+    bool gstats_ = false;
+    std::vector<uint8_t> in_deg_;              // gstats_: max input value of each pending node
+    std::vector<std::string> in_key_;          // gstats_: the node's input (terms + constant)
     int sched_ = 0;
     int round_ = 256;  // level fill granule (bootstraps per GPU)
     double run_ns_ = 0.0;  // host time inside run() (trace)
@@ -164,6 +169,7 @@ private:
     PbsDesc* d_desc_ = nullptr;
     size_t d_desc_cap_ = 0;
     void ensure_desc(size_t n);
+    void graph_stats(const std::vector<std::vector<int32_t>>& deps);
     PbsDesc* stage_desc(size_t n, PbsDesc** dev);
 };
 
