@@ -373,7 +373,12 @@ int fhe_radix_cast(fhe_ctx* c, const fhe_radix* a, uint32_t bits, fhe_radix** ou
 }
 int fhe_schedule_levels(const int32_t* off, const int32_t* deps, size_t n, int mode, int32_t* level_of,
                         int32_t* nlevels) {
-    if ((n && (!off || !level_of)) || !nlevels || (mode != 0 && mode != 1)) return FHE_ERR_INVALID;
+    return fhe_schedule_levels_ranks(off, deps, n, mode, 1, level_of, nlevels);
+}
+
+int fhe_schedule_levels_ranks(const int32_t* off, const int32_t* deps, size_t n, int mode, int ranks, int32_t* level_of,
+                              int32_t* nlevels) {
+    if ((n && (!off || !level_of)) || !nlevels || (mode != 0 && mode != 1) || ranks < 1) return FHE_ERR_INVALID;
     return guarded([&] {
         std::vector<std::vector<int32_t>> g(n);
         for (size_t i = 0; i < n; ++i)
@@ -381,7 +386,8 @@ int fhe_schedule_levels(const int32_t* off, const int32_t* deps, size_t n, int m
                 engine_check(deps && deps[k] >= 0 && (size_t)deps[k] < i, "dependency must name an earlier node");
                 g[i].push_back(deps[k]);
             }
-        std::vector<std::vector<int32_t>> lv = schedule_levels(g, mode);
+        // the engine's flush (radix.cpp): a fanned-out level's fill granule is one latency round per rank
+        std::vector<std::vector<int32_t>> lv = schedule_levels(g, mode, (size_t)256 * (size_t)ranks);
         for (size_t l = 0; l < lv.size(); ++l)
             for (int32_t i : lv[l]) level_of[i] = (int32_t)l + 1;
         *nlevels = (int32_t)lv.size();

@@ -129,6 +129,8 @@ _SIGNATURES = [
     ("fhe_ctx_rank_pbs", C.c_int, [C.c_void_p, u64p]),
     ("fhe_schedule_levels", C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_size_t, C.c_int,
                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    ("fhe_schedule_levels_ranks", C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_size_t, C.c_int, C.c_int,
+                                            C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("fhe_biguint_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_from_digits", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_size_t)]),

@@ -304,6 +304,11 @@ int fhe_ctx_rank_pbs(const fhe_ctx* ctx, uint64_t* pbs);
  * list scheduling (the engine's default), 1: forward deadline-driven (FHE_SCHED=1). */
 int fhe_schedule_levels(const int32_t* dep_offsets, const int32_t* deps, size_t n, int mode, int32_t* level_of,
                         int32_t* nlevels);
+/* The same as the engine schedules under a fan-out over `ranks` GPUs: levels are filled to whole
+ * latency rounds of every rank (multiples of 256 x ranks), so a filled level is split over the ranks
+ * (fhe_ctx_set_fanout) and each rank's slice is at most one round. */
+int fhe_schedule_levels_ranks(const int32_t* dep_offsets, const int32_t* deps, size_t n, int mode, int ranks,
+                              int32_t* level_of, int32_t* nlevels);
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */

@@ -12,7 +12,7 @@ import pytest
 from fhe_sign import _lib
 
 
-def schedule(deps, mode=0):
+def schedule(deps, mode=0, ranks=1):
     n = len(deps)
     off = np.zeros(n + 1, np.int32)
     for i, d in enumerate(deps):
@@ -21,8 +21,8 @@ def schedule(deps, mode=0):
     level = np.zeros(max(n, 1), np.int32)
     nl = C.c_int32()
     P = C.POINTER(C.c_int32)
-    rc = _lib.load().fhe_schedule_levels(off.ctypes.data_as(P), flat.ctypes.data_as(P), n, mode,
-                                         level.ctypes.data_as(P), C.byref(nl))
+    rc = _lib.load().fhe_schedule_levels_ranks(off.ctypes.data_as(P), flat.ctypes.data_as(P), n, mode, ranks,
+                                               level.ctypes.data_as(P), C.byref(nl))
     assert rc == 0, _lib.load().fhe_last_error()
     return level[:n].tolist(), nl.value
 
@@ -80,6 +80,52 @@ def test_chain_with_background_work():
     assert sizes[:2].sum() > 20000  # the rest as large early batches
     lf, nf = schedule(deps, 1)
     check(deps, lf, nf)
+
+
+FANOUT_MIN = 257  # bench.py / fhe_ctx_set_fanout default: levels of at least this many bootstraps are split
+
+
+def chain_graph(steps=100, width=64, jobs_n=20000):
+    deps, prev, jobs = [], [], []
+    for j in range(jobs_n):
+        deps.append([])
+        deps.append([len(deps) - 1])
+        jobs.append(len(deps) - 1)
+    for step in range(steps):
+        cur = []
+        for k in range(width):
+            d = list(prev[max(0, k - 2):k + 1]) + [jobs[(step * 200 + k) % len(jobs)]]
+            deps.append(sorted(set(d)))
+            cur.append(len(deps) - 1)
+        prev = cur
+    return deps
+
+
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+def test_fanout_partition_divides_the_fill(ranks):
+    """The fan-out partition (config 5a) on the chain-with-background graph, as the engine's flush runs
+    it over N ranks (levels filled to one latency round PER RANK, 256 N): the level count stays the
+    chain's; the 40000 off-chain bootstraps ride inside the chain levels, the filled ones reach the
+    split threshold and are divided over the ranks, so no rank's slice of any level exceeds one round:
+    the op takes exactly as many latency rounds as the chain has levels (the 1-GPU schedule needs ~80
+    more rounds for the fill).  Levels below the threshold -- the chain plus fill that cannot move later
+    -- run redundantly: one round either way, so splitting them would only add a collective."""
+    deps = chain_graph()
+    level, nl = schedule(deps, 0, ranks)
+    check(deps, level, nl)
+    assert nl == 102
+    sizes = np.bincount(level, minlength=nl + 1)[1:]
+    assert (sizes <= 256 * ranks).all()
+    split = sizes >= FANOUT_MIN
+    per_rank = [(-(-int(g) // ranks) if s else int(g)) for g, s in zip(sizes, split)]
+    assert max(per_rank) <= 256  # every level is one latency round on every rank
+    rounds = sum(-(-p // 256) for p in per_rank)
+    assert rounds == nl  # every level is one round on every rank: the chain's floor
+    assert sum(per_rank) < len(deps) * 0.6  # each rank runs well under the whole graph
+    l1, n1 = schedule(deps, 0, 1)
+    assert n1 == nl
+    rounds1 = sum(-(-int(g) // 256) for g in np.bincount(l1, minlength=n1 + 1)[1:])
+    assert rounds1 > nl + 70
 
 
 def test_invalid_graph_rejected():
