@@ -6,6 +6,7 @@
 // boundaries (the carry-propagation rounds), never inside a bootstrap.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <thread>
@@ -163,8 +164,12 @@ void fhe_ctx::mark_progress() {
 
 int fhe_ctx::allreduce_min_u8(uint8_t* flags, size_t n) {
     if (!comm || n == 0) return FHE_OK;
-    uint8_t* d = nullptr;
-    FHE_HIP_CHECK(hipMalloc(&d, n));
+    if (n > flags_cap) {  // grown rarely (a hipFree synchronises the device)
+        if (d_flags) FHE_HIP_CHECK(hipFree(d_flags));
+        flags_cap = std::max<size_t>(n, 1 << 16);
+        FHE_HIP_CHECK(hipMalloc(&d_flags, flags_cap));
+    }
+    uint8_t* d = d_flags;
     ncclComm_t cm = (ncclComm_t)comm;
     int rc = hipMemcpyAsync(d, flags, n, hipMemcpyHostToDevice, stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc)
@@ -173,7 +178,6 @@ int fhe_ctx::allreduce_min_u8(uint8_t* flags, size_t n) {
     if (!rc) rc = hipMemcpyAsync(flags, d, n, hipMemcpyDeviceToHost, stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = comm_wait_impl(this, "ncclAllReduce (dead nodes)");
     if (comm) (void)hipStreamSynchronize(stream);
-    (void)hipFree(d);
     return rc;
 }
 

@@ -565,7 +565,7 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     c->engine = nullptr;
     c->release_comm();
     void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
-                    c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_mono, c->d_bsk_qx, c->d_zeta_full, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
+                    c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_mono, c->d_bsk_qx, c->d_zeta_full, c->d_flags, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)

@@ -118,6 +118,8 @@ struct fhe_ctx {
     // *flags (one byte per entry) = min over the ranks, in place (one all-reduce; a no-op without a
     // communicator).  The engine's dead-node agreement.
     int allreduce_min_u8(uint8_t* flags, size_t n);
+    uint8_t* d_flags = nullptr;  // device staging of allreduce_min_u8 (grown, freed with the context)
+    size_t flags_cap = 0;
 
     int ensure_ms(size_t count);
     int ensure_ks(size_t count);
