@@ -434,7 +434,19 @@ def pbs_leg(a, kind, dist, rank, world, device):
         ctx.pbs(cts, lid)
     pcie_rate = host_reps * B / (time.perf_counter() - t0)
 
+    # the latency kernel at the level sizes of the serial carry chains (one ciphertext per CU): best of
+    # 3 blind-rotate times (HIP events) at B = 1 and 256 -- the per-level floor of the compat mul / sign
+    lat = {}
+    ctx.enable_timing(True)
+    for nb in (1, 256):
+        best = 1e9
+        for _ in range(3):
+            ctx.pbs_device(d_in, nb, d_lut, d_out)
+            best = min(best, ctx.last_pbs_timing()[1])
+        lat[f"B={nb}"] = best
+    ctx.enable_timing(False)
     # correctness spot check of the last step (decrypt a sample)
+    ctx.pbs_device(d_in, B, d_lut, d_out)
     out = np.zeros_like(cts)
     ctx.d2h(out, d_out)
     ok = all(ck.decrypt_block(out[i]) == (i % 16 + 1) % 16 for i in range(0, B, max(1, B // 64)))
@@ -479,6 +491,7 @@ def pbs_leg(a, kind, dist, rank, world, device):
                    "bytes_per_launch": l2_bytes},
         },
         "pcie_inclusive_pbs_per_s": pcie_rate * world,  # per-rank host-buffer rate x ranks
+        "latency_level_ms": lat,
     }
     return ck, ctx, res
 
@@ -561,6 +574,7 @@ def main():
         res["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
                                           "speedup": v / ops[k]["seconds"]} for k, v in readme.items() if k in ops}
     res["pcie_inclusive_pbs_per_s"] = cl["pcie_inclusive_pbs_per_s"]
+    res["latency_level_ms"] = cl["latency_level_ms"]  # blind rotate of one latency level, B = 1 / 256
     if mb is not None:
         # tfhe-rs' MultiBitPBS shape (grouping factor 2) on the same client key: same decrypted results
         t_mb, src_mb = pmc_traffic(B, "k_blind_rotate_quad<2>")
