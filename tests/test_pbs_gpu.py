@@ -166,9 +166,9 @@ def test_zero_and_sparse_masks_both_kernels(env):
         assert ok.decrypt(ref[m]) == tables[lut_of[m]][m]
 
 
-@pytest.mark.parametrize("kind", [3, 1])  # FHE_BR_QX (classic default, br_qx.hip), FHE_BR_QUAD (br_quad.hip)
+@pytest.mark.parametrize("kind", [3, 4, 1])  # FHE_BR_QX (br_qx.hip), FHE_BR_QY (br_qy.hip), FHE_BR_QUAD (br_quad.hip)
 def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
-    """Both throughput kernels at ragged batches (1, 2, 3, 37, 259) with every LUT give the latency
+    """The throughput kernels at ragged batches (1, 2, 3, 37, 259) with every LUT give the latency
     kernel's and the oracle's words (multi-bit parameters always run br_quad.hip); the retired
     blind-rotate kernels (0: round-1 2-wave, 2: the pair kernel) are refused."""
     _, _, ok, ctx = env
@@ -191,14 +191,14 @@ def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
         assert not bad, f"kernel {kind}, batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(thr[37][:6], ref)
-    for bad_kind in (0, 2, 4):
+    for bad_kind in (0, 2, 5):
         with pytest.raises(Exception):
             ctx.set_br_kernel(bad_kind)
 
 
 def test_throughput_kernels_identical_at_full_batch(env):
-    """br_qx.hip and br_quad.hip on the same 4096 distinct encryptions (16 rounds of 256 CUs): every
-    output word identical, a seeded sample of 8 equal to the oracle."""
+    """br_qx.hip, br_qy.hip and br_quad.hip on the same 4096 distinct encryptions (16 rounds of 256
+    CUs): every output word identical, a seeded sample of 8 equal to the oracle."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = np.array([ctx.lut(t) for t in tables], np.uint32)
@@ -211,10 +211,13 @@ def test_throughput_kernels_identical_at_full_batch(env):
         quad = ctx.pbs(cts, ids[lut_of])
         ctx.set_br_kernel(3)
         qx = ctx.pbs(cts, ids[lut_of])
+        ctx.set_br_kernel(4)
+        qy = ctx.pbs(cts, ids[lut_of])
     finally:
         ctx.set_br_kernel(3)
-    bad = np.flatnonzero((quad != qx).any(axis=1))
-    assert bad.size == 0, f"{bad.size} ciphertexts differ between the throughput kernels, first {bad[:5]}"
+    for name, other in (("quad", quad), ("qy", qy)):
+        bad = np.flatnonzero((other != qx).any(axis=1))
+        assert bad.size == 0, f"{bad.size} ciphertexts differ between qx and {name}, first {bad[:5]}"
     pick = np.array([0, 1, 513, 1024, 2047, 2048, 3333, 4095])
     ref = ok.pbs_batch(np.ascontiguousarray(cts[pick]), np.stack([ok.make_lut(t) for t in tables]),
                        lut_of[pick].astype(np.uint32))
