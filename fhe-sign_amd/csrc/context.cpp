@@ -279,9 +279,9 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     if ((int)count <= wide_threshold)
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
-    if (p.grouping == 1 && br_kernel == FHE_BR_QY && d_bsk_qx)
+    if (p.grouping == 1 && (br_kernel == FHE_BR_QY || br_kernel == FHE_BR_QYL) && d_bsk_qx)
         return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
-                                      d_zeta_full, d_mono, out, (int)count, (int)p.n, stream);
+                                      d_zeta_full, d_mono, out, (int)count, (int)p.n, br_kernel == FHE_BR_QYL, stream);
     if (p.grouping == 1 && br_kernel == FHE_BR_QX && d_bsk_qx)
         return launch_blind_rotate_qx(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
                                       d_zeta_full, d_mono, out, (int)count, (int)p.n, stream);
@@ -762,7 +762,7 @@ int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
                   "FHE_BR_QUAD is the throughput kernel");
         return FHE_ERR_INVALID;
     }
-    if (kind != FHE_BR_QUAD && kind != FHE_BR_QX && kind != FHE_BR_QY) return FHE_ERR_INVALID;
+    if (kind != FHE_BR_QUAD && kind != FHE_BR_QX && kind != FHE_BR_QY && kind != FHE_BR_QYL) return FHE_ERR_INVALID;
     c->br_kernel = kind;
     return FHE_OK;
 }

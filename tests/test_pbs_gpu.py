@@ -166,7 +166,7 @@ def test_zero_and_sparse_masks_both_kernels(env):
         assert ok.decrypt(ref[m]) == tables[lut_of[m]][m]
 
 
-@pytest.mark.parametrize("kind", [3, 4, 1])  # FHE_BR_QX (br_qx.hip), FHE_BR_QY (br_qy.hip), FHE_BR_QUAD (br_quad.hip)
+@pytest.mark.parametrize("kind", [3, 4, 5, 1])  # FHE_BR_QX (br_qx.hip), FHE_BR_QY / QYL (br_qy.hip), FHE_BR_QUAD
 def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
     """The throughput kernels at ragged batches (1, 2, 3, 37, 259) with every LUT give the latency
     kernel's and the oracle's words (multi-bit parameters always run br_quad.hip); the retired
@@ -191,14 +191,14 @@ def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
         assert not bad, f"kernel {kind}, batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(thr[37][:6], ref)
-    for bad_kind in (0, 2, 5):
+    for bad_kind in (0, 2, 6):
         with pytest.raises(Exception):
             ctx.set_br_kernel(bad_kind)
 
 
 def test_throughput_kernels_identical_at_full_batch(env):
-    """br_qx.hip, br_qy.hip and br_quad.hip on the same 4096 distinct encryptions (16 rounds of 256
-    CUs): every output word identical, a seeded sample of 8 equal to the oracle."""
+    """br_qx.hip, br_qy.hip (both tunings) and br_quad.hip on the same 4096 distinct encryptions (16
+    rounds of 256 CUs): every output word identical, a seeded sample of 8 equal to the oracle."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = np.array([ctx.lut(t) for t in tables], np.uint32)
@@ -213,9 +213,11 @@ def test_throughput_kernels_identical_at_full_batch(env):
         qx = ctx.pbs(cts, ids[lut_of])
         ctx.set_br_kernel(4)
         qy = ctx.pbs(cts, ids[lut_of])
+        ctx.set_br_kernel(5)
+        qyl = ctx.pbs(cts, ids[lut_of])
     finally:
         ctx.set_br_kernel(3)
-    for name, other in (("quad", quad), ("qy", qy)):
+    for name, other in (("quad", quad), ("qy", qy), ("qyl", qyl)):
         bad = np.flatnonzero((other != qx).any(axis=1))
         assert bad.size == 0, f"{bad.size} ciphertexts differ between qx and {name}, first {bad[:5]}"
     pick = np.array([0, 1, 513, 1024, 2047, 2048, 3333, 4095])
