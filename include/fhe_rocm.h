@@ -151,6 +151,13 @@ int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
+/* Latency-level blind rotate (batches of at most the threshold, classic parameters): FHE_LAT_WIDE
+ * (br_wide.hip, 8 waves per ciphertext) or FHE_LAT_QYL (br_qy.hip tuned for one ciphertext per CU,
+ * 4 waves).  Multi-bit latency levels always run br_wide.hip.  Identical bits either way.  The
+ * environment variable FHE_LAT_KERNEL sets the initial choice of every new context. */
+#define FHE_LAT_WIDE 0
+#define FHE_LAT_QYL 1
+int fhe_ctx_set_lat_kernel(fhe_ctx* ctx, int kind);
 /* Throughput blind-rotate kernel for levels above the threshold, 4 waves per ciphertext:
  * FHE_BR_QX (default; classic parameters: the round-4 layouts without DPP transposes, br_qx.hip),
  * FHE_BR_QY (classic: the same with two instead of four workgroup barriers per CMUX, br_qy.hip),

@@ -135,6 +135,32 @@ def test_wide_and_quad_kernels_bit_identical(env):
     assert np.array_equal(wide[:6], ref)
 
 
+def test_latency_kernel_choice_bit_identical(env):
+    """Latency levels (batch <= the threshold) through either latency kernel -- br_wide.hip or
+    br_qy.hip's one-ciphertext-per-CU tuning (FHE_LAT_QYL; multi-bit levels stay on br_wide.hip) --
+    give identical words at B = 1, 37, 256, equal to the oracle; an unknown kind is refused."""
+    _, _, ok, ctx = env
+    tables = _luts()
+    ids = [ctx.lut(t) for t in tables]
+    r = ok.rng(4242)
+    cts = np.stack([ok.encrypt(r, (5 * i + 3) % 16) for i in range(256)])
+    lut_ids = np.array([ids[i % len(ids)] for i in range(256)], np.uint32)
+    with pytest.raises(Exception):
+        ctx.set_lat_kernel(2)
+    got = {}
+    try:
+        for kind in (0, 1):
+            ctx.set_lat_kernel(kind)
+            got[kind] = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 37, 256)}
+    finally:
+        ctx.set_lat_kernel(0)
+    for c in (1, 37, 256):
+        bad = np.flatnonzero((got[0][c] != got[1][c]).any(axis=1))
+        assert bad.size == 0, f"batch {c}: ciphertexts {bad[:5]} differ between the latency kernels"
+    ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
+    assert np.array_equal(got[1][37][:6], ref)
+
+
 def test_zero_and_sparse_masks_both_kernels(env):
     """Ciphertexts whose modulus-switched mask is 0 at every key bit (trivial encryptions: mask 0,
     body m delta -- every CMUX is an a = 0 step, the kernels run it with e - 1 = 0 while the oracle
