@@ -162,7 +162,7 @@ def cpu_baseline(seed, target_s, op_levels=None):
     return res
 
 
-def pmc_traffic(batch, kernel="k_blind_rotate_qx"):
+def pmc_traffic(batch, kernel="k_blind_rotate_qy"):
     """HBM-side bytes per launch of the blind-rotate kernel at this batch, from the committed PMC
     summary of the same kernel (tools/profile_round.sh; FETCH_SIZE x2 + WRITE_SIZE, gfx950
     correction of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits included)"""
@@ -474,7 +474,7 @@ def pbs_leg(a, kind, dist, rank, world, device):
         "roofline": {
             "bound": "fp64_valu",
             "compute_pipe": "fp64 VALU (FFT butterflies; no dense contraction on the path)",
-            "kernel": "k_blind_rotate_qx" if kind == "classic" else "k_blind_rotate_quad<2>",
+            "kernel": "k_blind_rotate_qy" if kind == "classic" else "k_blind_rotate_quad<2>",
             "achieved": achieved,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",

@@ -85,23 +85,7 @@ FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
 }
 }  // namespace
 
-// LAT = true (FHE_BR_QYL): the same kernel tuned for one ciphertext per CU (latency levels): one wave
-// per SIMD, so the register file is not the occupancy limit -- the step-invariant twiddles and untwist
-// factors are read once into registers instead of from LDS / global memory every step, and all 16 key
-// slices of step i + 1 are issued right after step i's MAC (in flight across a whole inverse and
-// forward transform instead of a few dozen instructions).  Identical arithmetic, identical bits.
-// (QYL_TW / QYL_PST / QYL_KPRE = 0: variant builds without one of the three, tools/gpu_lat.sh)
-#ifndef QYL_TW
-#define QYL_TW 1
-#endif
-#ifndef QYL_PST
-#define QYL_PST 1
-#endif
-#ifndef QYL_KPRE
-#define QYL_KPRE 1
-#endif
-template <bool LAT0>
-__global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uint64_t* __restrict__ ms, int ms_stride,
+__global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __restrict__ ms, int ms_stride,
                                                             const PbsDesc* __restrict__ desc,
                                                             const uint32_t* __restrict__ lut_idx,
                                                             const uint64_t* __restrict__ luts,
@@ -109,7 +93,6 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
                                                             const cplx* __restrict__ ps, const cplx* __restrict__ Z,
                                                             const cplx* __restrict__ mono, uint64_t* __restrict__ out,
                                                             int n) {
-    constexpr bool LAT = LAT0 && QYL_TW, LATP = LAT0 && QYL_PST, LATK = LAT0 && QYL_KPRE;
     constexpr int XL_W = 2 * XR_SZ, XL_Z = XL_W + XTW_SZ, XL_T = XL_Z + XZ_SZ;
     __shared__ __attribute__((aligned(16))) cplx s_lds[XL_T + XT_SZ];
     cplx* s_w = s_lds + XL_W;
@@ -184,31 +167,18 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
     auto lane_factor = [&](uint32_t a) { return bptr{mono_rs, ((c4 * a) & 4095u) * 16u, 0u}[0]; };
     cplx Fn = pair_factor(a_next), Ebn = lane_factor(a_next);
     __syncthreads();
-    // LAT: step-invariant tables in registers (the non-LAT kernel reads them where they are used)
-    cplx tz[7], tv[10], pst0[8];
-    if constexpr (LAT) {
-        tz[0] = s_z[k98], tz[1] = s_z[4 + 2 * k98], tz[2] = s_z[5 + 2 * k98];
-        tz[3] = s_z[12 + U], tz[4] = s_z[44 + U], tz[5] = s_z[76 + U], tz[6] = s_z[108 + U];
-        const cplx* t2 = s_t + 5 * m2;
-        tv[0] = t2[0], tv[1] = t2[1], tv[2] = t2[2], tv[3] = t2[3];
-        tv[4] = s_t[20 + 17 * h + kB], tv[5] = s_t[54 + 17 * h + kB];
-        tv[6] = s_w[tpos(4 * u)], tv[7] = s_w[tpos(2 * u)], tv[8] = s_w[tpos(u)], tv[9] = s_w[tpos(u + 128)];
+#ifdef QY_STAGGER
+    // (variant build only) the first round of workgroups starts in lockstep, three per CU: offset the
+    // second and third by a third and two thirds of a CMUX so their barriers and LDS phases interleave
+    if (blockIdx.x < 768u && blockIdx.x >= 256u) {
+        __builtin_amdgcn_s_sleep(QY_STAGGER);
+        if (blockIdx.x >= 512u) __builtin_amdgcn_s_sleep(QY_STAGGER);
     }
-    if constexpr (LATP) {
-        const bptr P{table_rsrc(ps), 16u * (uint32_t)u, 0u};
-#pragma unroll
-        for (int r = 0; r < 8; ++r) pst0[r] = P[1024 + 128 * r];
-    }
+#endif
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
     const cplx* Zu = Z;  // uniform zetas of stages 0-2: Z[1], Z[2], Z[4], Z[6]
     uint32_t upd = 0;
     bool red_in = false;
-    cplx Kb[16];  // key slices of the step in the E layout [4 (row, column) + point k]
-    if constexpr (LATK) {
-        const bptr kb{bsk_rs, 16u * (uint32_t)L, (uint32_t)(w * 256) * 16u};
-#pragma unroll
-        for (int q = 0; q < 16; ++q) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
-    }
     for (int i = 0; i < n; ++i) {
         const uint32_t a = a_next;
         a_next = a_next1;
@@ -248,8 +218,7 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
             if (!(r & 2)) qx_permlane<4>(x[r], x[r + 2]);
         // ---- phase B: stages 3 (b6, register bit 2), 4 (b5, bit 1); b7 = register bit 0
         {
-            const cplx z3 = LAT ? tz[0] : s_z[k98], z4a = LAT ? tz[1] : s_z[4 + 2 * k98],
-                       z4b = LAT ? tz[2] : s_z[5 + 2 * k98];
+            const cplx z3 = s_z[k98], z4a = s_z[4 + 2 * k98], z4b = s_z[5 + 2 * k98];
 #pragma unroll
             for (int r = 0; r < 4; ++r) dit_bfly(x[r], x[r + 4], (r & 1) ? mul_i(z3) : z3);  // block (b9 b8 b7)
 #pragma unroll
@@ -267,8 +236,7 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
         for (int r = 0; r < 8; ++r) x[r] = reg[bBp + xq(idx_Bp(0, 0, r))];
         // ---- phase B': stages 5 (b4, register bit 2), 6 (b3, bit 1), 7 (b2, bit 0)
         {
-            const cplx z5 = LAT ? tz[3] : s_z[12 + U], z6 = LAT ? tz[4] : s_z[44 + U],
-                       z7a = LAT ? tz[5] : s_z[76 + U], z7b = LAT ? tz[6] : s_z[108 + U];
+            const cplx z5 = s_z[12 + U], z6 = s_z[44 + U], z7a = s_z[76 + U], z7b = s_z[108 + U];
 #pragma unroll
             for (int r = 0; r < 4; ++r) dit_bfly(x[r], x[r + 4], z5);
 #pragma unroll
@@ -282,13 +250,11 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
         }
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bBp + xq(idx_Bp(0, 0, r))] = x[r];
-        // key slices of this step (row, column, point k): points 0, 1 now, in flight across the barrier,
-        // 2, 3 after it (LAT: all issued after the previous step's MAC)
-        if constexpr (!LATK) {
+        // key slices of this step in the E layout (row, column, point k): in flight across the barrier
+        cplx Kb[16];  // [4 (row, column) + point k]; points 0, 1 now, 2, 3 after the barrier
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if ((q & 3) < 2) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
-        }
+        for (int q = 0; q < 16; ++q)
+            if ((q & 3) < 2) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
         const cplx e0 = cmul(Ebn, Fn);  // exact when kk = 0 (Fn = E[0] = 1)
         Fn = pair_factor(a_next);
         Ebn = lane_factor(a_next);
@@ -296,11 +262,9 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
         // ---- phase E: both polynomials at this wave's points, stages 8 (b1), 9 (b0)
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
-        if constexpr (!LATK) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if ((q & 3) >= 2) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
-        }
+        for (int q = 0; q < 16; ++q)
+            if ((q & 3) >= 2) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
 #pragma unroll
         for (int r = 0; r < 8; ++r)
             if (!(r & 2)) dit_bfly(x[r], x[r + 2], z8);
@@ -316,13 +280,6 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
             const cplx wv = k == 0 ? make_double2(e0.x - 1.0, e0.y) : turn_sel_m1(e0, tr);
             x[k] = cmul(o0, wv);
             x[4 + k] = cmul(o1, wv);
-        }
-        if constexpr (LATK) {  // the next step's key slices, in flight across the inverse and forward
-            if (i + 1 < n) {
-                const bptr kn{bsk_rs, 16u * (uint32_t)L, (uint32_t)((i + 1) * 4096 + w * 256) * 16u};
-#pragma unroll
-                for (int q = 0; q < 16; ++q) Kb[q] = kn[(q >> 2) * 1024 + (q & 3) * 64];
-            }
         }
         // ---- inverse: b0 (twiddle 1), b1 (twiddles 1, -i) in E
 #pragma unroll
@@ -345,11 +302,11 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
         for (int r = 0; r < 8; ++r) x[r] = reg[bBp + xq(idx_Bp(0, 0, r))];
         {
             const cplx* t2 = s_t + 5 * m2;
-            const cplx w2 = conj_(LAT ? tv[0] : t2[0]);
+            const cplx w2 = conj_(t2[0]);
             dit_pairs<0>(x, [&](int) { return w2; });
-            const cplx w3 = LAT ? tv[1] : t2[1];
+            const cplx w3 = t2[1];
             dit_pairs<1>(x, [&](int r) { return conj_((r & 1) ? mul_i(w3) : w3); });    // b2 = register bit 0
-            const cplx w4a = LAT ? tv[2] : t2[2], w4b = LAT ? tv[3] : t2[3];
+            const cplx w4a = t2[2], w4b = t2[3];
             dit_pairs<2>(x, [&](int r) {                                                 // b3 b2 = bits 1, 0
                 const cplx base = (r & 1) ? w4b : w4a;
                 return conj_((r & 2) ? mul_i(base) : base);
@@ -363,9 +320,9 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
         for (int r = 0; r < 8; ++r) x[r] = reg[bB + xq(idx_B(0, 0, r))];
         cplx pst[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) pst[r] = LATP ? pst0[r] : P[1024 + 128 * r];
+        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
         {
-            const cplx w5 = LAT ? tv[4] : s_t[20 + 17 * h + kB], w6 = LAT ? tv[5] : s_t[54 + 17 * h + kB];
+            const cplx w5 = s_t[20 + 17 * h + kB], w6 = s_t[54 + 17 * h + kB];
             dit_pairs<1>(x, [&](int) { return conj_(w5); });
             dit_pairs<2>(x, [&](int r) { return conj_((r & 2) ? mul_i(w6) : w6); });     // b5 = register bit 1
         }
@@ -377,11 +334,11 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
             if (!(r & 2)) qx_permlane<4>(x[r], x[r + 2]);
         // ---- A (inverse): b7 (register bit 0), b8 (bit 1), b9 (bit 2)
         {
-            const cplx w7 = LAT ? tv[6] : s_w[tpos(4 * u)];
+            const cplx w7 = s_w[tpos(4 * u)];
             dit_pairs<0>(x, [&](int) { return conj_(w7); });
-            const cplx w8 = LAT ? tv[7] : s_w[tpos(2 * u)];
+            const cplx w8 = s_w[tpos(2 * u)];
             dit_pairs<1>(x, [&](int r) { return conj_((r & 1) ? mul_i(w8) : w8); });
-            const cplx w9a = LAT ? tv[8] : s_w[tpos(u)], w9b = LAT ? tv[9] : s_w[tpos(u + 128)];
+            const cplx w9a = s_w[tpos(u)], w9b = s_w[tpos(u + 128)];
             dit_pairs<2>(x, [&](int r) {
                 const cplx base = (r & 1) ? w9b : w9a;
                 return conj_((r & 2) ? mul_i(base) : base);
@@ -416,15 +373,10 @@ __global__ __launch_bounds__(256, LAT0 ? 1 : 3) void k_blind_rotate_qy(const uin
 
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                   const uint64_t* luts, const cplx* bsk_qx, const cplx* tw, const cplx* ps,
-                                  const cplx* zfull, const cplx* mono, uint64_t* out, int count, int n, bool lat,
-                                  hipStream_t s) {
+                                  const cplx* zfull, const cplx* mono, uint64_t* out, int count, int n, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    if (lat)
-        hipLaunchKernelGGL(k_blind_rotate_qy<true>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
-                           bsk_qx, tw, ps, zfull, mono, out, n);
-    else
-        hipLaunchKernelGGL(k_blind_rotate_qy<false>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
-                           bsk_qx, tw, ps, zfull, mono, out, n);
+    hipLaunchKernelGGL(k_blind_rotate_qy, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk_qx,
+                       tw, ps, zfull, mono, out, n);
     return hipGetLastError();
 }
 

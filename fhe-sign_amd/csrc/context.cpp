@@ -276,15 +276,12 @@ hipError_t fhe_ctx::keyswitch(const uint64_t* in, const fhe::PbsDesc* desc, size
 }
 
 hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_idx, uint64_t* out, size_t count) {
-    if ((int)count <= wide_threshold && p.grouping == 1 && lat_kernel == FHE_LAT_QYL && d_bsk_qx)
-        return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
-                                      d_zeta_full, d_mono, out, (int)count, (int)p.n, true, stream);
     if ((int)count <= wide_threshold)
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
-    if (p.grouping == 1 && (br_kernel == FHE_BR_QY || br_kernel == FHE_BR_QYL) && d_bsk_qx)
+    if (p.grouping == 1 && br_kernel == FHE_BR_QY && d_bsk_qx)
         return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
-                                      d_zeta_full, d_mono, out, (int)count, (int)p.n, br_kernel == FHE_BR_QYL, stream);
+                                      d_zeta_full, d_mono, out, (int)count, (int)p.n, stream);
     if (p.grouping == 1 && br_kernel == FHE_BR_QX && d_bsk_qx)
         return launch_blind_rotate_qx(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
                                       d_zeta_full, d_mono, out, (int)count, (int)p.n, stream);
@@ -551,7 +548,6 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
     FHE_HIP_CHECK(hipMemcpy(c->d_tw_wide, tww.data(), tww.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMemcpy(c->d_psi_wide, psiw.data(), psiw.size() * sizeof(double2), hipMemcpyHostToDevice));
     if (const char* e = getenv("FHE_WIDE_THRESHOLD")) c->wide_threshold = atoi(e);
-    if (const char* e = getenv("FHE_LAT_KERNEL")) c->lat_kernel = atoi(e) == FHE_LAT_QYL ? FHE_LAT_QYL : FHE_LAT_WIDE;
     std::vector<double2> mono;
     mono_table(psi, &mono);
     FHE_HIP_CHECK(hipMalloc(&c->d_mono, mono.size() * sizeof(double2)));
@@ -766,14 +762,8 @@ int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
                   "FHE_BR_QUAD is the throughput kernel");
         return FHE_ERR_INVALID;
     }
-    if (kind != FHE_BR_QUAD && kind != FHE_BR_QX && kind != FHE_BR_QY && kind != FHE_BR_QYL) return FHE_ERR_INVALID;
+    if (kind != FHE_BR_QUAD && kind != FHE_BR_QX && kind != FHE_BR_QY) return FHE_ERR_INVALID;
     c->br_kernel = kind;
-    return FHE_OK;
-}
-
-int fhe_ctx_set_lat_kernel(fhe_ctx* c, int kind) {
-    if (!c || (kind != FHE_LAT_WIDE && kind != FHE_LAT_QYL)) return FHE_ERR_INVALID;
-    c->lat_kernel = kind;
     return FHE_OK;
 }
 

@@ -59,7 +59,7 @@ struct fhe_ctx {
     double2* d_zeta_quad = nullptr; // br_quad.hip zeta layout (context.cpp:quad_zetas)
     double2* d_zeta_wide = nullptr; // [10][256] (context.cpp:wide_zetas)
     double2* d_mono = nullptr;      // monomial table E[4096] of the multi-bit blind rotation (mono_table)
-    int br_kernel = FHE_BR_QX;      // throughput kernel for levels above wide_threshold (classic; multi-bit: quad)
+    int br_kernel = FHE_BR_QY;      // throughput kernel for levels above wide_threshold (classic; multi-bit: quad)
     int8_t* d_ksk_planes = nullptr; // KSK as balanced signed-byte planes (ks_mfma.hip)
     int ks_kernel = FHE_KS_MFMA;
     int8_t* d_ks_digits = nullptr;  // keyswitch digits workspace
@@ -69,7 +69,6 @@ struct fhe_ctx {
     // time -- >128 KB LDS -- so one round over the 256 CUs); the throughput kernel above, which holds
     // 2-3 per CU (profiles/r2/latency_sweep_r2b.txt: from 320 on it is as fast or faster)
     int wide_threshold = 256;
-    int lat_kernel = FHE_LAT_WIDE;  // classic latency levels (<= wide_threshold): br_wide.hip or br_qy.hip's QYL tuning
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;

@@ -63,11 +63,10 @@ hipError_t launch_blind_rotate_qx(const uint64_t* ms, int ms_stride, const PbsDe
                                   const double2* zfull, const double2* mono, uint64_t* out, int count, int n,
                                   hipStream_t s);
 hipError_t launch_bsk_to_qx(const double2* bsk, int npoly, double2* out, hipStream_t s);
-// the same with two workgroup barriers per CMUX (br_qy.hip): same key layout (bsk_qx) and tables;
-// lat = the one-ciphertext-per-CU tuning (tables in registers, key slices a step ahead)
+// the same with two workgroup barriers per CMUX (br_qy.hip): same key layout (bsk_qx) and tables
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                   const uint64_t* luts, const double2* bsk_qx, const double2* tw, const double2* ps,
-                                  const double2* zfull, const double2* mono, uint64_t* out, int count, int n, bool lat,
+                                  const double2* zfull, const double2* mono, uint64_t* out, int count, int n,
                                   hipStream_t s);
 
 // dst[i][0..2049) = src[i * 2049 ..] for i < count (all-gathered level outputs -> block slots)

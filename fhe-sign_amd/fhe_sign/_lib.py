@@ -67,7 +67,6 @@ _SIGNATURES = [
     ("fhe_ctx_last_pbs_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("fhe_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_ctx_set_wide_threshold", C.c_int, [C.c_void_p, C.c_int]),
-    ("fhe_ctx_set_lat_kernel", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_ctx_set_br_kernel", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_ctx_set_ks_kernel", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),

@@ -212,8 +212,7 @@ class Context:
         check(load().fhe_ctx_sync(self._h))
 
     def set_br_kernel(self, kind: int) -> None:
-        """3 = br_qx.hip (classic default), 4 / 5 = br_qy.hip (two barriers per CMUX; 5 = its
-        one-ciphertext-per-CU tuning), 1 = br_quad.hip (always used for multi-bit); 0 and 2, the
+        """4 = br_qy.hip (classic default), 3 = br_qx.hip, 1 = br_quad.hip (always used for multi-bit); 0 and 2, the
         retired 2-wave and pair kernels, are refused (FHE_ERR_INVALID)."""
         check(load().fhe_ctx_set_br_kernel(self._h, int(kind)))
 
@@ -223,11 +222,6 @@ class Context:
 
     def set_wide_threshold(self, threshold: int) -> None:
         check(load().fhe_ctx_set_wide_threshold(self._h, int(threshold)))
-
-    def set_lat_kernel(self, kind: int) -> None:
-        """latency levels (classic): 0 = br_wide.hip (8 waves per ciphertext), 1 = br_qy.hip's
-        one-ciphertext-per-CU tuning; identical results"""
-        check(load().fhe_ctx_set_lat_kernel(self._h, int(kind)))
 
     # ---- multi-GPU fan-out (one process per GPU; SURVEY.md 8e)
     def attach_comm(self, unique_id: bytes, nranks: int, rank: int, timeout_ms: int = 120000) -> None:

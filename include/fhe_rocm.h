@@ -151,17 +151,9 @@ int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
-/* Latency-level blind rotate (batches of at most the threshold, classic parameters): FHE_LAT_WIDE
- * (br_wide.hip, 8 waves per ciphertext) or FHE_LAT_QYL (br_qy.hip tuned for one ciphertext per CU,
- * 4 waves).  Multi-bit latency levels always run br_wide.hip.  Identical bits either way.  The
- * environment variable FHE_LAT_KERNEL sets the initial choice of every new context. */
-#define FHE_LAT_WIDE 0
-#define FHE_LAT_QYL 1
-int fhe_ctx_set_lat_kernel(fhe_ctx* ctx, int kind);
 /* Throughput blind-rotate kernel for levels above the threshold, 4 waves per ciphertext:
- * FHE_BR_QX (default; classic parameters: the round-4 layouts without DPP transposes, br_qx.hip),
- * FHE_BR_QY (classic: the same with two instead of four workgroup barriers per CMUX, br_qy.hip),
- * FHE_BR_QYL (br_qy.hip tuned for one ciphertext per CU: tables in registers, key slices a step ahead) or
+ * FHE_BR_QY (default; classic parameters: the round-4 layouts without DPP transposes and with two
+ * workgroup barriers per CMUX, br_qy.hip), FHE_BR_QX (the same layouts with four barriers, br_qx.hip) or
  * FHE_BR_QUAD (br_quad.hip; always used for the multi-bit blind rotation).  The retired kernels --
  * FHE_BR_NARROW (2 waves per ciphertext, round 1) and FHE_BR_PAIR (two ciphertexts per 4-wave
  * workgroup, rounds 2-3) -- are refused with FHE_ERR_INVALID.  All blind-rotate kernels produce
@@ -171,7 +163,6 @@ int fhe_ctx_set_lat_kernel(fhe_ctx* ctx, int kind);
 #define FHE_BR_PAIR 2
 #define FHE_BR_QX 3
 #define FHE_BR_QY 4
-#define FHE_BR_QYL 5
 int fhe_ctx_set_br_kernel(fhe_ctx* ctx, int kind);
 
 /* Keyswitch: int8 matrix-core contraction against the KSK's byte planes (FHE_KS_MFMA, default) or

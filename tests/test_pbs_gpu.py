@@ -135,32 +135,6 @@ def test_wide_and_quad_kernels_bit_identical(env):
     assert np.array_equal(wide[:6], ref)
 
 
-def test_latency_kernel_choice_bit_identical(env):
-    """Latency levels (batch <= the threshold) through either latency kernel -- br_wide.hip or
-    br_qy.hip's one-ciphertext-per-CU tuning (FHE_LAT_QYL; multi-bit levels stay on br_wide.hip) --
-    give identical words at B = 1, 37, 256, equal to the oracle; an unknown kind is refused."""
-    _, _, ok, ctx = env
-    tables = _luts()
-    ids = [ctx.lut(t) for t in tables]
-    r = ok.rng(4242)
-    cts = np.stack([ok.encrypt(r, (5 * i + 3) % 16) for i in range(256)])
-    lut_ids = np.array([ids[i % len(ids)] for i in range(256)], np.uint32)
-    with pytest.raises(Exception):
-        ctx.set_lat_kernel(2)
-    got = {}
-    try:
-        for kind in (0, 1):
-            ctx.set_lat_kernel(kind)
-            got[kind] = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 37, 256)}
-    finally:
-        ctx.set_lat_kernel(0)
-    for c in (1, 37, 256):
-        bad = np.flatnonzero((got[0][c] != got[1][c]).any(axis=1))
-        assert bad.size == 0, f"batch {c}: ciphertexts {bad[:5]} differ between the latency kernels"
-    ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
-    assert np.array_equal(got[1][37][:6], ref)
-
-
 def test_zero_and_sparse_masks_both_kernels(env):
     """Ciphertexts whose modulus-switched mask is 0 at every key bit (trivial encryptions: mask 0,
     body m delta -- every CMUX is an a = 0 step, the kernels run it with e - 1 = 0 while the oracle
@@ -192,7 +166,7 @@ def test_zero_and_sparse_masks_both_kernels(env):
         assert ok.decrypt(ref[m]) == tables[lut_of[m]][m]
 
 
-@pytest.mark.parametrize("kind", [3, 4, 5, 1])  # FHE_BR_QX (br_qx.hip), FHE_BR_QY / QYL (br_qy.hip), FHE_BR_QUAD
+@pytest.mark.parametrize("kind", [3, 4, 1])  # FHE_BR_QX (br_qx.hip), FHE_BR_QY (br_qy.hip), FHE_BR_QUAD (br_quad.hip)
 def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
     """The throughput kernels at ragged batches (1, 2, 3, 37, 259) with every LUT give the latency
     kernel's and the oracle's words (multi-bit parameters always run br_quad.hip); the retired
@@ -211,20 +185,20 @@ def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
         thr = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 2, 3, 37, 259)}
     finally:
         ctx.set_wide_threshold(256)
-        ctx.set_br_kernel(3)
+        ctx.set_br_kernel(4)
     for c, out in thr.items():
         bad = [i for i in range(c) if not np.array_equal(out[i], wide[i])]
         assert not bad, f"kernel {kind}, batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(thr[37][:6], ref)
-    for bad_kind in (0, 2, 6):
+    for bad_kind in (0, 2, 5):
         with pytest.raises(Exception):
             ctx.set_br_kernel(bad_kind)
 
 
 def test_throughput_kernels_identical_at_full_batch(env):
-    """br_qx.hip, br_qy.hip (both tunings) and br_quad.hip on the same 4096 distinct encryptions (16
-    rounds of 256 CUs): every output word identical, a seeded sample of 8 equal to the oracle."""
+    """br_qx.hip, br_qy.hip and br_quad.hip on the same 4096 distinct encryptions (16 rounds of 256
+    CUs): every output word identical, a seeded sample of 8 equal to the oracle."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = np.array([ctx.lut(t) for t in tables], np.uint32)
@@ -239,11 +213,9 @@ def test_throughput_kernels_identical_at_full_batch(env):
         qx = ctx.pbs(cts, ids[lut_of])
         ctx.set_br_kernel(4)
         qy = ctx.pbs(cts, ids[lut_of])
-        ctx.set_br_kernel(5)
-        qyl = ctx.pbs(cts, ids[lut_of])
     finally:
-        ctx.set_br_kernel(3)
-    for name, other in (("quad", quad), ("qy", qy), ("qyl", qyl)):
+        ctx.set_br_kernel(4)
+    for name, other in (("quad", quad), ("qy", qy)):
         bad = np.flatnonzero((other != qx).any(axis=1))
         assert bad.size == 0, f"{bad.size} ciphertexts differ between qx and {name}, first {bad[:5]}"
     pick = np.array([0, 1, 513, 1024, 2047, 2048, 3333, 4095])

@@ -1,5 +1,5 @@
 """Latency-level blind rotate by kernel: the 8-wave latency kernel (wide) against the 4-wave throughput
-kernels (quad, qx, qy, and qy's one-ciphertext-per-CU tuning qyl) forced onto small batches (wide threshold 0), at B = 1 .. 512 distinct
+kernels (quad, qx, qy) forced onto small batches (wide threshold 0), at B = 1 .. 512 distinct
 encryptions, best of R launches each, every output checked by decryption.
 usage: python3 tools/lat_kinds.py [--pkg DIR] [--kinds a,b] [R] [B ...]   (DIR: a tools/build_variant.sh build)"""
 import os
@@ -23,7 +23,7 @@ from fhe_sign import Context, generate_keys  # noqa: E402
 assert os.path.dirname(fhe_sign.__file__).startswith(PKG), fhe_sign.__file__
 R = int(argv[0]) if argv else 5
 sizes = [int(b) for b in argv[1:]] or [1, 64, 256, 512]
-KINDS = [k for k in (("wide", None), ("quad", 1), ("qx", 3), ("qy", 4), ("qyl", 5)) if SEL is None or k[0] in SEL]
+KINDS = [k for k in (("wide", None), ("quad", 1), ("qx", 3), ("qy", 4)) if SEL is None or k[0] in SEL]
 ck, sk = generate_keys(seed=1)
 ctx = Context(0)
 ctx.set_server_key(sk)

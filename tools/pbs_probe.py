@@ -14,7 +14,7 @@ ck, sk = generate_keys(fhe_sign.multi_bit_params() if MB else None, seed=1)
 print(f"keygen {time.time()-t0:.2f}s", flush=True)
 ctx = Context(0)
 t0 = time.time(); ctx.set_server_key(sk); print(f"set_server_key {time.time()-t0:.2f}s", flush=True)
-if os.environ.get("FHE_PROBE_BR"):  # throughput kernel: 3 = br_qx (classic default), 1 = br_quad
+if os.environ.get("FHE_PROBE_BR"):  # throughput kernel: 4 = br_qy (classic default), 3 = br_qx, 1 = br_quad
     ctx.set_br_kernel(int(os.environ["FHE_PROBE_BR"]))
 lid = ctx.lut([(m + 1) % 16 for m in range(16)])
 cts = np.stack([ck.encrypt_block(m % 16) for m in range(64)])
