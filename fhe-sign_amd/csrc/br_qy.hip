@@ -167,14 +167,6 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
     auto lane_factor = [&](uint32_t a) { return bptr{mono_rs, ((c4 * a) & 4095u) * 16u, 0u}[0]; };
     cplx Fn = pair_factor(a_next), Ebn = lane_factor(a_next);
     __syncthreads();
-#ifdef QY_STAGGER
-    // (variant build only) the first round of workgroups starts in lockstep, three per CU: offset the
-    // second and third by a third and two thirds of a CMUX so their barriers and LDS phases interleave
-    if (blockIdx.x < 768u && blockIdx.x >= 256u) {
-        __builtin_amdgcn_s_sleep(QY_STAGGER);
-        if (blockIdx.x >= 512u) __builtin_amdgcn_s_sleep(QY_STAGGER);
-    }
-#endif
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
     const cplx* Zu = Z;  // uniform zetas of stages 0-2: Z[1], Z[2], Z[4], Z[6]
     uint32_t upd = 0;
