@@ -75,6 +75,11 @@ constexpr int XZ_SZ = 140;
 // [20 + 34 c + 17 h + k] = W[16 m5] (c = 0), W[8 m5] (c = 1), m5 = (b4 .. b0) = 2 k + h (phase B)
 constexpr int XT_SZ = 20 + 68;
 
+// key-slice points issued before the B' -> E barrier (the rest after it); variant builds only
+#ifndef QY_KSPLIT
+#define QY_KSPLIT 2
+#endif
+
 template <int K, class F>
 FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
 #pragma unroll
@@ -246,7 +251,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         cplx Kb[16];  // [4 (row, column) + point k]; points 0, 1 now, 2, 3 after the barrier
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-            if ((q & 3) < 2) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+            if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
         const cplx e0 = cmul(Ebn, Fn);  // exact when kk = 0 (Fn = E[0] = 1)
         Fn = pair_factor(a_next);
         Ebn = lane_factor(a_next);
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         for (int r = 0; r < 8; ++r) x[r] = s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-            if ((q & 3) >= 2) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+            if ((q & 3) >= QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
 #pragma unroll
         for (int r = 0; r < 8; ++r)
             if (!(r & 2)) dit_bfly(x[r], x[r + 2], z8);
