@@ -79,6 +79,9 @@ constexpr int XT_SZ = 20 + 68;
 #ifndef QY_KSPLIT
 #define QY_KSPLIT 2
 #endif
+#ifndef QY_KEARLY  // where those are issued: 0 after the B' stores, 1 at the top of the step, 2 before B'
+#define QY_KEARLY 0
+#endif
 
 template <int K, class F>
 FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
@@ -184,6 +187,12 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         const bptr P{ps_rs, 16u * (uint32_t)u, 0u};
         const bptr kb{bsk_rs, 16u * (uint32_t)L, (uint32_t)(i * 4096 + w * 256) * 16u};
 
+#if QY_KEARLY == 1
+        cplx Kb[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+#endif
         // digits of acc itself (factored CMUX), with the previous update's deferred reduction
         cplx x[8];
         if (red_in) {
@@ -231,6 +240,12 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         wave_sync();
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bBp + xq(idx_Bp(0, 0, r))];
+#if QY_KEARLY == 2
+        cplx Kb[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+#endif
         // ---- phase B': stages 5 (b4, register bit 2), 6 (b3, bit 1), 7 (b2, bit 0)
         {
             const cplx z5 = s_z[12 + U], z6 = s_z[44 + U], z7a = s_z[76 + U], z7b = s_z[108 + U];
@@ -247,11 +262,13 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         }
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bBp + xq(idx_Bp(0, 0, r))] = x[r];
+#if QY_KEARLY == 0
         // key slices of this step in the E layout (row, column, point k): in flight across the barrier
         cplx Kb[16];  // [4 (row, column) + point k]; points 0, 1 now, 2, 3 after the barrier
 #pragma unroll
         for (int q = 0; q < 16; ++q)
             if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+#endif
         const cplx e0 = cmul(Ebn, Fn);  // exact when kk = 0 (Fn = E[0] = 1)
         Fn = pair_factor(a_next);
         Ebn = lane_factor(a_next);
