@@ -79,8 +79,11 @@ constexpr int XT_SZ = 20 + 68;
 #ifndef QY_KSPLIT
 #define QY_KSPLIT 2
 #endif
-#ifndef QY_KEARLY  // where those are issued: 0 after the B' stores, 1 at the top of the step, 2 before B'
-#define QY_KEARLY 0
+// where those are issued: 1 (default) at the top of the step, in flight across the whole forward
+// transform (same-box A/B 213.6-214.1 vs 216.3-217.1 ms per 32768, profiles/r4/sched_ab_r4r.txt);
+// 0 after the B' stores, 2 before the B' stages (the scheduler's own choice for 0 under max-memory-clause)
+#ifndef QY_KEARLY
+#define QY_KEARLY 1
 #endif
 
 template <int K, class F>
