@@ -85,6 +85,10 @@ constexpr int XT_SZ = 20 + 68;
 #ifndef QY_KEARLY
 #define QY_KEARLY 1
 #endif
+// untwist-factor loads: 0 (default) after the B' -> B round trip, 1 after the second barrier, 2 after the MAC
+#ifndef QY_PEARLY
+#define QY_PEARLY 0
+#endif
 
 template <int K, class F>
 FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
@@ -298,6 +302,11 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
             x[k] = cmul(o0, wv);
             x[4 + k] = cmul(o1, wv);
         }
+#if QY_PEARLY == 2
+        cplx pst[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
+#endif
         // ---- inverse: b0 (twiddle 1), b1 (twiddles 1, -i) in E
 #pragma unroll
         for (int r = 0; r < 8; r += 2) {
@@ -314,6 +323,11 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
 #pragma unroll
         for (int r = 0; r < 8; ++r) s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))] = x[r];
         __syncthreads();
+#if QY_PEARLY == 1
+        cplx pst[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
+#endif
         // ---- B' (inverse): b2 (register bit 0), b3 (bit 1), b4 (bit 2)
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bBp + xq(idx_Bp(0, 0, r))];
@@ -335,9 +349,11 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         wave_sync();
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bB + xq(idx_B(0, 0, r))];
+#if QY_PEARLY == 0
         cplx pst[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
+#endif
         {
             const cplx w5 = s_t[20 + 17 * h + kB], w6 = s_t[54 + 17 * h + kB];
             dit_pairs<1>(x, [&](int) { return conj_(w5); });
