@@ -85,9 +85,11 @@ constexpr int XT_SZ = 20 + 68;
 #ifndef QY_KEARLY
 #define QY_KEARLY 1
 #endif
-// untwist-factor loads: 0 (default) after the B' -> B round trip, 1 after the second barrier, 2 after the MAC
+// untwist-factor loads: 1 (default) right after the second barrier, with the post-RA scheduler off
+// (Makefile; same-box 222.6-222.9 vs 224.2-224.9 ms, profiles/r4/sched_ab_r4s.txt -- either change
+// alone is slower); 0 after the B' -> B round trip, 2 after the MAC (spills)
 #ifndef QY_PEARLY
-#define QY_PEARLY 0
+#define QY_PEARLY 1
 #endif
 
 template <int K, class F>
