@@ -28,6 +28,9 @@
 // WMB7 (timing-only variant builds, tools/g3_probe.sh): the G = 2 kernel with a grouping-3 step's
 // shape -- n/3 steps, 7 key patterns per step loaded and bundled -- on the grouping-2 key's slices
 // (wrong numbers; for the grouping-3 cost estimate of DESIGN.md 3a only)
+#ifndef WIDE_KPRE
+#define WIDE_KPRE 0
+#endif
 #ifdef WMB7
 constexpr int WMBP = 7, WMBDIV = 3;
 #else
@@ -298,11 +301,27 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#if WIDE_KPRE
+    // (variant build) classic: the key slices of step i + 1 are loaded right after step i's MAC
+    cplx Kown[4], Koth[4];
+    if constexpr (G == 1) {
+        const bptr kb{bsk_rs, kvo, 0u};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            Kown[2 * k] = kb[0 * 1024 + 128 * k];
+            Koth[2 * k] = kb[2 * 1024 + 128 * k];
+            Kown[2 * k + 1] = kb[3 * 1024 + 128 * k];
+            Koth[2 * k + 1] = kb[1 * 1024 + 128 * k];
+        }
+    }
+#endif
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
     bool red_in = false;  // the previous update's reduction, deferred to this step's digits (red_digit_s)
     for (int i = 0; i < n / (G == 1 ? 1 : WMBDIV); ++i) {  // n / G in the product build
         cplx x[4];
+#if !WIDE_KPRE
         cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
+#endif
         uint32_t mB[3] = {0u, 0u, 0u};
         const bool reduce = (upd++ & 1u) != 0;
         cplx e1;  // G = 1: zeta^((4 j0 + 1) a) of this lane's point r = 0
@@ -340,7 +359,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         // BSK slice for this iteration (issued early; consumed after the forward FFT): for MAC pair
         // k (points 2k, 2k + 1; this lane's point 2k + hL) the rows 0, 1 of column 0 (Kown[2k],
         // Koth[2k]) and of column 1 (Kown[2k + 1], Koth[2k + 1])
-        {
+        if (!WIDE_KPRE) {
             const bptr kb{bsk_rs, kvo, (uint32_t)i * 65536u};
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -450,6 +469,18 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 x[2 * k] = o0;
                 x[2 * k + 1] = o1;
             }
+#if WIDE_KPRE
+            if (i + 1 < n) {  // the next step's key slices, in flight across the inverse and the forward
+                const bptr kb{bsk_rs, kvo, (uint32_t)(i + 1) * 65536u};
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    Kown[2 * k] = kb[0 * 1024 + 128 * k];
+                    Koth[2 * k] = kb[2 * 1024 + 128 * k];
+                    Kown[2 * k + 1] = kb[3 * 1024 + 128 * k];
+                    Koth[2 * k + 1] = kb[1 * 1024 + 128 * k];
+                }
+            }
+#endif
         } else {
             cplx y[4];
             const cplx* cross_other = s_cross[p ^ 1];
