@@ -85,11 +85,12 @@ constexpr int XT_SZ = 20 + 68;
 #ifndef QY_KEARLY
 #define QY_KEARLY 1
 #endif
-// untwist-factor loads: 1 (default) right after the second barrier, with the post-RA scheduler off
-// (Makefile; same-box 222.6-222.9 vs 224.2-224.9 ms, profiles/r4/sched_ab_r4s.txt -- either change
-// alone is slower); 0 after the B' -> B round trip, 2 after the MAC (spills)
+// untwist-factor loads: 0 (default) after the B' -> B round trip; 1 right after the second barrier,
+// 2 after the MAC (spills).  1 with the post-RA scheduler off won one same-box A/B (-0.8 %,
+// profiles/r4/sched_ab_r4s.txt) and lost another by 3 % with the L2 hit rate falling 0.976 -> 0.758
+// (10x the L2 fills, profiles/r4/l2ab_r4u/): workgroups drift apart in the key stream; not adopted
 #ifndef QY_PEARLY
-#define QY_PEARLY 1
+#define QY_PEARLY 0
 #endif
 
 template <int K, class F>
