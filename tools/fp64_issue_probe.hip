@@ -56,6 +56,29 @@ __global__ void k_fma_dpp(unsigned long long* cyc, double* out, double a, double
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+template <int C>
+__global__ void k_add32(unsigned long long* cyc, double* out, double a, double b, int iters) {
+    // C independent 32-bit integer chains (v_add_u32 / v_xor), the transposes' and index math's class
+    uint32_t x[C];
+    const uint32_t ia = (uint32_t)(a * 1000.0), ib = (uint32_t)(b * 1e9);
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = threadIdx.x + c;
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 32 / C; ++k)
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = (x[c] + ia) ^ ib;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) s += x[c];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <class K>
 double run(K kern, int waves_per_simd, int iters, const char* name, int ops_per_iter) {
     const int blocks = 256, threads = 256 * waves_per_simd;
@@ -90,6 +113,7 @@ int main() {
         run(k_fma<4>, w, 512, "fma_f64 4 chains", 32);
         run(k_fma<8>, w, 512, "fma_f64 8 chains", 32);
         run(k_fma_dpp<8>, w, 512, "fma_f64 8 chains + 16 dpp", 32);
+        run(k_add32<8>, w, 512, "add+xor u32 8 chains", 64);
     }
     return 0;
 }
