@@ -15,6 +15,11 @@ for i in $(seq 1 $R); do
     for B in 1 256; do
       for V in base $(cd build_variants && ls -d w_* 2>/dev/null); do run $V $B; done
     done
+    if [ -n "${SAB_MB_LAT:-}" ]; then  # the multi-bit latency kernel too
+      for B in 1 256; do
+        for V in base $(cd build_variants && ls -d w_* 2>/dev/null); do runmb $V $B; done
+      done
+    fi
   fi
   if ls -d build_variants/mb_* > /dev/null 2>&1; then
     for V in base $(cd build_variants && ls -d mb_* 2>/dev/null); do runmb $V 32768; done
