@@ -85,11 +85,6 @@ constexpr int XT_SZ = 20 + 68;
 #ifndef QY_KEARLY
 #define QY_KEARLY 1
 #endif
-// wave priority variants (0 = default): 1 raised between the two barriers, 2 raised on the stretches
-// leading into each barrier
-#ifndef QY_PRIO
-#define QY_PRIO 0
-#endif
 // untwist-factor loads: 0 (default) after the B' -> B round trip; 1 right after the second barrier,
 // 2 after the MAC (spills).  1 with the post-RA scheduler off won one same-box A/B (-0.8 %,
 // profiles/r4/sched_ab_r4s.txt) and lost another by 3 % with the L2 hit rate falling 0.976 -> 0.758
@@ -261,7 +256,6 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         for (int q = 0; q < 16; ++q)
             if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
 #endif
-        if (QY_PRIO == 2) __builtin_amdgcn_s_setprio(1);  // the stretch into the B' -> E barrier
         // ---- phase B': stages 5 (b4, register bit 2), 6 (b3, bit 1), 7 (b2, bit 0)
         {
             const cplx z5 = s_z[12 + U], z6 = s_z[44 + U], z7a = s_z[76 + U], z7b = s_z[108 + U];
@@ -289,8 +283,6 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         Fn = pair_factor(a_next);
         Ebn = lane_factor(a_next);
         __syncthreads();
-        if (QY_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-        if (QY_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         // ---- phase E: both polynomials at this wave's points, stages 8 (b1), 9 (b0)
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
@@ -331,11 +323,9 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
             dit_bfly_unit(x[r], x[r + 2], (r & 1) ? mul_negi(x[r + 2]) : x[r + 2]);
         }
         // (no barrier before these stores: E reads and writes only this wave's own points)
-        if (QY_PRIO == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int r = 0; r < 8; ++r) s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))] = x[r];
         __syncthreads();
-        if (QY_PRIO) __builtin_amdgcn_s_setprio(0);
 #if QY_PEARLY == 1
         cplx pst[8];
 #pragma unroll
