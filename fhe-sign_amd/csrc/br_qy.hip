@@ -103,7 +103,14 @@ FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __restrict__ ms, int ms_stride,
+// G = blind-rotation grouping (as br_wide.hip / br_quad.hip).  G = 2 (multi-bit, oracle
+// fho_blind_rotate grouping 2): per pair of key bits the digits of acc itself and, per Fourier point of
+// phase E, the key bundle K_rc = sum_B (e_B - 1) G_B,rc (B = 1..3, patterns in order, from +0) -- it
+// depends on the key and the group's monomials only, so it is built during the forward transform, one
+// pattern's 16 key slices at a time -- then the MAC with no (e - 1) factor after it; the last forward
+// stage as t = zeta c, (a + t, a - t).  Two workgroups per CU.
+template <int G>
+__global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const uint64_t* __restrict__ ms, int ms_stride,
                                                             const PbsDesc* __restrict__ desc,
                                                             const uint32_t* __restrict__ lut_idx,
                                                             const uint64_t* __restrict__ luts,
@@ -184,24 +191,46 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
     auto pair_factor = [&](uint32_t a) { return bptr{mono_rs, 0u, 16u * ((256u * kk * a) & 4095u)}[0]; };
     auto lane_factor = [&](uint32_t a) { return bptr{mono_rs, ((c4 * a) & 4095u) * 16u, 0u}[0]; };
     cplx Fn = pair_factor(a_next), Ebn = lane_factor(a_next);
+    cplx FnB[3], EbnB[3];  // G = 2: the group's pair and lane factors per pattern, loaded a group ahead
+    if constexpr (G == 2) {
+        const uint32_t m0[3] = {a_next, a_next1, (a_next + a_next1) & 4095u};
+#pragma unroll
+        for (int B = 0; B < 3; ++B) {
+            FnB[B] = pair_factor(m0[B]);
+            EbnB[B] = lane_factor(m0[B]);
+        }
+    }
     __syncthreads();
     const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps);
     const cplx* Zu = Z;  // uniform zetas of stages 0-2: Z[1], Z[2], Z[4], Z[6]
     uint32_t upd = 0;
     bool red_in = false;
-    for (int i = 0; i < n; ++i) {
-        const uint32_t a = a_next;
-        a_next = a_next1;
-        a_next1 = modswitch_2n(a_ct[i + 2 <= n ? i + 2 : n]);
+    for (int i = 0; i < n / G; ++i) {
+        uint32_t a = 0, mB[3] = {0u, 0u, 0u};
+        if constexpr (G == 1) {
+            a = a_next;
+            a_next = a_next1;
+            a_next1 = modswitch_2n(a_ct[i + 2 <= n ? i + 2 : n]);
+        } else {
+            mB[0] = a_next;
+            mB[1] = a_next1;
+            mB[2] = (a_next + a_next1) & 4095u;
+            if (2 * i + 2 < n) {
+                a_next = modswitch_2n(a_ct[2 * i + 2]);
+                a_next1 = modswitch_2n(a_ct[2 * i + 3]);
+            }
+        }
         const bool reduce = (upd++ & 1u) != 0;
         const bptr P{ps_rs, 16u * (uint32_t)u, 0u};
         const bptr kb{bsk_rs, 16u * (uint32_t)L, (uint32_t)(i * 4096 + w * 256) * 16u};
 
+        cplx Kb[16];  // G = 1: key slices [4 (row, column) + point k]; G = 2: the key bundle, same order
 #if QY_KEARLY == 1
-        cplx Kb[16];
+        if constexpr (G == 1) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+            for (int q = 0; q < 16; ++q)
+                if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        }
 #endif
         // digits of acc itself (factored CMUX), with the previous update's deferred reduction
         cplx x[8];
@@ -215,6 +244,34 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
             for (int r = 0; r < 8; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 8]));
         }
 
+        if constexpr (G == 2) {
+            // key bundle of this group per point of phase E (oracle cmul_acc, patterns in order), and
+            // the next group's monomial factors
+            cplx eB[3];
+#pragma unroll
+            for (int B = 0; B < 3; ++B) eB[B] = cmul(EbnB[B], FnB[B]);  // exact when kk = 0
+            if (2 * i + 2 < n) {
+                const uint32_t mn[3] = {a_next, a_next1, (a_next + a_next1) & 4095u};
+#pragma unroll
+                for (int B = 0; B < 3; ++B) {
+                    FnB[B] = pair_factor(mn[B]);
+                    EbnB[B] = lane_factor(mn[B]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) Kb[q] = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int B = 0; B < 3; ++B) {
+                const bptr kg{bsk_rs, 16u * (uint32_t)L, (uint32_t)((3 * i + B) * 4096 + w * 256) * 16u};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t tr = (uint32_t)((k >> 1) + 2 * (k & 1)) * mB[B];  // (j8 + 2 j9) m_B
+                    const cplx wv = k == 0 ? make_double2(eB[B].x - 1.0, eB[B].y) : turn_sel_m1(eB[B], tr);
+#pragma unroll
+                    for (int rc = 0; rc < 4; ++rc) Kb[rc * 4 + k] = cmul_acc(Kb[rc * 4 + k], kg[rc * 1024 + k * 64], wv);
+                }
+            }
+        }
         // ---- phase A: stages 0-2 (uniform zetas)
 #pragma unroll
         for (int r = 0; r < 4; ++r) dit_bfly(x[r], x[r + 4], Zu[1]);
@@ -251,10 +308,11 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bBp + xq(idx_Bp(0, 0, r))];
 #if QY_KEARLY == 2
-        cplx Kb[16];
+        if constexpr (G == 1) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+            for (int q = 0; q < 16; ++q)
+                if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        }
 #endif
         // ---- phase B': stages 5 (b4, register bit 2), 6 (b3, bit 1), 7 (b2, bit 0)
         {
@@ -274,36 +332,56 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
         for (int r = 0; r < 8; ++r) reg[bBp + xq(idx_Bp(0, 0, r))] = x[r];
 #if QY_KEARLY == 0
         // key slices of this step in the E layout (row, column, point k): in flight across the barrier
-        cplx Kb[16];  // [4 (row, column) + point k]; points 0, 1 now, 2, 3 after the barrier
+        if constexpr (G == 1) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+            for (int q = 0; q < 16; ++q)
+                if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        }
 #endif
-        const cplx e0 = cmul(Ebn, Fn);  // exact when kk = 0 (Fn = E[0] = 1)
-        Fn = pair_factor(a_next);
-        Ebn = lane_factor(a_next);
+        cplx e0 = make_double2(1.0, 0.0);
+        if constexpr (G == 1) {
+            e0 = cmul(Ebn, Fn);  // exact when kk = 0 (Fn = E[0] = 1)
+            Fn = pair_factor(a_next);
+            Ebn = lane_factor(a_next);
+        }
         __syncthreads();
         // ---- phase E: both polynomials at this wave's points, stages 8 (b1), 9 (b0)
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
+        if constexpr (G == 1) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if ((q & 3) >= QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+            for (int q = 0; q < 16; ++q)
+                if ((q & 3) >= QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        }
 #pragma unroll
         for (int r = 0; r < 8; ++r)
             if (!(r & 2)) dit_bfly(x[r], x[r + 2], z8);
+        if constexpr (G == 1) {
 #pragma unroll
-        for (int r = 0; r < 8; r += 2) dit_bfly(x[r], x[r + 1], (r & 2) ? mul_i(z9) : z9);
+            for (int r = 0; r < 8; r += 2) dit_bfly(x[r], x[r + 1], (r & 2) ? mul_i(z9) : z9);
+        } else {  // multi-bit: t = zeta c, (a + t, a - t) (oracle forward_twisted)
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) {
+                const cplx t = cmul(x[r + 1], (r & 2) ? mul_i(z9) : z9), a0 = x[r];
+                x[r] = cadd(a0, t);
+                x[r + 1] = csub(a0, t);
+            }
+        }
         // MAC (own digit first, oracle mac_own_first) and (X^a - 1) per point, shared by both outputs
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const cplx d0 = x[k], d1 = x[4 + k];
             const cplx o0 = mac2(d0, Kb[0 * 4 + k], d1, Kb[2 * 4 + k]);  // D0 B00 + D1 B10
             const cplx o1 = mac2(d1, Kb[3 * 4 + k], d0, Kb[1 * 4 + k]);  // D1 B11 + D0 B01
-            const uint32_t tr = (uint32_t)((k >> 1) + 2 * (k & 1)) * a;   // (j8 + 2 j9) a
-            const cplx wv = k == 0 ? make_double2(e0.x - 1.0, e0.y) : turn_sel_m1(e0, tr);
-            x[k] = cmul(o0, wv);
-            x[4 + k] = cmul(o1, wv);
+            if constexpr (G == 1) {
+                const uint32_t tr = (uint32_t)((k >> 1) + 2 * (k & 1)) * a;  // (j8 + 2 j9) a
+                const cplx wv = k == 0 ? make_double2(e0.x - 1.0, e0.y) : turn_sel_m1(e0, tr);
+                x[k] = cmul(o0, wv);
+                x[4 + k] = cmul(o1, wv);
+            } else {  // the (e - 1) factors are in the bundle
+                x[k] = o0;
+                x[4 + k] = o1;
+            }
         }
 #if QY_PEARLY == 2
         cplx pst[8];
@@ -409,10 +487,15 @@ __global__ __launch_bounds__(256, 3) void k_blind_rotate_qy(const uint64_t* __re
 
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                   const uint64_t* luts, const cplx* bsk_qx, const cplx* tw, const cplx* ps,
-                                  const cplx* zfull, const cplx* mono, uint64_t* out, int count, int n, hipStream_t s) {
+                                  const cplx* zfull, const cplx* mono, int grouping, uint64_t* out, int count, int n,
+                                  hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blind_rotate_qy, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts, bsk_qx,
-                       tw, ps, zfull, mono, out, n);
+    if (grouping == 2)
+        hipLaunchKernelGGL(k_blind_rotate_qy<2>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
+                           bsk_qx, tw, ps, zfull, mono, out, n);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_qy<1>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
+                           bsk_qx, tw, ps, zfull, mono, out, n);
     return hipGetLastError();
 }
 

@@ -279,9 +279,9 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     if ((int)count <= wide_threshold)
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
-    if (p.grouping == 1 && br_kernel == FHE_BR_QY && d_bsk_qx)
+    if ((p.grouping == 1 || mb_qy) && br_kernel == FHE_BR_QY && d_bsk_qx)
         return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
-                                      d_zeta_full, d_mono, out, (int)count, (int)p.n, stream);
+                                      d_zeta_full, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
     if (p.grouping == 1 && br_kernel == FHE_BR_QX && d_bsk_qx)
         return launch_blind_rotate_qx(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
                                       d_zeta_full, d_mono, out, (int)count, (int)p.n, stream);
@@ -548,6 +548,7 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
     FHE_HIP_CHECK(hipMemcpy(c->d_tw_wide, tww.data(), tww.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMemcpy(c->d_psi_wide, psiw.data(), psiw.size() * sizeof(double2), hipMemcpyHostToDevice));
     if (const char* e = getenv("FHE_WIDE_THRESHOLD")) c->wide_threshold = atoi(e);
+    if (const char* e = getenv("FHE_MB_QY")) c->mb_qy = atoi(e) != 0;  // multi-bit throughput levels on br_qy.hip
     std::vector<double2> mono;
     mono_table(psi, &mono);
     FHE_HIP_CHECK(hipMalloc(&c->d_mono, mono.size() * sizeof(double2)));
@@ -609,7 +610,7 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     FHE_HIP_CHECK(launch_bsk_to_fourier(d_std, npoly, c->d_W, c->d_psi, c->d_bsk, c->stream));
     FHE_HIP_CHECK(hipMalloc(&c->d_bsk_quad, (size_t)npoly * 1024 * sizeof(double2)));
     FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, c->d_bsk_quad, c->stream));
-    if (p.grouping == 1) {  // the classic throughput kernel's layout (br_qx.hip)
+    if (p.grouping == 1 || c->mb_qy) {  // the qx/qy kernels' layout (br_qx.hip)
         FHE_HIP_CHECK(hipMalloc(&c->d_bsk_qx, (size_t)npoly * 1024 * sizeof(double2)));
         FHE_HIP_CHECK(launch_bsk_to_qx(c->d_bsk, npoly, c->d_bsk_qx, c->stream));
     }

@@ -63,11 +63,12 @@ hipError_t launch_blind_rotate_qx(const uint64_t* ms, int ms_stride, const PbsDe
                                   const double2* zfull, const double2* mono, uint64_t* out, int count, int n,
                                   hipStream_t s);
 hipError_t launch_bsk_to_qx(const double2* bsk, int npoly, double2* out, hipStream_t s);
-// the same with two workgroup barriers per CMUX (br_qy.hip): same key layout (bsk_qx) and tables
+// the same with two workgroup barriers per CMUX (br_qy.hip): same key layout (bsk_qx) and tables;
+// grouping 2 = the multi-bit blind rotation on the multi-bit key in the same E layout
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                   const uint64_t* luts, const double2* bsk_qx, const double2* tw, const double2* ps,
-                                  const double2* zfull, const double2* mono, uint64_t* out, int count, int n,
-                                  hipStream_t s);
+                                  const double2* zfull, const double2* mono, int grouping, uint64_t* out, int count,
+                                  int n, hipStream_t s);
 
 // dst[i][0..2049) = src[i * 2049 ..] for i < count (all-gathered level outputs -> block slots)
 hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s);

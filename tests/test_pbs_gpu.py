@@ -282,3 +282,46 @@ def test_noise_budget_at_radix_limit(env):
     carry = ctx.lut([1 if v >= 8 else 0 for v in range(16)])
     out = ctx.pbs(comb, carry)
     assert [ok.decrypt(o) for o in out] == [int(v >= 8) for v in m]
+
+
+def test_multibit_qy_kernel_bit_identical():
+    """br_qy.hip's multi-bit instance (FHE_MB_QY=1: the key bundle per point of phase E, built during
+    the forward transform) gives the multi-bit latency kernel's and the oracle's words, at ragged
+    batches and at 4096 distinct encryptions (16 rounds of 256 CUs)."""
+    import os
+    mb = multi_bit_params()
+    ck, sk = generate_keys(mb, seed=SEED)
+    ok = oracle.OracleKeys(SEED, oracle.multibit_params())
+    tables = _luts()
+    r = ok.rng(2024)
+    B = 4096
+    cts = np.stack([ok.encrypt(r, (7 * i + 2) % 16) for i in range(B)])
+    lut_of = np.arange(B) % len(tables)
+    os.environ["FHE_MB_QY"] = "1"
+    try:
+        ctx = Context(0)
+    finally:
+        del os.environ["FHE_MB_QY"]
+    try:
+        ctx.set_server_key(sk)
+        ids = np.array([ctx.lut(t) for t in tables], np.uint32)
+        ctx.set_wide_threshold(1 << 30)
+        wide = ctx.pbs(cts[:259], ids[lut_of[:259]])
+        ctx.set_wide_threshold(0)
+        ctx.set_br_kernel(4)
+        got = {c: ctx.pbs(cts[:c], ids[lut_of[:c]]) for c in (1, 37, 259)}
+        full = ctx.pbs(cts, ids[lut_of])
+        ctx.set_br_kernel(1)
+        quad = ctx.pbs(cts, ids[lut_of])
+    finally:
+        ctx.close()
+    for c, out in got.items():
+        bad = np.flatnonzero((out != wide[:c]).any(axis=1))
+        assert bad.size == 0, f"batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
+    bad = np.flatnonzero((full != quad).any(axis=1))
+    assert bad.size == 0, f"{bad.size} ciphertexts differ between qy<2> and quad<2>, first {bad[:5]}"
+    pick = np.array([0, 1, 777, 2048, 4095])
+    ref = ok.pbs_batch(np.ascontiguousarray(cts[pick]), np.stack([ok.make_lut(t) for t in tables]),
+                       lut_of[pick].astype(np.uint32))
+    for k, i in enumerate(pick):
+        assert np.array_equal(full[i], ref[k]), f"ciphertext {i} differs from the oracle"
