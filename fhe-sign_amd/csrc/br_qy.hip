@@ -244,10 +244,31 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
             for (int r = 0; r < 8; ++r) x[r] = make_double2(tor_digit_s(acc[r]), tor_digit_s(acc[r + 8]));
         }
 
+        // G = 2: the key bundle of this group per point of phase E (oracle cmul_acc, patterns in order),
+        // in six chunks of 8 key slices (pattern B, rows/columns rc in {2 h, 2 h + 1}, all points) spread
+        // over the forward phases: each chunk's loads are issued a phase before it is folded in (sched
+        // barriers keep the compiler from bunching all 48 loads); and the next group's monomial factors
+        cplx eB[3], Ga[8], Gb[8];
+        auto issue = [&](int c, cplx (&g)[8]) {
+            const int B = c >> 1, h2 = c & 1;
+            const bptr kg{bsk_rs, 16u * (uint32_t)L, (uint32_t)((3 * i + B) * 4096 + w * 256) * 16u};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) g[q] = kg[(2 * h2 + (q >> 2)) * 1024 + (q & 3) * 64];
+        };
+        auto fold = [&](int c, const cplx (&g)[8]) {
+            const int B = c >> 1, h2 = c & 1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t tr = (uint32_t)((k >> 1) + 2 * (k & 1)) * mB[B];  // (j8 + 2 j9) m_B
+                const cplx wv = k == 0 ? make_double2(eB[B].x - 1.0, eB[B].y) : turn_sel_m1(eB[B], tr);
+#pragma unroll
+                for (int r2 = 0; r2 < 2; ++r2) {
+                    const int rc = 2 * h2 + r2;
+                    Kb[rc * 4 + k] = cmul_acc(Kb[rc * 4 + k], g[r2 * 4 + k], wv);
+                }
+            }
+        };
         if constexpr (G == 2) {
-            // key bundle of this group per point of phase E (oracle cmul_acc, patterns in order), and
-            // the next group's monomial factors
-            cplx eB[3];
 #pragma unroll
             for (int B = 0; B < 3; ++B) eB[B] = cmul(EbnB[B], FnB[B]);  // exact when kk = 0
             if (2 * i + 2 < n) {
@@ -260,17 +281,8 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
             }
 #pragma unroll
             for (int q = 0; q < 16; ++q) Kb[q] = make_double2(0.0, 0.0);
-#pragma unroll
-            for (int B = 0; B < 3; ++B) {
-                const bptr kg{bsk_rs, 16u * (uint32_t)L, (uint32_t)((3 * i + B) * 4096 + w * 256) * 16u};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t tr = (uint32_t)((k >> 1) + 2 * (k & 1)) * mB[B];  // (j8 + 2 j9) m_B
-                    const cplx wv = k == 0 ? make_double2(eB[B].x - 1.0, eB[B].y) : turn_sel_m1(eB[B], tr);
-#pragma unroll
-                    for (int rc = 0; rc < 4; ++rc) Kb[rc * 4 + k] = cmul_acc(Kb[rc * 4 + k], kg[rc * 1024 + k * 64], wv);
-                }
-            }
+            issue(0, Ga);
+            __builtin_amdgcn_sched_barrier(0);
         }
         // ---- phase A: stages 0-2 (uniform zetas)
 #pragma unroll
@@ -282,6 +294,12 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
         for (int r = 0; r < 8; r += 2) {
             const cplx base = (r >> 2) ? Zu[6] : Zu[4];
             dit_bfly(x[r], x[r + 1], ((r >> 1) & 1) ? mul_i(base) : base);
+        }
+        if constexpr (G == 2) {
+            __builtin_amdgcn_sched_barrier(0);
+            fold(0, Ga);
+            issue(1, Gb);
+            __builtin_amdgcn_sched_barrier(0);
         }
         // ---- A -> B: register bits 2, 1 <-> lane bits 5, 4
 #pragma unroll
@@ -301,6 +319,12 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
                 dit_bfly(x[r], x[r + 2], (r >> 2) ? mul_i(base) : base);                 // b6
             }
         }
+        if constexpr (G == 2) {
+            __builtin_amdgcn_sched_barrier(0);
+            fold(1, Gb);
+            issue(2, Ga);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         // ---- B -> B' (wave-private LDS round trip)
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bB + xq(idx_B(0, 0, r))] = x[r];
@@ -314,6 +338,12 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
                 if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
         }
 #endif
+        if constexpr (G == 2) {
+            __builtin_amdgcn_sched_barrier(0);
+            fold(2, Ga);
+            issue(3, Gb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         // ---- phase B': stages 5 (b4, register bit 2), 6 (b3, bit 1), 7 (b2, bit 0)
         {
             const cplx z5 = s_z[12 + U], z6 = s_z[44 + U], z7a = s_z[76 + U], z7b = s_z[108 + U];
@@ -338,6 +368,12 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
                 if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
         }
 #endif
+        if constexpr (G == 2) {
+            __builtin_amdgcn_sched_barrier(0);
+            fold(3, Gb);
+            issue(4, Ga);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         cplx e0 = make_double2(1.0, 0.0);
         if constexpr (G == 1) {
             e0 = cmul(Ebn, Fn);  // exact when kk = 0 (Fn = E[0] = 1)
@@ -345,6 +381,10 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
             Ebn = lane_factor(a_next);
         }
         __syncthreads();
+        if constexpr (G == 2) {
+            issue(5, Gb);
+            fold(4, Ga);
+        }
         // ---- phase E: both polynomials at this wave's points, stages 8 (b1), 9 (b0)
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
@@ -367,6 +407,7 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
                 x[r + 1] = csub(a0, t);
             }
         }
+        if constexpr (G == 2) fold(5, Gb);
         // MAC (own digit first, oracle mac_own_first) and (X^a - 1) per point, shared by both outputs
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
