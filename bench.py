@@ -162,15 +162,20 @@ def cpu_baseline(seed, target_s, op_levels=None):
     return res
 
 
-def pmc_traffic(batch, kernel="k_blind_rotate_qy"):
+def pmc_traffic(batch, kernels=("k_blind_rotate_qy<1>", "k_blind_rotate_qy grid")):
     """HBM-side bytes per launch of the blind-rotate kernel at this batch, from the committed PMC
     summary of the same kernel (tools/profile_round.sh; FETCH_SIZE x2 + WRITE_SIZE, gfx950
-    correction of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits included)"""
+    correction of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits included).  `kernels`: name
+    patterns tried in order (the classic kernel is the <1> instance of br_qy.hip's template; summaries
+    from before it was a template name it without the argument)"""
     try:
         d = json.load(open(PMC_SUMMARY))["pmc"][f"B={batch}"]
-        k = next(v for k, v in d.items() if kernel in k)
-        return k["hbm_side_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
-    except (OSError, KeyError, StopIteration, ValueError):
+        for kernel in kernels:
+            k = next((v for k, v in d.items() if kernel in k), None)
+            if k is not None:
+                return k["hbm_side_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
+        return None, None
+    except (OSError, KeyError, ValueError):
         return None, None
 
 
@@ -474,7 +479,7 @@ def pbs_leg(a, kind, dist, rank, world, device):
         "roofline": {
             "bound": "fp64_valu",
             "compute_pipe": "fp64 VALU (FFT butterflies; no dense contraction on the path)",
-            "kernel": "k_blind_rotate_qy" if kind == "classic" else "k_blind_rotate_quad<2>",
+            "kernel": "k_blind_rotate_qy<1>" if kind == "classic" else "k_blind_rotate_qy<2>",
             "achieved": achieved,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
@@ -577,7 +582,7 @@ def main():
     res["latency_level_ms"] = cl["latency_level_ms"]  # blind rotate of one latency level, B = 1 / 256
     if mb is not None:
         # tfhe-rs' MultiBitPBS shape (grouping factor 2) on the same client key: same decrypted results
-        t_mb, src_mb = pmc_traffic(B, "k_blind_rotate_quad<2>")
+        t_mb, src_mb = pmc_traffic(B, ("k_blind_rotate_qy<2>",))
         mb["roofline"]["traffic"] = t_mb
         mb["roofline"]["traffic_source"] = src_mb
         res["multibit"] = mb

@@ -548,7 +548,7 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
     FHE_HIP_CHECK(hipMemcpy(c->d_tw_wide, tww.data(), tww.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMemcpy(c->d_psi_wide, psiw.data(), psiw.size() * sizeof(double2), hipMemcpyHostToDevice));
     if (const char* e = getenv("FHE_WIDE_THRESHOLD")) c->wide_threshold = atoi(e);
-    if (const char* e = getenv("FHE_MB_QY")) c->mb_qy = atoi(e) != 0;  // multi-bit throughput levels on br_qy.hip
+    if (const char* e = getenv("FHE_MB_QY")) c->mb_qy = atoi(e) != 0;  // 0: multi-bit throughput levels on br_quad.hip
     std::vector<double2> mono;
     mono_table(psi, &mono);
     FHE_HIP_CHECK(hipMalloc(&c->d_mono, mono.size() * sizeof(double2)));

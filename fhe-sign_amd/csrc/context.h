@@ -69,7 +69,7 @@ struct fhe_ctx {
     // time -- >128 KB LDS -- so one round over the 256 CUs); the throughput kernel above, which holds
     // 2-3 per CU (profiles/r2/latency_sweep_r2b.txt: from 320 on it is as fast or faster)
     int wide_threshold = 256;
-    bool mb_qy = false;  // multi-bit throughput levels on br_qy.hip<2> instead of br_quad.hip (FHE_MB_QY)
+    bool mb_qy = true;  // multi-bit throughput levels on br_qy.hip<2>, not br_quad.hip (FHE_MB_QY=0 turns it off)
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;
