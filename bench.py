@@ -41,7 +41,7 @@ FLOPS_PER_GROUP_MB = FLOPS_PER_CMUX + 1024 * (3 + 96)
 L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 ~34.5 TB/s aggregate
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -55,7 +55,111 @@ def parse():
     ap.add_argument("--seed", type=int, default=0xF11E51)
     ap.add_argument("--no-ops", action="store_true", help="skip the 256-bit mul / sign wall-clock legs")
     ap.add_argument("--no-multibit", action="store_true", help="skip the multi-bit (grouping 2) measurement")
-    return ap.parse_args()
+    ap.add_argument("--launch-deadline", type=float, default=LAUNCH_DEADLINE_S,
+                    help="self-launched N > 1 runs: seconds before every rank is killed")
+    # GPU-free rehearsal of the N > 1 control plane (the launcher test): every rank joins the gloo
+    # group, times a barrier-bracketed sleep, takes the max over ranks, rank 0 prints the line
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------------------------ launcher
+LAUNCH_DEADLINE_S = 1500.0
+LAUNCH_GRACE_S = 30.0  # after one rank fails, how long the others get to finish before being killed
+LAUNCH_FAIL_EXIT = 4
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n: int, argv: list, deadline_s: float) -> int:
+    """`--gpus N > 1` started from a bare shell (no RANK/WORLD_SIZE in the environment): this process
+    becomes the launcher.  It makes no GPU call (nothing here imports torch or the engine); it starts
+    N rank processes of this same script as children -- subprocess, never exec -- each with
+    RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT set, relays rank 0's stdout (the JSON line)
+    and returns non-zero if any rank fails (its first failing status, or LAUNCH_FAIL_EXIT for a
+    signal), killing the rest after LAUNCH_GRACE_S; at `deadline_s` every rank still running is
+    killed and the launcher returns 124.  Under torchrun (WORLD_SIZE set) this is never reached."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, start_new_session=True))
+
+    def relay():
+        for line in procs[0].stdout:
+            sys.stdout.write(line.decode(errors="replace"))
+            sys.stdout.flush()
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                pass
+
+    t_end = time.monotonic() + deadline_s
+    failed_at, status = None, 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and failed_at is None:
+            failed_at = time.monotonic()
+            status = bad[0] if bad[0] > 0 else LAUNCH_FAIL_EXIT
+            sys.stderr.write(f"bench launcher: a rank exited with status {bad[0]}\n")
+        if all(c is not None for c in codes):
+            break
+        now = time.monotonic()
+        if now > t_end:
+            sys.stderr.write(f"bench launcher: deadline of {deadline_s:.0f} s passed; killing every rank\n")
+            kill_all()
+            th.join(5)
+            return 124
+        if failed_at is not None and now - failed_at > LAUNCH_GRACE_S:
+            sys.stderr.write("bench launcher: killing the ranks left after a failure\n")
+            kill_all()
+            break
+        time.sleep(0.2)
+    th.join(10)
+    return status
+
+
+def dry_run(a, dist, rank, world):
+    """The N > 1 control plane without a GPU: barrier + sleep + barrier, max over ranks, one line."""
+    if rank == a.dry_fail_rank:
+        sys.stderr.write(f"bench dry run: rank {rank} failing on request\n")
+        sys.exit(5)
+    barrier(dist)
+    t0 = time.perf_counter()
+    time.sleep(0.05 * (rank + 1))
+    dt = allmax(dist, time.perf_counter() - t0)
+    barrier(dist)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": world * a.steps / dt, "unit": "steps/s (dry run)",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+                          "dry_run": True, "pid": os.getpid()}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def dist_setup(n):
@@ -407,6 +511,26 @@ def pbs_leg(a, kind, dist, rank, world, device):
     ctx.h2d(d_in, cts)
     ctx.h2d(d_lut, np.full(B, lid, np.uint32))
 
+    def latency_levels():
+        """the latency kernel at the level sizes of the serial carry chains (one ciphertext per CU):
+        best of 3 blind-rotate times (HIP events) at B = 1 and 256 -- the per-level floor of the
+        compat mul / sign"""
+        lat = {}
+        ctx.enable_timing(True)
+        for nb in (1, 256):
+            ctx.pbs_device(d_in, nb, d_lut, d_out)  # untimed first launch (code object, workspace)
+            best = 1e9
+            for _ in range(3):
+                ctx.pbs_device(d_in, nb, d_lut, d_out)
+                best = min(best, ctx.last_pbs_timing()[1])
+            lat[f"B={nb}"] = best
+        ctx.enable_timing(False)
+        return lat
+
+    # before any throughput launch (cool chip) and again after the timed steps (clock under load):
+    # both in the line, so a difference between them is the clock, measured in the same run
+    lat_before = latency_levels()
+
     for _ in range(a.warmup):
         ctx.pbs_device(d_in, B, d_lut, d_out)
     ctx.sync()
@@ -439,17 +563,7 @@ def pbs_leg(a, kind, dist, rank, world, device):
         ctx.pbs(cts, lid)
     pcie_rate = host_reps * B / (time.perf_counter() - t0)
 
-    # the latency kernel at the level sizes of the serial carry chains (one ciphertext per CU): best of
-    # 3 blind-rotate times (HIP events) at B = 1 and 256 -- the per-level floor of the compat mul / sign
-    lat = {}
-    ctx.enable_timing(True)
-    for nb in (1, 256):
-        best = 1e9
-        for _ in range(3):
-            ctx.pbs_device(d_in, nb, d_lut, d_out)
-            best = min(best, ctx.last_pbs_timing()[1])
-        lat[f"B={nb}"] = best
-    ctx.enable_timing(False)
+    lat = {"before_throughput": lat_before, "after_throughput": latency_levels()}
     # correctness spot check of the last step (decrypt a sample)
     ctx.pbs_device(d_in, B, d_lut, d_out)
     out = np.zeros_like(cts)
@@ -503,12 +617,22 @@ def pbs_leg(a, kind, dist, rank, world, device):
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # bare `python bench.py --gpus N`: be the launcher (no GPU call in this process)
+        sys.exit(self_launch(a.gpus, sys.argv[1:], a.launch_deadline))
     dist, rank, world, local = dist_setup(a.gpus)
+    if a.dry_run:
+        dry_run(a, dist, rank, world)
+        return
 
     device = local
     if dist is not None:  # more ranks than visible GPUs (rehearsals): ranks share devices round-robin
         import torch
-        device = local % max(1, torch.cuda.device_count())
+        ndev = max(1, torch.cuda.device_count())
+        device = local % ndev
+        if world > ndev and rank == 0:
+            sys.stderr.write(f"bench: {world} ranks on {ndev} visible GPU(s): ranks share devices (rehearsal); "
+                             "RCCL refuses two ranks on one device, so the fan-out legs report that error\n")
     B = a.batch
     # headline: the default (classic) parameters of configs[1]; the multi-bit blind rotation (same
     # client key, grouping 2) is measured beside it with the same protocol
@@ -579,7 +703,8 @@ def main():
         res["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
                                           "speedup": v / ops[k]["seconds"]} for k, v in readme.items() if k in ops}
     res["pcie_inclusive_pbs_per_s"] = cl["pcie_inclusive_pbs_per_s"]
-    res["latency_level_ms"] = cl["latency_level_ms"]  # blind rotate of one latency level, B = 1 / 256
+    # blind rotate of one latency level, B = 1 / 256, before and after the timed throughput steps
+    res["latency_level_ms"] = cl["latency_level_ms"]
     if mb is not None:
         # tfhe-rs' MultiBitPBS shape (grouping factor 2) on the same client key: same decrypted results
         t_mb, src_mb = pmc_traffic(B, ("k_blind_rotate_qy<2>",))

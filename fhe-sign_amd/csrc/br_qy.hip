@@ -526,17 +526,35 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
     }
 }
 
+// Fourier BSK: blind-rotate layout (R = 4v + q, lane L' <-> idx = 4 (L' + 64 v) + q) -> E layout
+// [poly][wave e][point k][lane], one workgroup per polynomial.
+__global__ __launch_bounds__(256) void k_bsk_to_e(const cplx* __restrict__ src, cplx* __restrict__ dst) {
+    const cplx* s = src + (size_t)blockIdx.x * 1024;
+    cplx* d = dst + (size_t)blockIdx.x * 1024;
+    for (int o = threadIdx.x; o < 1024; o += 256) {
+        const int e = o >> 8, k = (o >> 6) & 3, L = o & 63;
+        const int idx = idx_E(e, L, k);
+        const int q = idx & 3, Lp = (idx >> 2) & 63, v = idx >> 8;
+        d[o] = s[(4 * v + q) * 64 + Lp];
+    }
+}
+
+hipError_t launch_bsk_to_e(const cplx* bsk, int npoly, cplx* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_bsk_to_e, dim3(npoly), dim3(256), 0, s, bsk, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
-                                  const uint64_t* luts, const cplx* bsk_qx, const cplx* tw, const cplx* ps,
+                                  const uint64_t* luts, const cplx* bsk_e, const cplx* tw, const cplx* ps,
                                   const cplx* zfull, const cplx* mono, int grouping, uint64_t* out, int count, int n,
                                   hipStream_t s) {
     if (count <= 0) return hipSuccess;
     if (grouping == 2)
         hipLaunchKernelGGL(k_blind_rotate_qy<2>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
-                           bsk_qx, tw, ps, zfull, mono, out, n);
+                           bsk_e, tw, ps, zfull, mono, out, n);
     else
         hipLaunchKernelGGL(k_blind_rotate_qy<1>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
-                           bsk_qx, tw, ps, zfull, mono, out, n);
+                           bsk_e, tw, ps, zfull, mono, out, n);
     return hipGetLastError();
 }
 

@@ -54,15 +54,11 @@ int comm_wait_impl(fhe_ctx* c, const char* what) {
     for (;;) {
         const hipError_t q = hipStreamQuery(c->stream);
         if (q == hipSuccess) {
-            c->prog_done = c->prog_rec;
+            c->prog_q.clear();
             return FHE_OK;
         }
         // the deadline counts time without progress: a completed level mark restarts it
-        while (c->prog_done < c->prog_rec &&
-               hipEventQuery(c->prog_ev[c->prog_done % fhe_ctx::kProgRing]) == hipSuccess) {
-            ++c->prog_done;
-            t0 = std::chrono::steady_clock::now();
-        }
+        if (c->drain_progress()) t0 = std::chrono::steady_clock::now();
         if (q != hipErrorNotReady) {
             set_error(std::string(what) + ": " + hipGetErrorString(q));
             return FHE_ERR_HIP;
@@ -150,16 +146,68 @@ int fhe_ctx::allgather(uint64_t* buf, size_t words) {
                        "ncclAllGather", comm_timeout_ms, false);
 }
 
+bool fhe_ctx::drain_progress() {
+    size_t k = 0;
+    while (k < prog_q.size() && hipEventQuery(prog_ev[prog_q[k].ev]) == hipSuccess) ++k;
+    prog_q.erase(prog_q.begin(), prog_q.begin() + k);
+    return k > 0;
+}
+
+namespace {
+// Every mark outstanding and a new one due at level `newest`: the inner mark i whose neighbours are
+// closest (dropping it merges the two shortest adjacent intervals; the newest mark's right
+// neighbour is the new mark).  Greedy merging keeps every gap within about 2x the mean.
+size_t merge_victim(const std::vector<uint64_t>& seq, uint64_t newest) {
+    size_t best = 1;
+    uint64_t span = UINT64_MAX;
+    for (size_t i = 1; i < seq.size(); ++i) {
+        const uint64_t right = i + 1 < seq.size() ? seq[i + 1] : newest;
+        if (right - seq[i - 1] < span) {
+            span = right - seq[i - 1];
+            best = i;
+        }
+    }
+    return best;
+}
+}  // namespace
+
 void fhe_ctx::mark_progress() {
     if (!comm) return;
-    if (!prog_ev[0])
+    if (!prog_ev[0]) {
         for (auto& e : prog_ev)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+        prog_q.reserve(kProgRing);
+    }
     if (!prog_ev[kProgRing - 1]) return;
-    // a full ring re-records the newest mark (marks complete in stream order, so it still stands for
-    // "everything up to here")
-    const uint64_t slot = prog_rec - prog_done < (uint64_t)kProgRing ? prog_rec++ : prog_rec - 1;
-    (void)hipEventRecord(prog_ev[slot % kProgRing], stream);
+    ++prog_seq;
+    if (prog_q.size() == (size_t)kProgRing) drain_progress();
+    int ev = -1;
+    if (prog_q.size() < (size_t)kProgRing) {
+        bool used[kProgRing] = {};
+        for (const ProgMark& m : prog_q) used[m.ev] = true;
+        for (int e = 0; e < kProgRing && ev < 0; ++e)
+            if (!used[e]) ev = e;
+    } else {
+        std::vector<uint64_t> seq;
+        for (const ProgMark& m : prog_q) seq.push_back(m.seq);
+        const size_t v = merge_victim(seq, prog_seq);
+        ev = prog_q[v].ev;  // re-recorded below at the newest level
+        prog_q.erase(prog_q.begin() + v);
+    }
+    if (hipEventRecord(prog_ev[ev], stream) == hipSuccess) prog_q.push_back({ev, prog_seq});
+}
+
+extern "C" int fhe_progress_marks_probe(uint32_t levels, uint32_t* max_gap) {
+    if (!max_gap) return FHE_ERR_INVALID;
+    std::vector<uint64_t> q;  // mark_progress's bookkeeping with no mark completing
+    for (uint64_t seq = 1; seq <= levels; ++seq) {
+        if (q.size() == (size_t)fhe_ctx::kProgRing) q.erase(q.begin() + merge_victim(q, seq));
+        q.push_back(seq);
+    }
+    uint64_t gap = q.empty() ? 0 : q[0];
+    for (size_t i = 1; i < q.size(); ++i) gap = std::max<uint64_t>(gap, q[i] - q[i - 1]);
+    *max_gap = (uint32_t)gap;
+    return FHE_OK;
 }
 
 int fhe_ctx::allreduce_min_u8(uint8_t* flags, size_t n) {
@@ -187,7 +235,8 @@ void fhe_ctx::release_comm() {
         (void)ncclCommDestroy((ncclComm_t)comm);
         comm = nullptr;
     }
-    prog_rec = prog_done = 0;
+    prog_q.clear();
+    prog_seq = 0;
     nranks = 1;
     rank = 0;
 }
@@ -446,7 +495,7 @@ int fhe_ctx_detach_comm(fhe_ctx* c) {
 // the server key lives on one rank (e.g. deserialized from the client) and is
 // replicated device-to-device over xGMI.  Rank `root` broadcasts its parameters, then its
 // standard-layout KSK and Fourier BSK (123 MB at the default parameters); every other rank
-// derives the kernels' layouts (KSK byte planes, quad BSK) with its own conversion kernels, exactly
+// derives the kernels' layouts (KSK byte planes, E-layout BSK) with its own conversion kernels, exactly
 // as fhe_set_server_key would.  Collective: every rank of the communicator calls it.
 //
 // Failure handling (every rank takes the same branch, so no rank is left inside a collective its
@@ -500,24 +549,22 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     // usable until every collective and conversion has succeeded, then the two are swapped.
     uint64_t* n_ksk = nullptr;
     int8_t* n_planes = nullptr;
-    double2 *n_bsk = nullptr, *n_quad = nullptr, *n_qx = nullptr;
+    double2 *n_bsk = nullptr, *n_e = nullptr;
     auto drop_new = [&] {
         (void)hipStreamSynchronize(c->stream);
         if (n_ksk) (void)hipFree(n_ksk);
         if (n_planes) (void)hipFree(n_planes);
         if (n_bsk) (void)hipFree(n_bsk);
-        if (n_quad) (void)hipFree(n_quad);
-        if (n_qx) (void)hipFree(n_qx);
+        if (n_e) (void)hipFree(n_e);
         n_ksk = nullptr;
         n_planes = nullptr;
-        n_bsk = n_quad = n_qx = nullptr;
+        n_bsk = n_e = nullptr;
     };
     if (!is_root && local_ok) {
         hipError_t he = hipMalloc(&n_ksk, ksk_words * 8);
         if (he == hipSuccess) he = hipMalloc(&n_planes, fhe::ks_planes_bytes((int)p.n));
         if (he == hipSuccess) he = hipMalloc(&n_bsk, bsk_doubles * 8);
-        if (he == hipSuccess) he = hipMalloc(&n_quad, bsk_doubles * 8);
-        if (he == hipSuccess && p.grouping == 1) he = hipMalloc(&n_qx, bsk_doubles * 8);
+        if (he == hipSuccess) he = hipMalloc(&n_e, bsk_doubles * 8);
         if (he != hipSuccess) {
             drop_new();
             local_ok = 0;
@@ -547,8 +594,7 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
         return rc;
     }
     rc = launch_ksk_to_planes(n_ksk, (int)p.n, n_planes, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
-    if (!rc) rc = launch_bsk_to_quad(n_bsk, npoly, n_quad, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
-    if (!rc && n_qx) rc = launch_bsk_to_qx(n_bsk, npoly, n_qx, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
+    if (!rc) rc = launch_bsk_to_e(n_bsk, npoly, n_e, c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (!rc) rc = hipStreamSynchronize(c->stream) == hipSuccess ? FHE_OK : FHE_ERR_HIP;
     if (rc) {
         drop_new();
@@ -567,8 +613,7 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
     std::swap(c->d_ksk, n_ksk);
     std::swap(c->d_ksk_planes, n_planes);
     std::swap(c->d_bsk, n_bsk);
-    std::swap(c->d_bsk_quad, n_quad);
-    std::swap(c->d_bsk_qx, n_qx);
+    std::swap(c->d_bsk_e, n_e);
     drop_new();  // frees the previous key's buffers (null when there was none)
     if (!(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
         c->lut_ids.clear();

@@ -63,30 +63,6 @@ void zeta_table(std::vector<double2>* Z) {
         }
 }
 
-// br_quad.hip zeta layout (QZ_*): lane-varying zetas of stages 3-9 (even blocks), 1, -i, uniform ones
-void quad_zetas(const std::vector<double2>& Z, std::vector<double2>* q) {
-    q->assign(550, make_double2(0.0, 0.0));
-    for (int B3 = 0; B3 < 8; ++B3) {
-        (*q)[B3] = Z[8 + B3];
-        (*q)[8 + B3] = Z[16 + 2 * B3];
-        for (int j = 0; j < 2; ++j) (*q)[16 + 8 * j + B3] = Z[32 + 4 * B3 + 2 * j];
-    }
-    for (int B6 = 0; B6 < 64; ++B6) {
-        (*q)[32 + B6] = Z[64 + B6];
-        (*q)[96 + B6] = Z[128 + 2 * B6];
-        for (int j = 0; j < 2; ++j) (*q)[160 + 64 * j + B6] = Z[256 + 4 * B6 + 2 * j];
-    }
-    for (int r2 = 0; r2 < 4; ++r2)
-        for (int h = 0; h < 2; ++h)
-            for (int u = 0; u < 32; ++u) (*q)[288 + 64 * r2 + 32 * h + u] = Z[512 + 256 * h + 8 * u + 2 * r2];
-    (*q)[544] = make_double2(1.0, 0.0);
-    (*q)[545] = make_double2(0.0, -1.0);
-    (*q)[546] = Z[1];
-    (*q)[547] = Z[2];
-    (*q)[548] = Z[4];
-    (*q)[549] = Z[6];
-}
-
 // br_wide.hip: per-thread zetas of the twisted forward, [10][256] (t = 64 q + L): phases A..E, two each
 void wide_zetas(const std::vector<double2>& Z, std::vector<double2>* zw) {
     zw->assign(10 * 256, make_double2(0.0, 0.0));
@@ -279,14 +255,8 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     if ((int)count <= wide_threshold)
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
-    if ((p.grouping == 1 || mb_qy) && br_kernel == FHE_BR_QY && d_bsk_qx)
-        return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
-                                      d_zeta_full, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
-    if (p.grouping == 1 && br_kernel == FHE_BR_QX && d_bsk_qx)
-        return launch_blind_rotate_qx(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_qx, d_tw_quad, d_psi_quad,
-                                      d_zeta_full, d_mono, out, (int)count, (int)p.n, stream);
-    return launch_blind_rotate_quad(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_quad, d_tw_quad, d_psi_quad,
-                                    d_zeta_quad, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
+    return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_e, d_tw_quad, d_psi_quad, d_zeta_full,
+                                  d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
 }
 
 // =========================================================================== C ABI (core)
@@ -524,18 +494,15 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
         return FHE_ERR_HIP;
     }
     for (auto& ev : c->ev) FHE_HIP_CHECK(hipEventCreate(&ev));
-    std::vector<double2> W0, W, psi, tww, psiw, twq, psq, Z, zq;
+    std::vector<double2> W0, W, psi, tww, psiw, twq, psq, Z;
     fft_tables(&W0, &psi);
     zeta_table(&Z);
-    quad_zetas(Z, &zq);
     std::vector<double2> zw;
     wide_zetas(Z, &zw);
     FHE_HIP_CHECK(hipMalloc(&c->d_zeta_wide, zw.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_zeta_wide, zw.data(), zw.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMalloc(&c->d_zeta_full, Z.size() * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpy(c->d_zeta_full, Z.data(), Z.size() * sizeof(double2), hipMemcpyHostToDevice));
-    FHE_HIP_CHECK(hipMalloc(&c->d_zeta_quad, zq.size() * sizeof(double2)));
-    FHE_HIP_CHECK(hipMemcpy(c->d_zeta_quad, zq.data(), zq.size() * sizeof(double2), hipMemcpyHostToDevice));
     lane_twiddles(W0, &W);
     wide_tables(W0, psi, &tww, &psiw);
     quad_tables(W0, psi, &twq, &psq);
@@ -548,7 +515,6 @@ int fhe_ctx_create(int device, fhe_ctx** out) {
     FHE_HIP_CHECK(hipMemcpy(c->d_tw_wide, tww.data(), tww.size() * sizeof(double2), hipMemcpyHostToDevice));
     FHE_HIP_CHECK(hipMemcpy(c->d_psi_wide, psiw.data(), psiw.size() * sizeof(double2), hipMemcpyHostToDevice));
     if (const char* e = getenv("FHE_WIDE_THRESHOLD")) c->wide_threshold = atoi(e);
-    if (const char* e = getenv("FHE_MB_QY")) c->mb_qy = atoi(e) != 0;  // 0: multi-bit throughput levels on br_quad.hip
     std::vector<double2> mono;
     mono_table(psi, &mono);
     FHE_HIP_CHECK(hipMalloc(&c->d_mono, mono.size() * sizeof(double2)));
@@ -568,8 +534,8 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     delete c->engine;
     c->engine = nullptr;
     c->release_comm();
-    void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_bsk_quad, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
-                    c->d_psi_quad, c->d_zeta_quad, c->d_zeta_wide, c->d_mono, c->d_bsk_qx, c->d_zeta_full, c->d_flags, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
+    void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
+                    c->d_psi_quad, c->d_zeta_wide, c->d_mono, c->d_bsk_e, c->d_zeta_full, c->d_flags, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)
@@ -588,14 +554,12 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
         FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
         FHE_HIP_CHECK(hipFree(c->d_ksk));
         FHE_HIP_CHECK(hipFree(c->d_bsk));
-        FHE_HIP_CHECK(hipFree(c->d_bsk_quad));
-        if (c->d_bsk_qx) FHE_HIP_CHECK(hipFree(c->d_bsk_qx));
+        FHE_HIP_CHECK(hipFree(c->d_bsk_e));
         FHE_HIP_CHECK(hipFree(c->d_ksk_planes));
         c->d_ksk_planes = nullptr;
         c->d_ksk = nullptr;
         c->d_bsk = nullptr;
-        c->d_bsk_quad = nullptr;
-        c->d_bsk_qx = nullptr;
+        c->d_bsk_e = nullptr;
         c->has_key = false;
     }
     FHE_HIP_CHECK(hipMalloc(&c->d_ksk, sk->ksk.size() * 8));
@@ -608,12 +572,10 @@ int fhe_set_server_key(fhe_ctx* c, const fhe_server_key* sk) {
     FHE_HIP_CHECK(hipMalloc(&c->d_bsk, (size_t)npoly * 1024 * sizeof(double2)));
     FHE_HIP_CHECK(hipMemcpyAsync(d_std, sk->bsk.data(), sk->bsk.size() * 8, hipMemcpyHostToDevice, c->stream));
     FHE_HIP_CHECK(launch_bsk_to_fourier(d_std, npoly, c->d_W, c->d_psi, c->d_bsk, c->stream));
-    FHE_HIP_CHECK(hipMalloc(&c->d_bsk_quad, (size_t)npoly * 1024 * sizeof(double2)));
-    FHE_HIP_CHECK(launch_bsk_to_quad(c->d_bsk, npoly, c->d_bsk_quad, c->stream));
-    if (p.grouping == 1 || c->mb_qy) {  // the qx/qy kernels' layout (br_qx.hip)
-        FHE_HIP_CHECK(hipMalloc(&c->d_bsk_qx, (size_t)npoly * 1024 * sizeof(double2)));
-        FHE_HIP_CHECK(launch_bsk_to_qx(c->d_bsk, npoly, c->d_bsk_qx, c->stream));
-    }
+    // two resident layouts: d_bsk for the latency kernel (br_wide.hip), d_bsk_e for the throughput
+    // kernel (br_qy.hip); rounds 1-4 also kept br_quad.hip's and ran br_qx.hip (both retired in r5)
+    FHE_HIP_CHECK(hipMalloc(&c->d_bsk_e, (size_t)npoly * 1024 * sizeof(double2)));
+    FHE_HIP_CHECK(launch_bsk_to_e(c->d_bsk, npoly, c->d_bsk_e, c->stream));
     FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
     FHE_HIP_CHECK(hipFree(d_std));
     if (!c->has_key || !(c->p.msg_carry() == p.msg_carry() && c->p.delta() == p.delta())) {
@@ -662,6 +624,9 @@ int fhe_ctx_sync(fhe_ctx* c) {
     if (c->engine) {
         try {
             c->engine->flush();  // launch the deferred radix graph
+        } catch (const fhe::EngineError& e) {  // keeps its status (e.g. FHE_ERR_TIMEOUT of a collective)
+            set_error(e.what());
+            return e.code;
         } catch (const std::exception& e) {
             set_error(e.what());
             return FHE_ERR_HIP;
@@ -754,18 +719,13 @@ int fhe_ctx_set_ks_kernel(fhe_ctx* c, int kind) {
 
 int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
     if (!c) return FHE_ERR_INVALID;
-    if (kind == FHE_BR_NARROW) {
-        set_error("the 2-wave blind-rotate kernel (FHE_BR_NARROW) is retired; FHE_BR_QUAD is the throughput kernel");
+    if (kind == FHE_BR_QY) return FHE_OK;  // the one throughput kernel (classic and multi-bit)
+    if (kind == FHE_BR_NARROW || kind == FHE_BR_PAIR || kind == FHE_BR_QUAD || kind == FHE_BR_QX) {
+        set_error("retired blind-rotate kernel (NARROW r1, PAIR r2, QUAD r3, QX r4; sources in tools/retired/); "
+                  "FHE_BR_QY (br_qy.hip) is the throughput kernel");
         return FHE_ERR_INVALID;
     }
-    if (kind == FHE_BR_PAIR) {
-        set_error("the 2-wave pair kernel (FHE_BR_PAIR) is retired (it ran at parity with FHE_BR_QUAD); "
-                  "FHE_BR_QUAD is the throughput kernel");
-        return FHE_ERR_INVALID;
-    }
-    if (kind != FHE_BR_QUAD && kind != FHE_BR_QX && kind != FHE_BR_QY) return FHE_ERR_INVALID;
-    c->br_kernel = kind;
-    return FHE_OK;
+    return FHE_ERR_INVALID;
 }
 
 int fhe_ctx_set_wide_threshold(fhe_ctx* c, int threshold) {

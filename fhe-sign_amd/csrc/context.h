@@ -51,15 +51,12 @@ struct fhe_ctx {
     double2* d_psi = nullptr;
     double2* d_tw_wide = nullptr;   // [12][256]
     double2* d_psi_wide = nullptr;  // [4][256]
-    double2* d_bsk_quad = nullptr;  // Fourier BSK in the 4-wave kernel's layout (br_quad.hip)
-    double2* d_bsk_qx = nullptr;    // classic Fourier BSK in br_qx.hip's E layout (grouping 1 only)
-    double2* d_zeta_full = nullptr; // zeta(s, b) at [2^s + b], 1024 entries (br_qx.hip)
+    double2* d_bsk_e = nullptr;     // Fourier BSK in the throughput kernel's E layout (br_qy.hip)
+    double2* d_zeta_full = nullptr; // zeta(s, b) at [2^s + b], 1024 entries (br_qy.hip)
     double2* d_tw_quad = nullptr;   // W[0..512)
     double2* d_psi_quad = nullptr;  // [2][8][128]: twist (unused since the twisted forward), untwist
-    double2* d_zeta_quad = nullptr; // br_quad.hip zeta layout (context.cpp:quad_zetas)
     double2* d_zeta_wide = nullptr; // [10][256] (context.cpp:wide_zetas)
     double2* d_mono = nullptr;      // monomial table E[4096] of the multi-bit blind rotation (mono_table)
-    int br_kernel = FHE_BR_QY;      // throughput kernel for levels above wide_threshold (classic; multi-bit: quad)
     int8_t* d_ksk_planes = nullptr; // KSK as balanced signed-byte planes (ks_mfma.hip)
     int ks_kernel = FHE_KS_MFMA;
     int8_t* d_ks_digits = nullptr;  // keyswitch digits workspace
@@ -69,7 +66,6 @@ struct fhe_ctx {
     // time -- >128 KB LDS -- so one round over the 256 CUs); the throughput kernel above, which holds
     // 2-3 per CU (profiles/r2/latency_sweep_r2b.txt: from 320 on it is as fast or faster)
     int wide_threshold = 256;
-    bool mb_qy = true;  // multi-bit throughput levels on br_qy.hip<2>, not br_quad.hip (FHE_MB_QY=0 turns it off)
     // LUT registry: table contents -> id, device array of accumulator polynomials
     std::map<std::vector<uint32_t>, uint32_t> lut_ids;
     std::vector<uint64_t> h_luts;
@@ -111,11 +107,22 @@ struct fhe_ctx {
     // flush keeps completing progress marks and is never cut off)
     int wait_stream(const char* what);
     // progress marks: an event recorded on the stream after every launched level while a
-    // communicator is attached; wait_stream restarts its deadline whenever one completes
+    // communicator is attached; wait_stream restarts its deadline whenever one completes.  At most
+    // kProgRing marks are outstanding: when all are, the mark whose removal merges the two shortest
+    // neighbouring intervals (in levels) is re-recorded at the newest level, so the outstanding marks
+    // stay spread over everything queued -- the gaps between them grow evenly with the queue, never
+    // one gap from mark kProgRing to the end (a long healthy flush keeps showing progress)
     static constexpr int kProgRing = 32;
     hipEvent_t prog_ev[kProgRing] = {};
-    uint64_t prog_rec = 0, prog_done = 0;
+    struct ProgMark {
+        int ev;        // index into prog_ev
+        uint64_t seq;  // levels launched when it was recorded
+    };
+    std::vector<ProgMark> prog_q;  // outstanding marks, oldest first
+    uint64_t prog_seq = 0;
     void mark_progress();
+    // drops the completed marks at the front of prog_q; true if any completed
+    bool drain_progress();
     // *flags (one byte per entry) = min over the ranks, in place (one all-reduce; a no-op without a
     // communicator).  The engine's dead-node agreement.
     int allreduce_min_u8(uint8_t* flags, size_t n);

@@ -1,4 +1,4 @@
-// kernels.h -- host launchers for the gfx950 kernels (pbs_kernels.hip, radix_kernels.hip).
+// kernels.h -- host launchers for the gfx950 kernels (pbs_kernels.hip, ks_mfma.hip, br_wide.hip, br_qy.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -51,22 +51,12 @@ hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const Pbs
                                     int n, hipStream_t s);
 // dst_i = sum_t coef * src + cst, no bootstrap (linear radix ops)
 hipError_t launch_lincomb(const PbsDesc* desc, int count, hipStream_t s);
-hipError_t launch_blind_rotate_quad(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
-                                    const uint64_t* luts, const double2* bsk_quad, const double2* tw, const double2* ps,
-                                    const double2* zq, const double2* mono, int grouping, uint64_t* out, int count,
-                                    int n, hipStream_t s);
-hipError_t launch_bsk_to_quad(const double2* bsk, int npoly, double2* out, hipStream_t s);
-// classic throughput kernel with the round-4 layouts (br_qx.hip): no DPP transposes; bsk_qx from
-// launch_bsk_to_qx, zfull = the zeta table zeta(s, b) at [2^s + b] (context.cpp zeta_table)
-hipError_t launch_blind_rotate_qx(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
-                                  const uint64_t* luts, const double2* bsk_qx, const double2* tw, const double2* ps,
-                                  const double2* zfull, const double2* mono, uint64_t* out, int count, int n,
-                                  hipStream_t s);
-hipError_t launch_bsk_to_qx(const double2* bsk, int npoly, double2* out, hipStream_t s);
-// the same with two workgroup barriers per CMUX (br_qy.hip): same key layout (bsk_qx) and tables;
-// grouping 2 = the multi-bit blind rotation on the multi-bit key in the same E layout
+// throughput kernel (br_qy.hip): 4 waves per ciphertext, two workgroup barriers per CMUX; bsk_e =
+// the Fourier BSK in the E layout (launch_bsk_to_e), zfull = the zeta table zeta(s, b) at [2^s + b]
+// (context.cpp zeta_table); grouping 2 = the multi-bit blind rotation on the multi-bit key
+hipError_t launch_bsk_to_e(const double2* bsk, int npoly, double2* out, hipStream_t s);
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
-                                  const uint64_t* luts, const double2* bsk_qx, const double2* tw, const double2* ps,
+                                  const uint64_t* luts, const double2* bsk_e, const double2* tw, const double2* ps,
                                   const double2* zfull, const double2* mono, int grouping, uint64_t* out, int count,
                                   int n, hipStream_t s);
 

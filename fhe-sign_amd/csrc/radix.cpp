@@ -390,7 +390,12 @@ void Engine::flush() {
                 }
             }
         }
-        if (ctx_->comm) engine_check(ctx_->allreduce_min_u8(dead.data(), N0) == FHE_OK, "dead-node agreement");
+        // Only a real multi-rank communicator needs the agreement (the collective is rank-uniform: every
+        // rank takes this branch or none does); at world size 1 it would only drain the stream.
+        if (ctx_->comm && ctx_->nranks > 1) {
+            const int rc = ctx_->allreduce_min_u8(dead.data(), N0);
+            if (rc != FHE_OK) throw EngineError(rc, std::string("dead-node agreement: ") + last_error());
+        }
         for (size_t k = N0; k-- > 0;)
             if (dead[k]) pending_[k].hold.clear();
         size_t live = 0;
@@ -492,7 +497,8 @@ void Engine::flush() {
             // own slice (every slice when ranks are emulated on one GPU)
             for (int r = 0; r < W; ++r)
                 if (!ctx_->comm || r == ctx_->rank) pbs(r * chunk, std::min(G, (r + 1) * chunk));
-            engine_check(ctx_->allgather(ctx_->d_gather, chunk * kBigCt) == FHE_OK, "all-gather");
+            if (const int rc = ctx_->allgather(ctx_->d_gather, chunk * kBigCt); rc != FHE_OK)
+                throw EngineError(rc, std::string("all-gather: ") + last_error());
             hip_check(launch_scatter_blocks(ctx_->d_gather, reinterpret_cast<uint64_t* const*>(ld + G), (int)G,
                                             ctx_->stream),
                       "scatter");

@@ -212,8 +212,8 @@ class Context:
         check(load().fhe_ctx_sync(self._h))
 
     def set_br_kernel(self, kind: int) -> None:
-        """4 = br_qy.hip (classic default), 3 = br_qx.hip, 1 = br_quad.hip (always used for multi-bit); 0 and 2, the
-        retired 2-wave and pair kernels, are refused (FHE_ERR_INVALID)."""
+        """4 = br_qy.hip, the throughput kernel (classic and multi-bit); the retired kernels 0 (2-wave), 1 (quad),
+        2 (pair) and 3 (qx) are refused (FHE_ERR_INVALID)."""
         check(load().fhe_ctx_set_br_kernel(self._h, int(kind)))
 
     def set_ks_kernel(self, kind: int) -> None:

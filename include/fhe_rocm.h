@@ -151,13 +151,12 @@ int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
-/* Throughput blind-rotate kernel for levels above the threshold, 4 waves per ciphertext:
- * FHE_BR_QY (default; classic parameters: the round-4 layouts without DPP transposes and with two
- * workgroup barriers per CMUX, br_qy.hip), FHE_BR_QX (the same layouts with four barriers, br_qx.hip) or
- * FHE_BR_QUAD (br_quad.hip; always used for the multi-bit blind rotation).  The retired kernels --
- * FHE_BR_NARROW (2 waves per ciphertext, round 1) and FHE_BR_PAIR (two ciphertexts per 4-wave
- * workgroup, rounds 2-3) -- are refused with FHE_ERR_INVALID.  All blind-rotate kernels produce
- * identical bits. */
+/* Throughput blind-rotate kernel for levels above the threshold, 4 waves per ciphertext: FHE_BR_QY
+ * (br_qy.hip, two workgroup barriers per CMUX; classic and multi-bit parameters) is the only one.
+ * The retired kernels -- FHE_BR_NARROW (round 1), FHE_BR_PAIR (rounds 2-3), FHE_BR_QUAD (rounds 1-4,
+ * the multi-bit kernel until r4) and FHE_BR_QX (round 4, four barriers per CMUX; sources in
+ * tools/retired/) -- are refused with FHE_ERR_INVALID.  Every blind-rotate kernel that ever ran here
+ * produced identical bits. */
 #define FHE_BR_NARROW 0
 #define FHE_BR_QUAD 1
 #define FHE_BR_PAIR 2
@@ -311,6 +310,10 @@ int fhe_schedule_levels(const int32_t* dep_offsets, const int32_t* deps, size_t 
  * (fhe_ctx_set_fanout) and each rank's slice is at most one round. */
 int fhe_schedule_levels_ranks(const int32_t* dep_offsets, const int32_t* deps, size_t n, int mode, int ranks,
                               int32_t* level_of, int32_t* nlevels);
+/* Host-only check of the progress marks behind the bounded waits (fhe_ctx_sync with a communicator
+ * attached): after `levels` launched levels with none completed, the largest number of levels
+ * between consecutive outstanding marks (at most 32 are kept; their gaps stay even). */
+int fhe_progress_marks_probe(uint32_t levels, uint32_t* max_gap);
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */

@@ -198,3 +198,51 @@ def test_fanout_hang_exits_nonzero():
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert p.returncode == 3, (p.returncode, p.stderr)
     assert '"value": 1.0' in p.stdout and "status 3" in p.stderr
+
+
+def _bare_env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env["HIP_VISIBLE_DEVICES"] = ""  # the launcher makes no GPU call; neither does a dry rank
+    return env
+
+
+def test_bare_gpus2_self_launches_and_relays_rank0_line():
+    """`python bench.py --gpus 2` from a bare shell (no RANK/WORLD_SIZE): bench.py starts its own two
+    ranks as child processes (never exec), they meet on gloo, and the launcher relays rank 0's one
+    JSON line (n_gpus 2, max-over-ranks time) and exits 0."""
+    import json
+    import subprocess
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--dry-run"],
+                       capture_output=True, text=True, timeout=180, env=_bare_env())
+    assert p.returncode == 0, p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["steps"] == 3
+    # max over ranks: rank 1 sleeps 0.1 s, so the whole-job step time reflects it
+    assert rec["ms_per_step"] >= 0.1 / 3 * 1e3
+    assert rec["pid"] != os.getpid()
+
+
+def test_bare_launch_exits_nonzero_when_a_rank_fails():
+    """A failing rank (status 5) makes the launcher exit non-zero; its peer, stuck in the barrier,
+    is killed after the grace period instead of hanging the run."""
+    import subprocess
+    import time
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--dry-fail-rank", "1"], capture_output=True, text=True, timeout=240, env=_bare_env())
+    assert p.returncode == 5, (p.returncode, p.stderr)
+    assert "exited with status 5" in p.stderr
+    assert time.monotonic() - t0 < 200
+
+
+def test_bare_launch_deadline_kills_every_rank():
+    """The launcher's deadline kills ranks that never finish and returns 124."""
+    import subprocess
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--dry-fail-rank", "7", "--launch-deadline", "0.5"],
+                       capture_output=True, text=True, timeout=120, env=_bare_env())
+    assert p.returncode == 124, (p.returncode, p.stderr)
+    assert "deadline" in p.stderr

@@ -256,12 +256,34 @@ def test_config5_emulated_ranks_production_split(keys, config5_ref, ranks):
     ctx.close()
 
 
+def test_rccl_world1_long_flush_keeps_progress(keys):
+    """one flush of far more than 32 levels whose tail after the 32nd level takes longer
+    than the deadline -- the 256-bit division by an encrypted divisor, ~870 dependent levels, ~2 s --
+    completes under a 400 ms no-progress deadline: the outstanding progress marks are spread over
+    the whole queue (fhe_ctx::mark_progress), not stuck at the 32nd level."""
+    ck, sk = keys
+    ctx = Context(0)
+    ctx.set_server_key(sk)
+    ctx.attach_comm(comm_unique_id(), 1, 0)
+    set_server_key(ctx)
+    a, d = (1 << 255) + 0x1234_5678_9ABC_DEF0_1357, (1 << 127) + 0xFEDC_BA98_7654_3210
+    A, D = FheUint256.try_encrypt(a, ck), FheUint256.try_encrypt(d, ck)
+    ctx.sync()
+    ctx.set_comm_timeout(400)
+    q, r = A.div_rem(D)
+    ctx.sync()
+    assert load_comm_attached(ctx)
+    assert (q.decrypt(ck), r.decrypt(ck)) == (a // d, a % d)
+    set_server_key(None)
+    ctx.close()
+
+
 def test_rccl_world1_sync_is_bounded(keys):
     """While a communicator is attached, fhe_ctx_sync waits through the bounded path
     (fhe_ctx::wait_stream), whose deadline counts time WITHOUT PROGRESS: (a) a compat 256-bit mul
     (~0.6 s over 151 levels, no level above ~0.25 s) completes under a 400 ms deadline, since every
-    completed level restarts it, and its dead-node agreement (a byte-wise min all-reduce) runs at
-    every flush; (b) one raw 8192-PBS launch (one kernel, ~60 ms, no level marks) under a 2 ms
+    completed level restarts it (at world size 1 no dead-node agreement runs: that collective is for
+    nranks > 1 only); (b) one raw 8192-PBS launch (one kernel, ~60 ms, no level marks) under a 2 ms
     deadline returns FHE_ERR_TIMEOUT with the communicator aborted and detached, and the context
     keeps computing afterwards."""
     from fhe_sign._lib import FHE_ERR_TIMEOUT, FheError

@@ -33,11 +33,8 @@ def descriptors(src, tmp_path, flags=()):
 @pytest.mark.parametrize("src,flags,kernel,lds_per_cu_ok,max_regs,max_scratch", [
     ("br_wide.hip", (), "k_blind_rotate_wideILi1", 1, 256, 0),  # one 8-wave workgroup per CU (classic)
     ("br_wide.hip", (), "k_blind_rotate_wideILi2", 1, 256, 0),  # the same, multi-bit
-    ("br_quad.hip", (), "k_blind_rotate_quadILi1", 3, 168, 0),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
-    ("br_quad.hip", (), "k_blind_rotate_quadILi2", 2, 256, 0),  # multi-bit: 2 per CU, 2 waves/SIMD, deeper BSK ring
-    ("br_qx.hip", (), "k_blind_rotate_qx", 3, 168, 0),  # classic, round-4 layouts with four barriers per CMUX
-    ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qyILi1", 3, 168, 0),
-    ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qyILi2", 2, 256, 0),  # classic default: two barriers per CMUX, 3 waves/SIMD
+    ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qyILi1", 3, 168, 0),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
+    ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qyILi2", 2, 256, 0),  # multi-bit: 2 per CU, 2 waves/SIMD
     ("ks_mfma.hip", (), "k_ks_mfmaILi2", 3, 168, 0),  # keyswitch, latency levels: 3 workgroups per CU
     ("ks_mfma.hip", (), "k_ks_mfmaILi4", 2, 512, 0),  # keyswitch, large batches: one wave per SIMD, no spill
 ])

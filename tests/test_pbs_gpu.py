@@ -111,26 +111,27 @@ def test_pbs_empty_batch(env):
     assert out.shape == (0, 2049)
 
 
-def test_wide_and_quad_kernels_bit_identical(env):
+def test_latency_and_throughput_kernels_bit_identical(env):
     """The latency kernel (br_wide.hip, 8 waves per ciphertext) and the throughput kernel (4 waves,
-    br_quad.hip) implement the same arithmetic: identical output words, equal to the oracle.  37
-    ciphertexts: a ragged batch with every LUT.  The retired 2-wave kernel is refused loudly."""
+    br_qy.hip) implement the same arithmetic: identical output words, equal to the oracle.  37
+    ciphertexts: a ragged batch with every LUT.  The retired kernels are refused loudly."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = [ctx.lut(t) for t in tables]
     r = ok.rng(777)
     cts = np.stack([ok.encrypt(r, i % 16) for i in range(37)])
     lut_ids = np.array([ids[i % len(ids)] for i in range(37)], np.uint32)
-    with pytest.raises(Exception, match="retired"):
-        ctx.set_br_kernel(0)
+    for retired in (0, 1, 2, 3):  # NARROW (r1), QUAD (r3), PAIR (r2), QX (r4)
+        with pytest.raises(Exception, match="retired"):
+            ctx.set_br_kernel(retired)
     try:
         ctx.set_wide_threshold(0)
-        quad = ctx.pbs(cts, lut_ids)
+        thr = ctx.pbs(cts, lut_ids)
         ctx.set_wide_threshold(1 << 30)
         wide = ctx.pbs(cts, lut_ids)
     finally:
         ctx.set_wide_threshold(256)
-    assert np.array_equal(quad, wide)
+    assert np.array_equal(thr, wide)
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(wide[:6], ref)
 
@@ -166,11 +167,9 @@ def test_zero_and_sparse_masks_both_kernels(env):
         assert ok.decrypt(ref[m]) == tables[lut_of[m]][m]
 
 
-@pytest.mark.parametrize("kind", [3, 4, 1])  # FHE_BR_QX (br_qx.hip), FHE_BR_QY (br_qy.hip), FHE_BR_QUAD (br_quad.hip)
-def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
-    """The throughput kernels at ragged batches (1, 2, 3, 37, 259) with every LUT give the latency
-    kernel's and the oracle's words (multi-bit parameters always run br_quad.hip); the retired
-    blind-rotate kernels (0: round-1 2-wave, 2: the pair kernel) are refused."""
+def test_throughput_kernel_ragged_batches(env):
+    """The throughput kernel (br_qy.hip) at ragged batches (1, 2, 3, 37, 259) with every LUT gives
+    the latency kernel's and the oracle's words; FHE_BR_QY is accepted, unknown kinds are refused."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = [ctx.lut(t) for t in tables]
@@ -180,25 +179,24 @@ def test_throughput_kernels_ragged_batches_and_retired_kernels(env, kind):
     try:
         ctx.set_wide_threshold(1 << 30)
         wide = ctx.pbs(cts, lut_ids)
-        ctx.set_br_kernel(kind)
+        ctx.set_br_kernel(4)
         ctx.set_wide_threshold(0)
         thr = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 2, 3, 37, 259)}
     finally:
         ctx.set_wide_threshold(256)
-        ctx.set_br_kernel(4)
     for c, out in thr.items():
         bad = [i for i in range(c) if not np.array_equal(out[i], wide[i])]
-        assert not bad, f"kernel {kind}, batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
+        assert not bad, f"batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(thr[37][:6], ref)
-    for bad_kind in (0, 2, 5):
+    for bad_kind in (5, -1):
         with pytest.raises(Exception):
             ctx.set_br_kernel(bad_kind)
 
 
-def test_throughput_kernels_identical_at_full_batch(env):
-    """br_qx.hip, br_qy.hip and br_quad.hip on the same 4096 distinct encryptions (16 rounds of 256
-    CUs): every output word identical, a seeded sample of 8 equal to the oracle."""
+def test_throughput_kernel_full_batch(env):
+    """br_qy.hip and the latency kernel on the same 4096 distinct encryptions (16 rounds of 256 CUs):
+    every output word identical, a seeded sample of 8 equal to the oracle."""
     _, _, ok, ctx = env
     tables = _luts()
     ids = np.array([ctx.lut(t) for t in tables], np.uint32)
@@ -206,23 +204,19 @@ def test_throughput_kernels_identical_at_full_batch(env):
     r = ok.rng(31337)
     cts = np.stack([ok.encrypt(r, i % 16) for i in range(B)])
     lut_of = np.arange(B) % len(tables)
+    qy = ctx.pbs(cts, ids[lut_of])
     try:
-        ctx.set_br_kernel(1)
-        quad = ctx.pbs(cts, ids[lut_of])
-        ctx.set_br_kernel(3)
-        qx = ctx.pbs(cts, ids[lut_of])
-        ctx.set_br_kernel(4)
-        qy = ctx.pbs(cts, ids[lut_of])
+        ctx.set_wide_threshold(1 << 30)
+        wide = ctx.pbs(cts, ids[lut_of])
     finally:
-        ctx.set_br_kernel(4)
-    for name, other in (("quad", quad), ("qy", qy)):
-        bad = np.flatnonzero((other != qx).any(axis=1))
-        assert bad.size == 0, f"{bad.size} ciphertexts differ between qx and {name}, first {bad[:5]}"
+        ctx.set_wide_threshold(256)
+    bad = np.flatnonzero((wide != qy).any(axis=1))
+    assert bad.size == 0, f"{bad.size} ciphertexts differ between qy and the latency kernel, first {bad[:5]}"
     pick = np.array([0, 1, 513, 1024, 2047, 2048, 3333, 4095])
     ref = ok.pbs_batch(np.ascontiguousarray(cts[pick]), np.stack([ok.make_lut(t) for t in tables]),
                        lut_of[pick].astype(np.uint32))
     for k, i in enumerate(pick):
-        assert np.array_equal(qx[i], ref[k]), f"ciphertext {i} differs from the oracle"
+        assert np.array_equal(qy[i], ref[k]), f"ciphertext {i} differs from the oracle"
 
 
 def test_keyswitch_kernels_identical(env):
@@ -285,10 +279,9 @@ def test_noise_budget_at_radix_limit(env):
 
 
 def test_multibit_qy_kernel_bit_identical():
-    """br_qy.hip's multi-bit instance (FHE_MB_QY=1: the key bundle per point of phase E, built during
-    the forward transform) gives the multi-bit latency kernel's and the oracle's words, at ragged
-    batches and at 4096 distinct encryptions (16 rounds of 256 CUs)."""
-    import os
+    """br_qy.hip's multi-bit instance (the key bundle per point of phase E, built during the forward
+    transform) gives the multi-bit latency kernel's and the oracle's words, at ragged batches and at
+    4096 distinct encryptions (16 rounds of 256 CUs)."""
     mb = multi_bit_params()
     ck, sk = generate_keys(mb, seed=SEED)
     ok = oracle.OracleKeys(SEED, oracle.multibit_params())
@@ -297,29 +290,22 @@ def test_multibit_qy_kernel_bit_identical():
     B = 4096
     cts = np.stack([ok.encrypt(r, (7 * i + 2) % 16) for i in range(B)])
     lut_of = np.arange(B) % len(tables)
-    os.environ["FHE_MB_QY"] = "1"
-    try:
-        ctx = Context(0)
-    finally:
-        del os.environ["FHE_MB_QY"]
+    ctx = Context(0)
     try:
         ctx.set_server_key(sk)
         ids = np.array([ctx.lut(t) for t in tables], np.uint32)
         ctx.set_wide_threshold(1 << 30)
-        wide = ctx.pbs(cts[:259], ids[lut_of[:259]])
+        wide = ctx.pbs(cts, ids[lut_of])
         ctx.set_wide_threshold(0)
-        ctx.set_br_kernel(4)
         got = {c: ctx.pbs(cts[:c], ids[lut_of[:c]]) for c in (1, 37, 259)}
         full = ctx.pbs(cts, ids[lut_of])
-        ctx.set_br_kernel(1)
-        quad = ctx.pbs(cts, ids[lut_of])
     finally:
         ctx.close()
     for c, out in got.items():
         bad = np.flatnonzero((out != wide[:c]).any(axis=1))
         assert bad.size == 0, f"batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
-    bad = np.flatnonzero((full != quad).any(axis=1))
-    assert bad.size == 0, f"{bad.size} ciphertexts differ between qy<2> and quad<2>, first {bad[:5]}"
+    bad = np.flatnonzero((full != wide).any(axis=1))
+    assert bad.size == 0, f"{bad.size} ciphertexts differ between qy<2> and the latency kernel, first {bad[:5]}"
     pick = np.array([0, 1, 777, 2048, 4095])
     ref = ok.pbs_batch(np.ascontiguousarray(cts[pick]), np.stack([ok.make_lut(t) for t in tables]),
                        lut_of[pick].astype(np.uint32))

@@ -136,3 +136,15 @@ def test_invalid_graph_rejected():
     P = C.POINTER(C.c_int32)
     assert _lib.load().fhe_schedule_levels(off.ctypes.data_as(P), bad.ctypes.data_as(P), 1, 0,
                                            level.ctypes.data_as(P), C.byref(nl)) != 0
+
+
+def test_progress_marks_stay_spread():
+    """with up to 32 progress marks outstanding, a flush of L levels that the
+    GPU has not started keeps marks spread over the whole queue -- the largest gap between
+    consecutive outstanding marks stays within ~2x the mean (L / 32), so a long healthy flush shows
+    progress at least every ~L/16 levels instead of going silent after its 32nd level."""
+    import ctypes
+    for levels, bound in ((10, 1), (32, 1), (33, 2), (149, 10), (869, 60), (5000, 330)):
+        gap = ctypes.c_uint32()
+        assert _lib.load().fhe_progress_marks_probe(levels, ctypes.byref(gap)) == 0
+        assert 1 <= gap.value <= bound, (levels, gap.value)
