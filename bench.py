@@ -144,7 +144,7 @@ def self_launch(n: int, argv: list, deadline_s: float) -> int:
     return status
 
 
-def dry_run(a, dist, rank, world):
+def dry_run(a, dist, rank, world, out):
     """The N > 1 control plane without a GPU: barrier + sleep + barrier, max over ranks, one line."""
     if rank == a.dry_fail_rank:
         sys.stderr.write(f"bench dry run: rank {rank} failing on request\n")
@@ -157,7 +157,7 @@ def dry_run(a, dist, rank, world):
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": world * a.steps / dt, "unit": "steps/s (dry run)",
                           "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
-                          "dry_run": True, "pid": os.getpid()}), flush=True)
+                          "dry_run": True, "pid": os.getpid()}), file=out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -620,9 +620,14 @@ def main():
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # bare `python bench.py --gpus N`: be the launcher (no GPU call in this process)
         sys.exit(self_launch(a.gpus, sys.argv[1:], a.launch_deadline))
+    # stdout carries exactly the one JSON line: libraries that print banners there (RCCL prints its
+    # version block at communicator init) are sent to stderr instead
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
     dist, rank, world, local = dist_setup(a.gpus)
     if a.dry_run:
-        dry_run(a, dist, rank, world)
+        dry_run(a, dist, rank, world, out)
         return
 
     device = local
@@ -716,7 +721,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_seconds, op_levels)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=out, flush=True)
     if fan_hung:  # a collective of the abandoned legs may still hold the stream: no orderly teardown
         abandon("fan-out legs hung")
     ctx.close()

@@ -180,6 +180,31 @@ int fhe_ctx::register_lut(const uint32_t* table, uint32_t* id) {
     return FHE_OK;
 }
 
+int fhe_ctx::register_lut_half(const int32_t* half, uint32_t* id) {
+    const uint32_t mods = p.msg_carry();
+    // keyed apart from the integer tables: one more entry than they have
+    std::vector<uint32_t> key(1, 0xFFFFFFFFu);
+    for (uint32_t i = 0; i < mods; ++i) key.push_back((uint32_t)half[i]);
+    auto it = lut_ids.find(key);
+    if (it != lut_ids.end()) {
+        *id = it->second;
+        return FHE_OK;
+    }
+    const uint32_t box = kPolySize / mods, hb = box / 2;
+    const uint64_t hd = p.delta() / 2;
+    std::vector<uint64_t> tmp(kPolySize), poly(kPolySize);
+    for (uint32_t i = 0; i < mods; ++i)
+        for (uint32_t t = 0; t < box; ++t) tmp[i * box + t] = (uint64_t)(int64_t)half[i] * hd;
+    for (uint32_t t = 0; t < hb; ++t) tmp[t] = 0ull - tmp[t];  // as make_lut_poly: half-box rotation
+    for (uint32_t j = 0; j < kPolySize; ++j) poly[j] = tmp[(j + hb) % kPolySize];
+    const uint32_t nid = (uint32_t)lut_ids.size();
+    h_luts.insert(h_luts.end(), poly.begin(), poly.end());
+    lut_ids.emplace(std::move(key), nid);
+    luts_dirty = true;
+    *id = nid;
+    return FHE_OK;
+}
+
 int fhe_ctx::sync_luts() {
     if (!luts_dirty) return FHE_OK;
     const size_t nl = h_luts.size() / kPolySize;

@@ -136,6 +136,8 @@ struct fhe_ctx {
     int ensure_stage(size_t count);
     int sync_luts();
     int register_lut(const uint32_t* table, uint32_t* id);
+    // LUT with outputs in half message steps (raw PbsItems): f(v) = half[v] * delta / 2, v < 16
+    int register_lut_half(const int32_t* half, uint32_t* id);
     // KS + BR(+SE) over device arrays, async on `stream`
     int pbs_device(const uint64_t* d_in, size_t count, const uint32_t* d_lut, uint64_t* d_out);
     // blind rotate (+SE) of `count` modulus-switched inputs in d_ms, kernel chosen by batch size

@@ -15,6 +15,14 @@ struct PbsDesc {
     uint64_t cst;  // plaintext constant added to the body
     uint64_t* dst;
 };
+// A wider linear combination (nterms > kMaxTerms, at most kMaxWideTerms: the compat mul's carry-count
+// chain sums up to ~20 blocks in one lookup input): src[0] then points to nterms TermExt entries in
+// device memory (staged by Engine::flush after the level descriptors).
+constexpr int kMaxWideTerms = 32;
+struct TermExt {
+    const uint64_t* src;
+    int64_t coef;
+};
 
 // Keyswitch input coefficient j (2048 = body) of ciphertext ct: a contiguous batch of big LWE
 // or the linear combination a descriptor describes.
@@ -24,6 +32,11 @@ __device__ __forceinline__ uint64_t ks_input(const uint64_t* __restrict__ in, co
     if (!DESC) return in[(size_t)ct * 2049 + j];
     const PbsDesc& d = desc[ct];
     uint64_t a = (j == 2048) ? d.cst : 0ull;
+    if (d.nterms > (uint32_t)kMaxTerms) {
+        const TermExt* x = reinterpret_cast<const TermExt*>(d.src[0]);
+        for (uint32_t t = 0; t < d.nterms; ++t) a += (uint64_t)x[t].coef * x[t].src[j];
+        return a;
+    }
     for (uint32_t t = 0; t < d.nterms; ++t) a += (uint64_t)(int64_t)d.coef[t] * d.src[t][j];
     return a;
 }

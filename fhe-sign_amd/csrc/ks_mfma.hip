@@ -75,11 +75,21 @@ __global__ __launch_bounds__(256) void k_ks_digits(const uint64_t* __restrict__ 
         const PbsDesc& d = desc[ct];
 #pragma unroll
         for (int it = 0; it < 8; ++it) av[it] = 0ull;
+        if (d.nterms <= (uint32_t)kMaxTerms) {  // uniform
 #pragma unroll
-        for (int tm = 0; tm < kMaxTerms; ++tm) {
-            if (tm < (int)d.nterms) {  // uniform
-                const uint64_t* src = d.src[tm];
-                const uint64_t c = (uint64_t)(int64_t)d.coef[tm];
+            for (int tm = 0; tm < kMaxTerms; ++tm) {
+                if (tm < (int)d.nterms) {  // uniform
+                    const uint64_t* src = d.src[tm];
+                    const uint64_t c = (uint64_t)(int64_t)d.coef[tm];
+#pragma unroll
+                    for (int it = 0; it < 8; ++it) av[it] += c * src[threadIdx.x + 256 * it];
+                }
+            }
+        } else {  // wide combination (kernels.h TermExt)
+            const TermExt* x = reinterpret_cast<const TermExt*>(d.src[0]);
+            for (uint32_t tm = 0; tm < d.nterms; ++tm) {
+                const uint64_t* src = x[tm].src;
+                const uint64_t c = (uint64_t)x[tm].coef;
 #pragma unroll
                 for (int it = 0; it < 8; ++it) av[it] += c * src[threadIdx.x + 256 * it];
             }

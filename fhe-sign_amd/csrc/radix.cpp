@@ -169,6 +169,27 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     std::vector<int64_t> csts(items.size());
     for (size_t i = 0; i < items.size(); ++i) {
         PbsItem& it = items[i];
+        if (it.raw) {  // caller-guaranteed range (radix.h): no folding, no degree check
+            engine_check(it.half_table.size() == mc, "raw LUT table size");
+            int64_t cst = it.cst;
+            uint32_t noise = 0;
+            for (const Term& t : it.terms) {
+                if (t.coef == 0) continue;
+                if (t.b.trivial())
+                    cst += (int64_t)t.coef * t.b.value;
+                else {
+                    live[i].push_back(t);
+                    noise += (uint32_t)(t.coef * t.coef) * t.b.noise;
+                }
+            }
+            engine_check(noise <= kMaxNoise, "raw PBS input noise above the budget");
+            engine_check(!live[i].empty(), "raw PBS item without an encrypted term");
+            out[i].degree = it.raw_degree;
+            out[i].noise = 1;
+            csts[i] = cst;
+            gpu.push_back(i);
+            continue;
+        }
         engine_check(it.table.size() == mc, "LUT table size");
         int64_t cst = it.cst;
         uint32_t noise = 0;
@@ -211,9 +232,14 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
 
     // register LUTs, allocate destinations, record pending nodes
     const uint64_t delta = p.delta();
+    std::vector<TermExt> terms;
     for (size_t i : gpu) {
         uint32_t lut = 0;
-        engine_check(ctx_->register_lut(items[i].table.data(), &lut) == FHE_OK, "LUT registration");
+        const bool raw = items[i].raw;
+        if (raw)
+            engine_check(ctx_->register_lut_half(items[i].half_table.data(), &lut) == FHE_OK, "LUT registration");
+        else
+            engine_check(ctx_->register_lut(items[i].table.data(), &lut) == FHE_OK, "LUT registration");
         out[i].slot = pool_->alloc();
         Pending n;
         PbsDesc& d = n.d;
@@ -221,16 +247,16 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         n.hold.push_back(out[i].slot);
         // flatten lazy terms into their slot blocks (merging repeats)
         int64_t dcst = csts[i];
-        uint32_t nt = 0;
+        terms.clear();
+        const size_t cap = raw ? (size_t)kMaxWideTerms : (size_t)kMaxTerms;
         auto put = [&](const Block& b, int32_t coef) {
-            for (uint32_t u = 0; u < nt; ++u)
-                if (d.src[u] == b.ptr()) {
-                    d.coef[u] += coef;
+            for (TermExt& u : terms)
+                if (u.src == b.ptr()) {
+                    u.coef += coef;
                     return;
                 }
-            engine_check(nt < (uint32_t)kMaxTerms, "too many terms in one PBS input");
-            d.src[nt] = b.ptr();
-            d.coef[nt++] = coef;
+            engine_check(terms.size() < cap, "too many terms in one PBS input");
+            terms.push_back({b.ptr(), coef});
             n.hold.push_back(b.slot);
             if (b.slot->node >= 0) n.deps.push_back((int32_t)b.slot->node);
         };
@@ -242,19 +268,28 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
             dcst += (int64_t)t.coef * t.b.lin_cst;
             for (const Term& u : *t.b.lin) put(u.b, t.coef * u.coef);
         }
+        const uint32_t nt = (uint32_t)terms.size();
+        if (nt <= (uint32_t)kMaxTerms) {
+            for (uint32_t u = 0; u < nt; ++u) {
+                d.src[u] = terms[u].src;
+                d.coef[u] = (int32_t)terms[u].coef;
+            }
+        } else {
+            n.ext = terms;  // d.src[0] is set to their staged copy at flush
+        }
         d.nterms = nt;
         d.lut = lut;
-        d.cst = (uint64_t)dcst * delta;
+        d.cst = (uint64_t)dcst * delta + (uint64_t)((int64_t)items[i].half_cst * (int64_t)(delta / 2));
         if (gstats_) {
-            std::vector<std::pair<const uint64_t*, int32_t>> tk;
-            for (uint32_t u = 0; u < nt; ++u) tk.push_back({d.src[u], d.coef[u]});
+            std::vector<std::pair<const uint64_t*, int64_t>> tk;
+            for (uint32_t u = 0; u < nt; ++u) tk.push_back({terms[u].src, terms[u].coef});
             std::sort(tk.begin(), tk.end());
             std::string key(reinterpret_cast<const char*>(tk.data()), tk.size() * sizeof(tk[0]));
             key.append(reinterpret_cast<const char*>(&dcst), sizeof dcst);
             in_key_.push_back(std::move(key));
             bool okr;
-            const uint64_t rr = reachable(live[i], csts[i], &okr);
-            in_deg_.push_back((uint8_t)(63 - __builtin_clzll(rr | 1)));
+            const uint64_t rr = raw ? 0xFFFFull : reachable(live[i], csts[i], &okr);
+            in_deg_.push_back((uint8_t)(raw ? 16 : 63 - __builtin_clzll(rr | 1)));
         }
         d.dst = out[i].slot->p;
         out[i].slot->node = (int64_t)pending_.size();
@@ -451,6 +486,11 @@ void Engine::flush() {
         maxchunk = std::max(maxchunk, chunk);
         if (split) maxgather = std::max(maxgather, chunk * W);
     }
+    // wide combinations' term tables, staged after the level descriptors (PbsDesc-sized units)
+    size_t next = 0;
+    for (const Pending& n : pending_) next += n.ext.size();
+    const size_t ext_at = ndesc;
+    ndesc += (next * sizeof(TermExt) + sizeof(PbsDesc) - 1) / sizeof(PbsDesc);
     if (maxgather) engine_check(ctx_->ensure_gather(maxgather) == FHE_OK, "gather workspace");
     engine_check(ctx_->ensure_ms(maxchunk) == FHE_OK, "workspace");
     engine_check(ctx_->sync_luts() == FHE_OK, "LUT upload");
@@ -458,13 +498,22 @@ void Engine::flush() {
     PbsDesc* h = stage_desc(ndesc, &dev);
     std::vector<size_t> at(lv.size());
     size_t o = 0;
+    TermExt* h_ext = reinterpret_cast<TermExt*>(h + ext_at);
+    const TermExt* d_ext = reinterpret_cast<const TermExt*>(dev + ext_at);
+    size_t eo = 0;
     for (size_t li = 0; li < lv.size(); ++li) {
         const size_t G = lv[li].size();
         const bool split = W > 1 && G >= ctx_->fanout_min;
         at[li] = o;
         uint64_t** h_scat = reinterpret_cast<uint64_t**>(h + o + G);
         for (size_t g = 0; g < G; ++g) {
-            PbsDesc d = pending_[lv[li][g]].d;
+            const Pending& pn = pending_[lv[li][g]];
+            PbsDesc d = pn.d;
+            if (!pn.ext.empty()) {
+                std::copy(pn.ext.begin(), pn.ext.end(), h_ext + eo);
+                d.src[0] = reinterpret_cast<const uint64_t*>(d_ext + eo);
+                eo += pn.ext.size();
+            }
             if (split) {
                 // fanned-out levels bootstrap into the gather buffer (segment = owning rank), then scatter
                 h_scat[g] = d.dst;

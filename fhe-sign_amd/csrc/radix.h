@@ -89,6 +89,16 @@ struct PbsItem {
     std::vector<Term> terms;
     uint32_t cst = 0;             // plaintext constant (units of one message step)
     std::vector<uint32_t> table;  // LUT over [0, msg*carry)
+    // Raw items (the compat mul's carry-count chain, csrc/biguint.cpp): the caller guarantees the
+    // input's actual value lies in [-16, 16) (message steps; [-16, 0) reaches the negacyclic half of
+    // the blind rotation, where the output is -f(v + 16)).  No folding and no degree check; the LUT
+    // is `half_table` (16 outputs f(0..15) in units of HALF a message step) and `half_cst` (half steps,
+    // signed) is added to `cst`.  Output block: degree `raw_degree`, fresh noise.  Up to
+    // kMaxWideTerms input terms (ordinary items: kMaxTerms).
+    bool raw = false;
+    std::vector<int32_t> half_table;
+    int32_t half_cst = 0;
+    uint32_t raw_degree = 3;
 };
 
 // Executes PBS items on a context as a deferred dependency graph.  run() does the host-side
@@ -159,6 +169,7 @@ private:
         PbsDesc d;
         std::vector<std::shared_ptr<Slot>> hold;  // [0] output, then inputs: alive until launched
         std::vector<int32_t> deps;                // pending producers of the inputs
+        std::vector<TermExt> ext;                 // terms of a wide combination (d.nterms > kMaxTerms)
     };
     std::vector<Pending> pending_;
     size_t pending_dependent_ = 0;  // pending nodes with at least one pending producer

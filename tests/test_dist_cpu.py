@@ -216,8 +216,8 @@ def test_bare_gpus2_self_launches_and_relays_rank0_line():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--dry-run"],
                        capture_output=True, text=True, timeout=180, env=_bare_env())
     assert p.returncode == 0, p.stderr
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, p.stdout
+    lines = p.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout  # stdout: the one JSON line only
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["steps"] == 3
     # max over ranks: rank 1 sleeps 0.1 s, so the whole-job step time reflects it
