@@ -26,5 +26,8 @@ BigUint biguint_add(Engine& e, const BigUint& a, const BigUint& b, int mode);
 BigUint biguint_mul(Engine& e, const BigUint& a, const BigUint& b, int mode);
 // k + a * b, limbs identical to biguint_add(k, biguint_mul(a, b)) (src/schnorr.rs:274)
 BigUint biguint_mul_add(Engine& e, const BigUint& a, const BigUint& b, const BigUint& k, int mode);
+// kCompat limbs by the carry-count chain (compat_chain.cpp), for 2 <= min(la, lb) <= 8
+bool compat_chain_applies(size_t la, size_t lb);
+BigUint compat_chain_mul(Engine& e, const BigUint& a, const BigUint& b);
 
 }  // namespace fhe

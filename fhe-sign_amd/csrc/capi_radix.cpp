@@ -566,6 +566,64 @@ int fhe_biguint_mul(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, int 
     });
 }
 
+// Host-only run of the BigUintFHE mul / mul-add on publicly known limbs (no GPU, no key): every block
+// is trivial, so the engine folds each lookup on the host (Engine host_only) -- the radix algorithms'
+// indexing, LUTs and carry logic checked on the CPU against the reference's limb loop.
+int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k, size_t lk,
+                         int mode, uint32_t* out, size_t cap, size_t* n) {
+    if ((la && !a) || (lb && !b) || (lk && !k) || !n || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
+    return guarded([&] {
+        fhe_ctx c;  // parameters only: a host-only engine never touches the device
+        Engine e(&c, Engine::kHostFold);
+        auto make = [](const uint32_t* v, size_t n) {
+            BigUint r;
+            for (size_t i = 0; i < n; ++i) r.digits.push_back(radix_trivial(v[i], 0, kLimbBlocks));
+            return r;
+        };
+        const BigUint A = make(a, la), B = make(b, lb);
+        const BigUint R = k ? biguint_mul_add(e, A, B, make(k, lk), mode) : biguint_mul(e, A, B, mode);
+        *n = R.digits.size();
+        engine_check(R.digits.size() <= cap || !out, "output buffer too small");
+        for (size_t i = 0; out && i < R.digits.size(); ++i) {
+            uint64_t v = 0;
+            for (uint32_t q = 0; q < R.digits[i].nblocks(); ++q) {
+                const Block& blk = R.digits[i].blocks[q];
+                engine_check(blk.trivial() && !blk.half_neg && blk.value < 4, "host mul: a non-trivial output block");
+                v |= (uint64_t)blk.value << (2 * q);
+            }
+            out[i] = (uint32_t)v;
+        }
+        return FHE_OK;
+    });
+}
+
+// Dry run (no GPU): the same op on la x lb "encrypted" limbs (placeholder blocks) recorded and scheduled
+// by the engine without launching anything -- its bootstrap count, launch levels and level sizes.
+int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64_t* pbs, uint64_t* levels,
+                               uint32_t* level_sizes, size_t cap) {
+    if (!pbs || !levels || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
+    return guarded([&] {
+        fhe_ctx c;
+        Engine e(&c, Engine::kDry);
+        auto make = [&](size_t n) {
+            BigUint r;
+            for (size_t i = 0; i < n; ++i) {
+                Radix d;
+                for (uint32_t q = 0; q < kLimbBlocks; ++q) d.blocks.push_back(e.dry_block(3));
+                r.digits.push_back(std::move(d));
+            }
+            return r;
+        };
+        const BigUint A = make(la), B = make(lb);
+        BigUint R = lk ? biguint_mul_add(e, A, B, make(lk), mode) : biguint_mul(e, A, B, mode);
+        e.flush();
+        *pbs = e.pbs_count;
+        *levels = e.levels;
+        for (size_t i = 0; level_sizes && i < e.level_log.size() && i < cap; ++i) level_sizes[i] = e.level_log[i];
+        return FHE_OK;
+    });
+}
+
 int fhe_biguint_mul_add(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, const fhe_biguint* k, int mode,
                         fhe_biguint** out) {
     int rc = need_engine(c);

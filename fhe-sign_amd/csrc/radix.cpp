@@ -45,11 +45,18 @@ Slot::~Slot() {
 }
 
 BlockPool::~BlockPool() {
+    if (dry_) return;
     (void)hipSetDevice(device_);
     for (void* c : chunks_) (void)hipFree(c);
 }
 
 std::shared_ptr<Slot> BlockPool::alloc() {
+    if (dry_) {
+        auto s = std::make_shared<Slot>();
+        s->p = reinterpret_cast<uint64_t*>(dry_next_);
+        dry_next_ += kBigCt * 8;
+        return s;  // no pool: nothing to release
+    }
     if (free_.empty()) {
         const size_t per = 1024;  // 16 MiB chunks
         void* c = nullptr;
@@ -66,9 +73,10 @@ std::shared_ptr<Slot> BlockPool::alloc() {
 }
 
 // ============================================================================ engine
-Engine::Engine(fhe_ctx* ctx) : ctx_(ctx) {
-    pool_ = std::make_shared<BlockPool>(ctx->device);
-    for (auto& ev : desc_ev_) hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+Engine::Engine(fhe_ctx* ctx, int host_mode) : ctx_(ctx), host_mode_(host_mode) {
+    pool_ = std::make_shared<BlockPool>(ctx->device, host_mode_ == kDry);
+    if (host_mode_ == kDevice)
+        for (auto& ev : desc_ev_) hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
     // FHE_TRACE_LEVELS=1: synchronize after every level and print its size and wall time (stderr);
     // a diagnostic for schedule work, never set by the bench or the tests.
     if (const char* t = getenv("FHE_TRACE_LEVELS")) trace_ = atoi(t) != 0;
@@ -79,7 +87,17 @@ Engine::Engine(fhe_ctx* ctx) : ctx_(ctx) {
     if (const char* t = getenv("FHE_ROUND")) round_ = std::max(1, atoi(t));
 }
 
+Block Engine::dry_block(uint32_t degree) {
+    engine_check(host_mode_ == kDry, "dry_block outside a dry engine");
+    Block b;
+    b.slot = pool_->alloc();
+    b.degree = degree;
+    b.noise = 1;
+    return b;
+}
+
 Engine::~Engine() {
+    if (host_mode_ != kDevice) return;
     (void)hipSetDevice(ctx_->device);
     (void)hipStreamSynchronize(ctx_->stream);
     for (auto* h : h_desc_)
@@ -171,22 +189,31 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         PbsItem& it = items[i];
         if (it.raw) {  // caller-guaranteed range (radix.h): no folding, no degree check
             engine_check(it.half_table.size() == mc, "raw LUT table size");
-            int64_t cst = it.cst;
+            int64_t cst2 = 2 * (int64_t)it.cst + it.half_cst;  // half steps
             uint32_t noise = 0;
             for (const Term& t : it.terms) {
                 if (t.coef == 0) continue;
                 if (t.b.trivial())
-                    cst += (int64_t)t.coef * t.b.value;
+                    cst2 += (int64_t)t.coef * trivial_half2(t.b);
                 else {
                     live[i].push_back(t);
                     noise += (uint32_t)(t.coef * t.coef) * t.b.noise;
                 }
             }
             engine_check(noise <= kMaxNoise, "raw PBS input noise above the budget");
-            engine_check(!live[i].empty(), "raw PBS item without an encrypted term");
+            if (live[i].empty()) {  // a known input: evaluate on the host
+                engine_check(cst2 % 2 == 0 && cst2 >= -32 && cst2 < 32, "raw PBS item: known input off the grid");
+                const int64_t v = cst2 / 2;
+                const int32_t h = v >= 0 ? it.half_table[v] : -it.half_table[v + 16];
+                // an integer output, or a sign lookup's +-1/2 (kept as value - 1/2)
+                engine_check(h % 2 == 0 ? h >= 0 : (h == 1 || h == -1), "raw PBS item: known output off the grid");
+                out[i] = Block::make_trivial((uint32_t)((h + 1) / 2));
+                out[i].half_neg = h % 2 != 0;
+                continue;
+            }
             out[i].degree = it.raw_degree;
             out[i].noise = 1;
-            csts[i] = cst;
+            csts[i] = cst2;  // half steps (raw)
             gpu.push_back(i);
             continue;
         }
@@ -195,6 +222,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         uint32_t noise = 0;
         for (const Term& t : it.terms) {
             if (t.coef == 0) continue;
+            engine_check(!t.b.half_neg, "a sign lookup output in an ordinary item");
             if (t.b.trivial())
                 cst += (int64_t)t.coef * t.b.value;
             else {
@@ -229,6 +257,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         }
     }
     if (gpu.empty()) return out;
+    engine_check(host_mode_ != kHostFold, "host-only engine: an item needs a bootstrap (encrypted input)");
 
     // register LUTs, allocate destinations, record pending nodes
     const uint64_t delta = p.delta();
@@ -245,8 +274,9 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         PbsDesc& d = n.d;
         std::memset(&d, 0, sizeof d);
         n.hold.push_back(out[i].slot);
-        // flatten lazy terms into their slot blocks (merging repeats)
+        // flatten lazy terms into their slot blocks (merging repeats); dcst in half steps for raw items
         int64_t dcst = csts[i];
+        const int64_t unit = raw ? 2 : 1;
         terms.clear();
         const size_t cap = raw ? (size_t)kMaxWideTerms : (size_t)kMaxTerms;
         auto put = [&](const Block& b, int32_t coef) {
@@ -265,7 +295,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
                 put(t.b, t.coef);
                 continue;
             }
-            dcst += (int64_t)t.coef * t.b.lin_cst;
+            dcst += unit * (int64_t)t.coef * t.b.lin_cst;
             for (const Term& u : *t.b.lin) put(u.b, t.coef * u.coef);
         }
         const uint32_t nt = (uint32_t)terms.size();
@@ -279,7 +309,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         }
         d.nterms = nt;
         d.lut = lut;
-        d.cst = (uint64_t)dcst * delta + (uint64_t)((int64_t)items[i].half_cst * (int64_t)(delta / 2));
+        d.cst = raw ? (uint64_t)dcst * (delta / 2) : (uint64_t)dcst * delta;
         if (gstats_) {
             std::vector<std::pair<const uint64_t*, int64_t>> tk;
             for (uint32_t u = 0; u < nt; ++u) tk.push_back({terms[u].src, terms[u].coef});
@@ -475,6 +505,19 @@ void Engine::flush() {
     // a fanned-out level's round is one latency-kernel round on every rank
     const size_t round = (size_t)round_ * (size_t)std::max(1, ctx_->fanout_world());
     std::vector<std::vector<int32_t>> lv = schedule_levels(deps, sched_, round);
+    if (host_mode_ == kDry) {  // the schedule's statistics, nothing launched
+        for (auto& l : lv) {
+            pbs_count += l.size();
+            levels += 1;
+            rank_pbs += l.size();
+            if (level_log.size() < kLevelLogCap) level_log.push_back((uint32_t)l.size());
+        }
+        for (auto& n : pending_) n.hold[0]->node = -1;
+        pending_.clear();
+        pending_dependent_ = 0;
+        eager_ok_ = true;
+        return;
+    }
     // one staging copy of every level's descriptors (+ fanned-out levels' destination tables)
     const int W = ctx_->fanout_world();
     size_t ndesc = 0, maxchunk = 0, maxgather = 0;
@@ -1308,6 +1351,33 @@ std::vector<Radix> radix_sum_lazy(Engine& e, const std::vector<std::pair<const R
             res[i].blocks.push_back(block_lazy(t, 0, 3));
         }
     }
+    return res;
+}
+
+Blocks radix_carry_outs(Engine& e, const std::vector<std::vector<Blocks>>& problems) {
+    std::vector<PbsItem> items;
+    std::vector<size_t> start;
+    for (const auto& cols : problems) {
+        start.push_back(items.size());
+        for (size_t k = 0; k < cols.size(); ++k) {
+            PbsItem it;
+            for (const Block& b : cols[k]) it.terms.push_back({b, 1});
+            it.table = k == 0 ? LUT_GEN() : LUT_STATE();
+            items.push_back(it);
+        }
+    }
+    Blocks outs = e.run(items);
+    std::vector<Blocks> cur(problems.size());
+    std::vector<std::vector<uint32_t>> want(problems.size());
+    for (size_t p = 0; p < problems.size(); ++p) {
+        const size_t m = problems[p].size();
+        engine_check(m > 0, "carry out of an empty column set");
+        cur[p].assign(outs.begin() + start[p], outs.begin() + start[p] + m);
+        want[p] = {(uint32_t)(m - 1)};
+    }
+    std::vector<Blocks> car = carry_prefix(e, std::move(cur), want);
+    Blocks res;
+    for (size_t p = 0; p < problems.size(); ++p) res.push_back(car[p].back());
     return res;
 }
 

@@ -49,6 +49,8 @@ struct Block {
     // input term, flattened into the descriptor by Engine::run
     std::shared_ptr<const std::vector<Term>> lin;
     int32_t lin_cst = 0;
+    // trivial only: the block stands for value - 1/2 (a sign lookup's known output, raw items only)
+    bool half_neg = false;
     bool trivial() const { return !slot && !lin; }
     bool lazy() const { return (bool)lin; }
     const uint64_t* ptr() const { return slot ? slot->p : nullptr; }
@@ -64,7 +66,7 @@ using Blocks = std::vector<Block>;
 
 class BlockPool : public std::enable_shared_from_this<BlockPool> {
 public:
-    explicit BlockPool(int device) : device_(device) {}
+    explicit BlockPool(int device, bool dry = false) : device_(device), dry_(dry) {}
     ~BlockPool();
     std::shared_ptr<Slot> alloc();
     void release(uint64_t* p) { free_.push_back(p); }
@@ -72,6 +74,8 @@ public:
 
 private:
     int device_;
+    bool dry_;                // Engine kDry: slots are distinct placeholder addresses, never dereferenced
+    uintptr_t dry_next_ = 0x10000;
     std::vector<void*> chunks_;
     std::vector<uint64_t*> free_;
     size_t total_ = 0;
@@ -112,7 +116,15 @@ struct PbsItem {
 // count equals the critical path.
 class Engine {
 public:
-    explicit Engine(fhe_ctx* ctx);
+    // Host modes (no device work; the CPU tests and graph statistics):
+    //   kHostFold -- every item must fold on the host (trivial inputs): radix algorithms evaluated on
+    //                publicly known values (fhe_host_biguint_mul);
+    //   kDry      -- items on dry_block() inputs are recorded and scheduled like the real thing, nothing
+    //                is launched: levels and bootstrap counts of an op (fhe_host_biguint_mul_stats).
+    enum HostMode { kDevice = 0, kHostFold = 1, kDry = 2 };
+    explicit Engine(fhe_ctx* ctx, int host_mode = kDevice);
+    // kDry: an "encrypted" block of the given degree (a placeholder slot)
+    Block dry_block(uint32_t degree);
     ~Engine();
     fhe_ctx* ctx() const { return ctx_; }
     // Records one dependency level of items; returns one output block per item (possibly trivial).
@@ -150,6 +162,7 @@ public:
 
 private:
     fhe_ctx* ctx_;
+    int host_mode_ = kDevice;
     std::shared_ptr<BlockPool> pool_;
     uint64_t* d_up_ = nullptr;  // upload staging: n big LWEs, then n destination pointers
     size_t up_cap_ = 0;
@@ -185,6 +198,8 @@ private:
 };
 
 void engine_check(bool ok, const char* what);
+// 2 x the value a trivial block stands for (half_neg: value - 1/2)
+inline int64_t trivial_half2(const Block& b) { return 2 * (int64_t)b.value - (b.half_neg ? 1 : 0); }
 // An engine failure that carries its C-ABI status (e.g. FHE_ERR_TIMEOUT from a bounded stream wait):
 // the C entry points return `code` instead of the generic FHE_ERR_INVALID.
 struct EngineError : std::runtime_error {
@@ -225,6 +240,10 @@ std::vector<Radix> radix_sum_lazy(Engine& e, const std::vector<std::pair<const R
                                   std::vector<Radix*>& refresh);
 // Carry propagation of raw column blocks (each column may hold several blocks).
 Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks);
+// The carry out of the top column of each problem (columns already bounded: each a sum <= 6, <= 7 at
+// position 0, of <= 3 blocks), and nothing below it: one state level + the carry-chain nodes that
+// carry depends on.  A clean bit per problem.
+Blocks radix_carry_outs(Engine& e, const std::vector<std::vector<Blocks>>& problems);
 // Wrapping product.
 Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks);
 // Batched independent products (one level schedule for all); addends[i], if given, is summed into

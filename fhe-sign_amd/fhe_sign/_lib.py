@@ -132,6 +132,10 @@ _SIGNATURES = [
     ("fhe_schedule_levels_ranks", C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_size_t, C.c_int, C.c_int,
                                             C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("fhe_progress_marks_probe", C.c_int, [C.c_uint32, u32p]),
+    ("fhe_host_biguint_mul", C.c_int, [u32p, C.c_size_t, u32p, C.c_size_t, u32p, C.c_size_t, C.c_int, u32p, C.c_size_t,
+                                       C.POINTER(C.c_size_t)]),
+    ("fhe_host_biguint_mul_stats", C.c_int, [C.c_size_t, C.c_size_t, C.c_size_t, C.c_int, C.POINTER(C.c_uint64),
+                                             C.POINTER(C.c_uint64), u32p, C.c_size_t]),
     ("fhe_biguint_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_from_digits", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_size_t)]),

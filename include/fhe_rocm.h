@@ -314,6 +314,17 @@ int fhe_schedule_levels_ranks(const int32_t* dep_offsets, const int32_t* deps, s
  * attached): after `levels` launched levels with none completed, the largest number of levels
  * between consecutive outstanding marks (at most 32 are kept; their gaps stay even). */
 int fhe_progress_marks_probe(uint32_t levels, uint32_t* max_gap);
+/* Host-only check of the BigUintFHE limb algorithms (no GPU, no key): a * b (k == NULL) or k + a * b on
+ * publicly known limbs (LSB first) through the engine's host folding -- the same radix code path as
+ * fhe_biguint_mul / _mul_add, every lookup evaluated on the host.  Writes up to `cap` limbs to out
+ * and the limb count to *n. */
+int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k, size_t lk,
+                         int mode, uint32_t* out, size_t cap, size_t* n);
+/* Dry run (no GPU): the bootstraps and launch levels the engine schedules for the la x lb BigUintFHE mul
+ * (or k + a * b with lk > 0 limbs of k) on encrypted limbs -- recorded and scheduled, nothing launched.
+ * level_sizes (optional, up to cap entries): bootstraps per launched level. */
+int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64_t* pbs, uint64_t* levels,
+                               uint32_t* level_sizes, size_t cap);
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */
