@@ -95,20 +95,47 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
     // FHE_CHAIN_PHASES=1 (diagnostic, dry runs): flush and print the bootstrap count after each phase
     static const bool phases = getenv("FHE_CHAIN_PHASES") && atoi(getenv("FHE_CHAIN_PHASES"));
     auto phase = [&](const char* what) {
-        if (!phases) return;
+        if (!phases || getenv("FHE_CHAIN_NOFLUSH")) return;
         e.flush();
         fprintf(stderr, "[compat chain] %-28s %8llu PBS %4llu levels\n", what, (unsigned long long)e.pbs_count,
                 (unsigned long long)e.levels);
     };
     engine_check(compat_chain_applies(la, lb), "compat chain: limb counts");
-    // ---- the 64-bit products a_i * b_j (one batched multiplication, clean blocks)
+    // ---- the 64-bit products a_i * b_j: one batched multiplication, columns compressed but not
+    // propagated (each <= 6 over <= 3 blocks; exact, as the products fit 32 columns).  Split at the
+    // limb boundary: lo_cs = columns 0..15 = lo(P) + 2^32 c_P, hi_cs = columns 16..31 = hi(P) - c_P,
+    // c_P = the carry out of column 15 (a bit): only c_P is resolved per product, not the product.
     std::vector<Radix> a64(la), b64(lb);
     for (size_t i = 0; i < la; ++i) a64[i] = radix_resize(A.digits[i], 2 * kLimbBlocks);
     for (size_t j = 0; j < lb; ++j) b64[j] = radix_resize(B.digits[j], 2 * kLimbBlocks);
     std::vector<std::pair<const Radix*, const Radix*>> ops;
     for (size_t i = 0; i < la; ++i)
         for (size_t j = 0; j < lb; ++j) ops.push_back({&a64[i], &b64[j]});
-    std::vector<Radix> P = radix_mul_many(e, ops, 2 * kLimbBlocks);
+    std::vector<std::vector<Blocks>> PC = radix_mul_many_columns(e, ops, 2 * kLimbBlocks);
+    {
+        // entries must be fresh-noise blocks for the accumulation's noise budget (lazy multiples of a
+        // public block -- only from trivially encrypted limbs -- are refreshed)
+        static const auto ID = table([](uint32_t v) { return v; });
+        std::vector<PbsItem> items;
+        std::vector<Block*> at;
+        for (auto& cols : PC)
+            for (auto& c : cols)
+                for (Block& b : c)
+                    if (!b.trivial() && (b.lazy() || b.noise > 1)) {
+                        items.push_back(item({{b, 1}}, ID));
+                        at.push_back(&b);
+                    }
+        if (!items.empty()) {
+            Blocks outs = e.run(items);
+            for (size_t k = 0; k < outs.size(); ++k) *at[k] = outs[k];
+        }
+    }
+    Blocks cP;
+    {
+        std::vector<std::vector<Blocks>> lo(PC.size());
+        for (size_t k = 0; k < PC.size(); ++k) lo[k].assign(PC[k].begin(), PC[k].begin() + kLimbBlocks);
+        cP = radix_carry_outs(e, lo);
+    }
     phase("products");
 
     // ---- touches per limb
@@ -120,12 +147,16 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
             T[idx + 1].push_back({s, s, kMid, -1});
             if (idx + 2 < L) T[idx + 2].push_back({s, s, kTop, -1});
         }
-    // ---- prefix sums of each limb's addends: columns kept at <= 2 entries (lo + incoming hi, v <= 5;
-    // position 0 lo only), overflow O (the carries out of column 15, a small integer block)
+    // ---- prefix sums of each limb's addends, K_acc(p) = K(p) + 2^32 * (c_P of the BOT addends so far):
+    // 16 columns kept at <= 2 entries (lo <= 3 + incoming hi <= 2; position 0 lo only) by one
+    // compression per addend (a MID addend hi_cs brings its c_P along at column 0), the carries out of
+    // column 15 in a small-integer block O = 1 + sum(hi_15) - sum(c_P of BOT addends), so that
+    // H = floor(K / 2^32) = O - 1 + c1, c1 = the carry out of the 16 columns.  O stays in [0, 15]:
+    // O - 1 = H - c1 >= -1 and H <= 14.
     struct Prefix {
         std::vector<Blocks> cols;  // 16 columns
-        Block O;                   // floor-part accumulated so far
-        Block c1;                  // carry out of the 16 columns (H = O + c1)
+        Block O;                   // biased overflow (above)
+        Block c1;                  // carry out of the 16 columns
         Block g;                   // 15 - near * (K mod 16)
     };
     std::vector<std::vector<Prefix>> PF(L);
@@ -143,48 +174,38 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
                 t.prefix = (int)adds[l].size() - 1;
             }
         for (size_t l = 0; l < L; ++l) PF[l].resize(adds[l].size());
+        const Block kBias = Block::make_trivial(1);
         for (bool more = true; more;) {
             more = false;
             std::vector<PbsItem> items;
             struct Dst {
                 size_t l, p;
-                int col;  // 0..15: lo of that column; 16 + c: hi of column c; 32: O
+                int col;  // 0..15: lo of that column; 16 + c: hi of column c
             };
             std::vector<Dst> dst;
-            std::vector<std::pair<size_t, size_t>> firsts;
             for (size_t l = 0; l < L; ++l) {
                 const size_t p = next[l];
                 if (p >= adds[l].size()) continue;
                 more = true;
                 next[l]++;
-                const Radix& pr = P[adds[l][p].first];
-                const uint32_t off = adds[l][p].second ? kLimbBlocks : 0;
-                if (p == 0) {
-                    firsts.push_back({l, p});
-                    continue;
-                }
-                const Prefix& prev = PF[l][p - 1];
+                const auto& pc = PC[adds[l][p].first];
+                const bool hi = adds[l][p].second != 0;
+                const uint32_t off = hi ? kLimbBlocks : 0;
                 for (uint32_t m = 0; m < kLimbBlocks; ++m) {
                     std::vector<Term> t;
-                    for (const Block& b : prev.cols[m]) t.push_back({b, 1});
-                    t.push_back({pr.blocks[off + m], 1});
+                    if (p > 0)
+                        for (const Block& b : PF[l][p - 1].cols[m]) t.push_back({b, 1});
+                    for (const Block& b : pc[off + m]) t.push_back({b, 1});
+                    if (hi && m == 0) t.push_back({cP[adds[l][p].first], 1});
                     items.push_back(item(t, MOD4));
                     dst.push_back({l, p, (int)m});
                     items.push_back(item(t, DIV4));
                     dst.push_back({l, p, 16 + (int)m});
                 }
             }
-            for (auto& f : firsts) {
-                Prefix& x = PF[f.first][0];
-                const Radix& pr = P[adds[f.first][0].first];
-                const uint32_t off = adds[f.first][0].second ? kLimbBlocks : 0;
-                x.cols.assign(kLimbBlocks, {});
-                for (uint32_t m = 0; m < kLimbBlocks; ++m) x.cols[m].push_back(pr.blocks[off + m]);
-                x.O = Block::make_trivial(0);
-            }
             if (items.empty()) continue;
             Blocks outs = e.run(items);
-            // assemble the new columns, then the overflow update (O + hi_15) as its own item
+            // assemble the new columns, then the overflow update (O + hi_15 - [BOT] c_P)
             std::vector<PbsItem> oitems;
             std::vector<std::pair<size_t, size_t>> odst;
             for (size_t k = 0; k < outs.size(); ++k) {
@@ -196,20 +217,16 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
                 } else if (c - 16 + 1 < (int)kLimbBlocks) {
                     x.cols[c - 16 + 1].push_back(outs[k]);
                 } else {  // hi of column 15 -> overflow
-                    const Prefix& prev = PF[dst[k].l][dst[k].p - 1];
-                    if (outs[k].trivial() && outs[k].value == 0) {
-                        x.O = prev.O;
-                    } else {
-                        oitems.push_back(raw_item({{prev.O, 1}, {outs[k], 1}}, 0, [](uint32_t v) { return v; }, 15));
-                        odst.push_back({dst[k].l, dst[k].p});
-                    }
+                    const size_t l = dst[k].l, p = dst[k].p;
+                    const Block& O0 = p ? PF[l][p - 1].O : kBias;
+                    std::vector<Term> t{{O0, 1}, {outs[k], 1}};
+                    if (adds[l][p].second == 0) t.push_back({cP[adds[l][p].first], -1});
+                    oitems.push_back(raw_item(t, 0, [](uint32_t v) { return v; }, 15));
+                    odst.push_back({l, p});
                 }
             }
-            if (!oitems.empty()) {
-                // an item with a trivial O and a live hi is a plain raw identity
-                Blocks os = e.run(oitems);
-                for (size_t k = 0; k < os.size(); ++k) PF[odst[k].first][odst[k].second].O = os[k];
-            }
+            Blocks os = e.run(oitems);
+            for (size_t k = 0; k < os.size(); ++k) PF[odst[k].first][odst[k].second].O = os[k];
         }
     }
     phase("prefix sums");
@@ -219,10 +236,6 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
         std::vector<std::pair<size_t, size_t>> where;
         for (size_t l = 0; l < L; ++l)
             for (size_t p = 0; p < PF[l].size(); ++p) {
-                if (p == 0) {  // one canonical addend: < 2^32
-                    PF[l][p].c1 = Block::make_trivial(0);
-                    continue;
-                }
                 probs.push_back(PF[l][p].cols);
                 where.push_back({l, p});
             }
@@ -330,9 +343,10 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
                 k->terms.push_back({S[l - 1][m], c});
         };
         const Prefix* hp = prev[u].prefix >= 0 ? &PF[l - 1][prev[u].prefix] : nullptr;
-        if (hp) {
+        if (hp) {  // H = O - 1 + c1
             k->terms.push_back({hp->O, 1});
             k->terms.push_back({hp->c1, 1});
+            k->half -= 2;
         }
         add_s(u, 1);
         for (size_t m = 0; m < prev.size() && prev[m].step <= step; ++m)
@@ -374,6 +388,14 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
             S[l][at[q]] = outs[q];
             s_known0[l][at[q]] = false;
         }
+        if (phases) {
+            int32_t dmax = 0, gmax = 0;
+            for (size_t q = 0; q < at.size(); ++q) {
+                dmax = std::max(dmax, e.depth_of(outs[q]));
+                gmax = std::max(gmax, e.depth_of(PF[l][T[l][at[q]].prefix].g));
+            }
+            fprintf(stderr, "[compat chain] limb %2zu: %zu signs, depth %d (its g: %d)\n", l, at.size(), dmax, gmax);
+        }
     }
 
     phase("chain");
@@ -383,14 +405,7 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
     {
         // K_l(last) mod 2^32, canonical
         std::vector<Radix> X(L);
-        for (size_t l = 0; l < L; ++l) {
-            if (PF[l].size() == 1) {  // one canonical addend
-                X[l].blocks.clear();
-                for (const Blocks& c : PF[l][0].cols) X[l].blocks.push_back(c[0]);
-            } else {
-                X[l] = radix_propagate_columns(e, PF[l].back().cols, kLimbBlocks);
-            }
-        }
+        for (size_t l = 0; l < L; ++l) X[l] = radix_propagate_columns(e, PF[l].back().cols, kLimbBlocks);
         std::vector<Lin> kf(L);
         std::vector<bool> has_k(L);
         for (size_t l = 0; l < L; ++l) has_k[l] = k_of(l, (size_t)-1, &kf[l]);

@@ -87,6 +87,19 @@ Engine::Engine(fhe_ctx* ctx, int host_mode) : ctx_(ctx), host_mode_(host_mode) {
     if (const char* t = getenv("FHE_ROUND")) round_ = std::max(1, atoi(t));
 }
 
+int32_t Engine::depth_of(const Block& b) const {
+    int32_t d = 0;
+    auto one = [&](const Block& x) {
+        if (x.slot && x.slot->node >= 0 && (size_t)x.slot->node < pending_.size())
+            d = std::max(d, pending_[x.slot->node].depth);
+    };
+    if (b.lazy())
+        for (const Term& t : *b.lin) one(t.b);
+    else
+        one(b);
+    return d;
+}
+
 Block Engine::dry_block(uint32_t degree) {
     engine_check(host_mode_ == kDry, "dry_block outside a dry engine");
     Block b;
@@ -322,6 +335,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
             in_deg_.push_back((uint8_t)(raw ? 16 : 63 - __builtin_clzll(rr | 1)));
         }
         d.dst = out[i].slot->p;
+        for (int32_t dep : n.deps) n.depth = std::max(n.depth, pending_[dep].depth + 1);
         out[i].slot->node = (int64_t)pending_.size();
         if (!n.deps.empty()) ++pending_dependent_;
         pending_.push_back(std::move(n));
@@ -1470,8 +1484,29 @@ static void add_products(const Radix& a, const Radix& b, uint32_t nblocks, std::
     }
 }
 
+static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
+                                            uint32_t nblocks, const std::vector<const Radix*>& addends);
+
 std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                   uint32_t nblocks, const std::vector<const Radix*>& addends) {
+    std::vector<ColProblem> probs = mul_problems(e, ops, nblocks, addends);
+    return propagate_many(e, probs);
+}
+
+std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
+                                                        const std::vector<std::pair<const Radix*, const Radix*>>& ops,
+                                                        uint32_t nblocks) {
+    std::vector<ColProblem> probs = mul_problems(e, ops, nblocks, {});
+    std::vector<ColProblem*> ptrs;
+    for (auto& p : probs) ptrs.push_back(&p);
+    compress_columns(e, ptrs);
+    std::vector<std::vector<Blocks>> res;
+    for (auto& p : probs) res.push_back(std::move(p.cols));
+    return res;
+}
+
+static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
+                                            uint32_t nblocks, const std::vector<const Radix*>& addends) {
     std::vector<PbsItem> items;
     std::vector<uint32_t> cols_of;
     std::vector<std::vector<std::pair<uint32_t, Block>>> direct(ops.size());
@@ -1509,7 +1544,7 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
             for (uint32_t k = 0; k < nblocks && k < addends[i]->nblocks(); ++k)
                 probs[i].cols[k].push_back(addends[i]->blocks[k]);
     }
-    return propagate_many(e, probs);
+    return probs;
 }
 
 Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {

@@ -125,6 +125,8 @@ public:
     explicit Engine(fhe_ctx* ctx, int host_mode = kDevice);
     // kDry: an "encrypted" block of the given degree (a placeholder slot)
     Block dry_block(uint32_t degree);
+    // diagnostics: the dependency depth (levels) of a pending block's producer, 0 if none is pending
+    int32_t depth_of(const Block& b) const;
     ~Engine();
     fhe_ctx* ctx() const { return ctx_; }
     // Records one dependency level of items; returns one output block per item (possibly trivial).
@@ -183,6 +185,7 @@ private:
         std::vector<std::shared_ptr<Slot>> hold;  // [0] output, then inputs: alive until launched
         std::vector<int32_t> deps;                // pending producers of the inputs
         std::vector<TermExt> ext;                 // terms of a wide combination (d.nterms > kMaxTerms)
+        int32_t depth = 1;                        // 1 + the deepest pending producer (diagnostics)
     };
     std::vector<Pending> pending_;
     size_t pending_dependent_ = 0;  // pending nodes with at least one pending producer
@@ -250,6 +253,12 @@ Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks);
 // product i's columns before its carry propagation (a multiply-add costs no extra level).
 std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                   uint32_t nblocks, const std::vector<const Radix*>& addends = {});
+// The same products summed into columns and compressed only (each column a sum <= 6, <= 7 at
+// position 0, of <= 3 blocks; no carry propagation): the columns' value is the product mod 4^nblocks,
+// exactly the product when it fits (non-negative entries cannot wrap below it).
+std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
+                                                        const std::vector<std::pair<const Radix*, const Radix*>>& ops,
+                                                        uint32_t nblocks);
 // a * b + c (wrapping at nblocks), one carry propagation.
 Radix radix_mul_add(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks);
 Radix radix_scalar_and(Engine& e, const Radix& a, const BigConst& mask);
