@@ -624,6 +624,42 @@ int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64
     });
 }
 
+// Dry run of one radix op on encrypted operands of the given widths (FHE_HOST_OP_*): its bootstrap
+// count and launch levels as the engine schedules them, nothing launched.
+int fhe_host_radix_stats(int op, uint32_t bits, uint64_t* pbs, uint64_t* levels, uint32_t* level_sizes, size_t cap) {
+    if (!pbs || !levels || bits < 2 || bits % 2 || bits > FHE_RADIX_MAX_BITS) return FHE_ERR_INVALID;
+    return guarded([&] {
+        fhe_ctx c;
+        Engine e(&c, Engine::kDry);
+        auto make = [&] {
+            Radix r;
+            for (uint32_t q = 0; q < bits / 2; ++q) r.blocks.push_back(e.dry_block(3));
+            return r;
+        };
+        const Radix A = make(), B = make();
+        std::vector<Radix> keep;  // results stay referenced through the flush (else they are dead nodes)
+        switch (op) {
+        case FHE_HOST_OP_DIVREM: {
+            auto qr = radix_divrem(e, A, B);
+            keep = {qr.first, qr.second};
+            break;
+        }
+        case FHE_HOST_OP_MUL: keep = {radix_mul(e, A, B, bits / 2)}; break;
+        case FHE_HOST_OP_ADD: keep = {radix_sum(e, {&A, &B}, bits / 2)}; break;
+        case FHE_HOST_OP_SUB: keep = {radix_sub(e, A, B)}; break;
+        case FHE_HOST_OP_SHR: keep = {radix_shr(e, A, B)}; break;
+        case FHE_HOST_OP_LT: keep = {Radix{{radix_lt(e, A, B)}}}; break;
+        case FHE_HOST_OP_DIV_SCALAR: keep = {radix_scalar_div(e, A, BigConst{0xC0FFEE01u})}; break;
+        default: engine_check(false, "unknown host op");
+        }
+        e.flush();
+        *pbs = e.pbs_count;
+        *levels = e.levels;
+        for (size_t i = 0; level_sizes && i < e.level_log.size() && i < cap; ++i) level_sizes[i] = e.level_log[i];
+        return FHE_OK;
+    });
+}
+
 int fhe_biguint_mul_add(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, const fhe_biguint* k, int mode,
                         fhe_biguint** out) {
     int rc = need_engine(c);

@@ -325,6 +325,16 @@ int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t
  * level_sizes (optional, up to cap entries): bootstraps per launched level. */
 int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64_t* pbs, uint64_t* levels,
                                uint32_t* level_sizes, size_t cap);
+/* Dry run of one radix op on two encrypted `bits`-wide operands: bootstraps, launch levels and level
+ * sizes as the engine schedules them (nothing launched). */
+#define FHE_HOST_OP_DIVREM 0     /* a / b and a % b, encrypted divisor */
+#define FHE_HOST_OP_MUL 1
+#define FHE_HOST_OP_ADD 2
+#define FHE_HOST_OP_SUB 3
+#define FHE_HOST_OP_SHR 4        /* encrypted shift amount */
+#define FHE_HOST_OP_LT 5
+#define FHE_HOST_OP_DIV_SCALAR 6 /* a / 0xC0FFEE01 */
+int fhe_host_radix_stats(int op, uint32_t bits, uint64_t* pbs, uint64_t* levels, uint32_t* level_sizes, size_t cap);
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */
