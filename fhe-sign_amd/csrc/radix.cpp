@@ -85,6 +85,8 @@ Engine::Engine(fhe_ctx* ctx, int host_mode) : ctx_(ctx), host_mode_(host_mode) {
     if (const char* t = getenv("FHE_SCHED")) sched_ = atoi(t);
     // FHE_ROUND: level fill granule in bootstraps per GPU (schedule experiments; default 256)
     if (const char* t = getenv("FHE_ROUND")) round_ = std::max(1, atoi(t));
+    // FHE_NO_EAGER=1: no eager launch of a first large independent batch (schedule experiments)
+    if (const char* t = getenv("FHE_NO_EAGER")) no_eager_ = atoi(t) != 0;
 }
 
 int32_t Engine::depth_of(const Block& b) const {
@@ -345,7 +347,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     // products) is one throughput level under any schedule: launch it now, so the GPU works while
     // the host builds the rest of the graph (once per explicit flush: later independent batches,
     // e.g. the compressions that follow, stay in the graph to be spread over idle capacity)
-    if (eager_ok_ && pending_.size() >= kEagerBatch && pending_dependent_ == 0) {
+    if (eager_ok_ && !no_eager_ && pending_.size() >= kEagerBatch && pending_dependent_ == 0) {
         flush();
         eager_ok_ = false;
     }
@@ -1517,7 +1519,7 @@ static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pa
     // compat 256-bit mul's 32768 block products); the rest follows as the engine's eager batch.
     size_t est = 0;
     for (auto& op : ops) est += (size_t)op.first->nblocks() * op.second->nblocks();
-    bool head = e.eager_head_ok() && est >= 4 * Engine::kEagerHead;
+    bool head = e.eager_head_ok() && !e.no_eager() && est >= 4 * Engine::kEagerHead;
     Blocks outs;
     for (size_t i = 0; i < ops.size(); ++i) {
         start[i] = outs.size() + items.size();

@@ -152,6 +152,7 @@ public:
     static constexpr size_t kEagerHead = 3072;  // 4 rounds of the throughput kernel (3 x 256 CUs)
     // nothing pending and no eager batch since the last flush (radix_mul_many's early head launch)
     bool eager_head_ok() const { return eager_ok_ && pending_.empty(); }
+    bool no_eager() const { return no_eager_; }
     // statistics
     uint64_t pbs_count = 0, levels = 0, fanout_levels = 0;
     uint64_t dead_nodes = 0;  // recorded bootstraps dropped at flush: nothing could read their outputs
@@ -175,6 +176,7 @@ private:
     std::vector<uint8_t> in_deg_;              // gstats_: max input value of each pending node
     std::vector<std::string> in_key_;          // gstats_: the node's input (terms + constant)
     int sched_ = 0;
+    bool no_eager_ = false;
     int round_ = 256;  // level fill granule (bootstraps per GPU)
     double run_ns_ = 0.0;  // host time inside run() (trace)
     size_t run_calls_ = 0;

@@ -258,3 +258,31 @@ def test_biguint_compat_uneven_limbs(keys):
             want = R.biguint_mul(al, bl)
             assert a.mul(b, COMPAT).decrypt_limbs(ck) == want, (la, lb, trial)
             assert a.mul_add(b, k, COMPAT).decrypt_limbs(ck) == R.biguint_add(kl, want), (la, lb, trial)
+
+
+def test_biguint_compat_chain_shapes_and_boundaries(keys):
+    """The compat carry-count chain (csrc/compat_chain.cpp) on the GPU: shapes 2x8, 8x2 and 8x12 (the
+    shorter side decides), limbs at the 2^32 boundaries the chain's near / g logic keys on (2^32 - 1,
+    - 2, - 16, - 17, 15, 16), and the same products through the dependency-wave form
+    (FHE_COMPAT_WAVES=1, r4) -- equal decrypted limbs, equal to the reference's loop; 9x9 (outside the
+    chain's range) goes through the waves."""
+    import os
+    ck, _ = keys
+    M = 1 << 32
+    special = [M - 1, M - 2, M - 16, M - 17, 15, 16, 0]
+    rng = random.Random(0xC4A1)
+    cases = [(2, 8), (8, 2), (8, 12), (9, 9)]
+    for la, lb in cases:
+        al = [rng.choice(special + [rng.getrandbits(32)]) for _ in range(la)]
+        bl = [rng.choice(special + [rng.getrandbits(32)]) for _ in range(lb)]
+        al[-1] |= 1  # no leading zero limb (BigUintFHE::new drops them)
+        bl[-1] |= 1
+        want = R.biguint_mul(al, bl)
+        a, b = _big(ck, al), _big(ck, bl)
+        got = a.mul(b, COMPAT).decrypt_limbs(ck)
+        os.environ["FHE_COMPAT_WAVES"] = "1"
+        try:
+            waves = a.mul(b, COMPAT).decrypt_limbs(ck)
+        finally:
+            del os.environ["FHE_COMPAT_WAVES"]
+        assert got == want and waves == want, (la, lb)
