@@ -1503,6 +1503,62 @@ static void add_products(const Radix& a, const Radix& b, uint32_t nblocks, std::
 static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                             uint32_t nblocks, const std::vector<const Radix*>& addends);
 
+// An encrypted a times a PUBLIC b (every block of b trivial): no bootstrap at all, every product
+// entry is a lazy multiple of a block of a.  b's base-4 digits are recoded to {-1, 0, 1, 2} (a digit 3
+// becomes -1 with a carry into the next digit), and -x enters as the complement 3 - x with -3 in a
+// public constant, so the entries are x, 2x or 3 - x: degree <= 6 and noise <= 4 instead of 3x
+// (degree 9, noise 9), which the column compression packs twice as densely -- a 256-bit radix times
+// a 257-bit multiplier (radix_scalar_div) compresses with ~12.6k bootstraps in 5 rounds instead of
+// ~24.2k in 6 (tools/compress_sim.py).  The public constant (the -3's and the products of a's
+// trivial blocks) is reduced mod 4^nblocks and added as trivial column entries.
+static bool recode_public() {  // FHE_SCALAR_RECODE=0: the plain digits (read per call: same-process A/Bs)
+    const char* v = getenv("FHE_SCALAR_RECODE");
+    return !v || atoi(v) != 0;
+}
+
+static void scalar_products(const Radix& a, const Radix& b, uint32_t nblocks,
+                            std::vector<std::pair<uint32_t, Block>>& direct) {
+    // recoded digits of b, one more than b has (the last carry)
+    std::vector<int32_t> t;
+    int32_t carry = 0;
+    for (uint32_t q = 0; q <= b.nblocks(); ++q) {
+        int32_t v = (q < b.nblocks() ? (int32_t)b.blocks[q].value : 0) + carry;
+        carry = 0;
+        if (v >= 3) {
+            v -= 4;
+            carry = 1;
+        }
+        t.push_back(v);
+    }
+    std::vector<int64_t> kc(nblocks + 1, 0);  // signed public constant per column
+    for (uint32_t p = 0; p < a.nblocks() && p < nblocks; ++p) {
+        const Block& x = a.blocks[p];
+        for (uint32_t q = 0; q < t.size() && p + q < nblocks; ++q) {
+            if (t[q] == 0) continue;
+            if (x.trivial()) {
+                kc[p + q] += (int64_t)t[q] * x.value;
+                continue;
+            }
+            engine_check(x.degree <= 3 && !x.lazy(), "mul needs clean operands");
+            if (t[q] == 1)
+                direct.push_back({p + q, x});
+            else if (t[q] == 2)
+                direct.push_back({p + q, block_lazy({{x, 2}}, 0, 2 * x.degree)});
+            else {  // -x = (3 - x) - 3
+                direct.push_back({p + q, block_lazy({{x, -1}}, 3, 3)});
+                kc[p + q] -= 3;
+            }
+        }
+    }
+    // kc mod 4^nblocks as base-4 digits (floor division carries the sign up)
+    for (uint32_t k = 0; k < nblocks; ++k) {
+        int64_t c = kc[k] >= 0 ? kc[k] / 4 : -((-kc[k] + 3) / 4);
+        kc[k] -= 4 * c;
+        kc[k + 1] += c;
+        if (kc[k]) direct.push_back({k, Block::make_trivial((uint32_t)kc[k])});
+    }
+}
+
 std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                   uint32_t nblocks, const std::vector<const Radix*>& addends) {
     std::vector<ColProblem> probs = mul_problems(e, ops, nblocks, addends);
@@ -1537,7 +1593,19 @@ static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pa
     Blocks outs;
     for (size_t i = 0; i < ops.size(); ++i) {
         start[i] = outs.size() + items.size();
-        add_products(*ops[i].first, *ops[i].second, nblocks, items, cols_of, direct[i]);
+        const Radix* pa = ops[i].first;
+        const Radix* pb = ops[i].second;
+        auto all_trivial = [](const Radix& r) {
+            for (const Block& b : r.blocks)
+                if (!b.trivial()) return false;
+            return true;
+        };
+        if (all_trivial(*pa) && !all_trivial(*pb)) std::swap(pa, pb);
+        if (all_trivial(*pb) && !all_trivial(*pa) && recode_public()) {
+            scalar_products(*pa, *pb, nblocks, direct[i]);
+            continue;
+        }
+        add_products(*pa, *pb, nblocks, items, cols_of, direct[i]);
         if (head && items.size() >= Engine::kEagerHead) {
             outs = e.run(items);
             e.flush();

@@ -109,3 +109,30 @@ def test_div256_by_encrypted(keys):
     a, b = rng.getrandbits(256) | 1 << 255, rng.getrandbits(128) | 1 << 127
     q, r = FheUint256.try_encrypt(a, ck).div_rem(FheUint256.try_encrypt(b, ck))
     assert (q.decrypt(ck), r.decrypt(ck)) == (a // b, a % b)
+
+
+def test_public_scalar_recoding(keys):
+    """Products with a public operand recode its base-4 digits to {-1, 0, 1, 2} (csrc/radix.cpp
+    scalar_products: -x as 3 - x with a public -3): multipliers made of 3-digits (2^k - 1), mixed
+    ones, wrap-around widths, multiply-add and the Granlund-Montgomery divisions that use them --
+    equal to exact integer arithmetic and to the plain-digit form (FHE_SCALAR_RECODE=0)."""
+    import os
+    ck, _ = keys
+    rng = random.Random(0x5CA1)
+    m = (1 << 128) - 1
+    a = rng.getrandbits(128) | 1 << 127
+    A = FheUint128.try_encrypt(a, ck)
+    cases = [(1 << 128) - 1, (1 << 127) - 1, 0xFFFF_0000_FFFF_3333_3333_FFFF_0001_0003, 3, 0xF,
+             rng.getrandbits(128)]
+    for s in cases:
+        got = [(A * s).decrypt(ck), A.scalar_mul_add(s, 0x3FFF).decrypt(ck)]
+        os.environ["FHE_SCALAR_RECODE"] = "0"
+        try:
+            plain = [(A * s).decrypt(ck), A.scalar_mul_add(s, 0x3FFF).decrypt(ck)]
+        finally:
+            del os.environ["FHE_SCALAR_RECODE"]
+        want = [(a * s) & m, (a * s + 0x3FFF) & m]
+        assert got == want and plain == want, hex(s)
+    for d in (3, 5, 0xFFFFFFFF, (1 << 64) - 59, (1 << 127) + 1):
+        assert (A / d).decrypt(ck) == a // d, hex(d)
+        assert (A % d).decrypt(ck) == a % d, hex(d)
