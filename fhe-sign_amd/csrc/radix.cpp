@@ -1820,21 +1820,31 @@ Radix radix_scalar_div(Engine& e, const Radix& a, const BigConst& dd) {
 }
 
 Radix radix_sub(Engine& e, const Radix& a, const Radix& b) {
-    // a - b = a + ~b + 1 (mod 2^bits): ~b_k = 3 - b_k folded into the column sums
+    // a - b = a + ~b + 1 (mod 2^bits): ~b_k = 3 - b_k folded into the column sums as a lazy term
+    // (noise 1, no bootstrap: the complement level of rounds 1-4 is gone); a lazy or noisy b_k is
+    // complemented through an identity-range lookup instead
     const uint32_t n = a.nblocks();
     std::vector<Blocks> cols(n);
-    std::vector<PbsItem> items;  // complement blocks, materialized through identity-range LUTs
+    std::vector<PbsItem> items;
+    std::vector<uint32_t> at;
     for (uint32_t k = 0; k < n; ++k) {
         cols[k].push_back(a.blocks[k]);
         const Block bk = k < b.nblocks() ? b.blocks[k] : Block::make_trivial(0);
-        PbsItem it;
-        it.terms = {{bk, -1}};
-        it.cst = 3;
-        it.table = lut1([](uint32_t v) { return v & 3; });
-        items.push_back(it);
+        if (bk.trivial()) {
+            cols[k].push_back(Block::make_trivial(3 - std::min<uint32_t>(bk.value, 3)));
+        } else if (!bk.lazy() && bk.degree <= 3 && bk.noise <= 1) {
+            cols[k].push_back(block_lazy({{bk, -1}}, 3, 3));
+        } else {
+            PbsItem it;
+            it.terms = {{bk, -1}};
+            it.cst = 3;
+            it.table = lut1([](uint32_t v) { return v & 3; });
+            items.push_back(it);
+            at.push_back(k);
+        }
     }
     Blocks nb = e.run(items);
-    for (uint32_t k = 0; k < n; ++k) cols[k].push_back(nb[k]);
+    for (size_t i = 0; i < at.size(); ++i) cols[at[i]].push_back(nb[i]);
     cols[0].push_back(Block::make_trivial(1));
     return radix_propagate_columns(e, std::move(cols), n);
 }
