@@ -1977,8 +1977,95 @@ static Radix barrel(Engine& e, const Radix& a, const Radix& amount, bool right) 
     return r;
 }
 
-Radix radix_shr(Engine& e, const Radix& a, const Radix& amount) { return barrel(e, a, amount, true); }
-Radix radix_shl(Engine& e, const Radix& a, const Radix& amount) { return barrel(e, a, amount, false); }
+// The same shifter with 4-way stages: an amount BLOCK (two amount bits) selects one of four sources
+// per output block through four half-selects f_c(4 amt + src_c) (the sum of the previous stage's four
+// half-selects enters lazily: noise 16 + 4), so 8 amount bits take 4 stages instead of 8, the
+// amount's blocks need no bit-extraction level, and only an odd top bit takes a 2-way stage (its bit
+// extracted in the first level, beside the 1-bit-shifted copy).  Stage 0 (bits 0, 1) picks among x,
+// x >> 1 bit, x >> 1 block, x >> 1 block + 1 bit; stage j > 0 among x >> c 2^(2j-1) blocks.
+static Radix barrel4(Engine& e, const Radix& a, const Radix& amount, bool right) {
+    const uint32_t n = a.nblocks(), bitsw = 2 * n;
+    uint32_t nbits = 0;
+    while ((1u << nbits) < bitsw) ++nbits;
+    const uint32_t quads = nbits / 2;
+    const bool odd = nbits % 2;
+    const int64_t dir = right ? 1 : -1;
+    auto amt_block = [&](uint32_t j) { return j < amount.nblocks() ? amount.blocks[j] : Block::make_trivial(0); };
+    auto at = [&](const Blocks& v, int64_t k) { return (k >= 0 && k < (int64_t)n) ? v[k] : Block::make_trivial(0); };
+    static const auto LUT_SHR1 = lut2([](uint32_t hi, uint32_t lo) { return ((hi & 1) << 1) | (lo >> 1); });
+    static const auto LUT_SHL1 = lut2([](uint32_t hi, uint32_t lo) { return ((hi << 1) & 3) | (lo >> 1); });
+    // level 1: the 1-bit shifted copy; the odd top amount bit
+    std::vector<PbsItem> items;
+    for (uint32_t k = 0; k < n; ++k) {
+        if (right)
+            items.push_back(item2(at(a.blocks, k + 1), a.blocks[k], LUT_SHR1));
+        else
+            items.push_back(item2(a.blocks[k], at(a.blocks, (int64_t)k - 1), LUT_SHL1));
+    }
+    if (odd) items.push_back(item1(amt_block(quads), lut1([](uint32_t v) { return v & 1u; })));
+    Blocks o = e.run(items);
+    const Blocks sh1(o.begin(), o.begin() + n);
+    const Block topbit = odd ? o[n] : Block::make_trivial(0);
+    static std::vector<std::vector<uint32_t>> sel4;
+    if (sel4.empty())
+        for (uint32_t c = 0; c < 4; ++c) sel4.push_back(lut1([c](uint32_t v) { return (v >> 2) == c ? v & 3 : 0u; }));
+    static const auto LUT_IF = lut2([](uint32_t c, uint32_t v) { return c ? v : 0u; });
+    static const auto LUT_IFNOT = lut2([](uint32_t c, uint32_t v) { return c ? 0u : v; });
+    auto sel = [](const Block& c, const Block& v, const std::vector<uint32_t>& t) {
+        PbsItem it;
+        it.terms = {{c, 4}, {v, 1}};
+        it.table = t;
+        return it;
+    };
+    // exactly one half-select of a position is nonzero: their sum (lazy) stays within [0, 3]
+    auto lazy_sums = [&](const Blocks& h, uint32_t ways) {
+        Blocks r(n);
+        for (uint32_t k = 0; k < n; ++k) {
+            std::vector<Term> t;
+            for (uint32_t c = 0; c < ways; ++c) t.push_back({h[ways * k + c], 1});
+            r[k] = block_lazy(t, 0, 3);
+        }
+        return r;
+    };
+    Blocks cur = a.blocks;
+    for (uint32_t j = 0; j < quads; ++j) {
+        const Block amt = amt_block(j);
+        std::vector<PbsItem> its;
+        for (uint32_t k = 0; k < n; ++k)
+            for (uint32_t c = 0; c < 4; ++c) {
+                Block src;
+                if (j == 0) {  // bit shifts 0..3 of the original blocks
+                    const int64_t kb = (int64_t)k + dir * (int64_t)(c / 2);
+                    src = c % 2 == 0 ? at(a.blocks, kb) : at(sh1, kb);
+                } else {  // c 4^j bits = c 2^(2j-1) blocks
+                    src = at(cur, (int64_t)k + dir * ((int64_t)c << (2 * j - 1)));
+                }
+                its.push_back(sel(amt, src, sel4[c]));
+            }
+        cur = lazy_sums(e.run(its), 4);
+    }
+    if (odd) {  // the top amount bit: 2^(nbits-1) bits = 2^(nbits-2) blocks
+        const int64_t s = (int64_t)1 << (nbits - 2);
+        std::vector<PbsItem> its;
+        for (uint32_t k = 0; k < n; ++k) {
+            its.push_back(sel(topbit, cur[k], LUT_IFNOT));
+            its.push_back(sel(topbit, at(cur, (int64_t)k + dir * s), LUT_IF));
+        }
+        cur = lazy_sums(e.run(its), 2);
+    }
+    return radix_clean(e, Radix{cur});
+}
+
+static bool barrel_4way() {  // FHE_BARREL4=0: the 2-way shifter (same-process A/Bs)
+    const char* v = getenv("FHE_BARREL4");
+    return !v || atoi(v) != 0;
+}
+Radix radix_shr(Engine& e, const Radix& a, const Radix& amount) {
+    return barrel_4way() && a.nblocks() >= 2 ? barrel4(e, a, amount, true) : barrel(e, a, amount, true);
+}
+Radix radix_shl(Engine& e, const Radix& a, const Radix& amount) {
+    return barrel_4way() && a.nblocks() >= 2 ? barrel4(e, a, amount, false) : barrel(e, a, amount, false);
+}
 
 Radix radix_bitand(Engine& e, const Radix& a, const Radix& b) {
     static const auto LUT_AND = lut2([](uint32_t x, uint32_t y) { return x & y; });
