@@ -121,7 +121,7 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
         for (auto& cols : PC)
             for (auto& c : cols)
                 for (Block& b : c)
-                    if (!b.trivial() && (b.lazy() || b.noise > 1)) {
+                    if (!b.trivial() && (b.noise > 1 || (b.lazy() && b.lin->size() > 1))) {
                         items.push_back(item({{b, 1}}, ID));
                         at.push_back(&b);
                     }

@@ -15,6 +15,8 @@
 #include "radix.h"
 
 #include <algorithm>
+#include <array>
+#include <deque>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -1577,8 +1579,156 @@ std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
     return res;
 }
 
+// Karatsuba split of a full product of two encrypted n-block operands (n >= FHE_KARA_MIN blocks,
+// default 16; FHE_KARATSUBA=0 turns it off; both read per call for same-process A/Bs):
+//   a b = z0 + X^2 z2 + X (m - z0 - z2),  X = 4^h, h = ceil(n / 2),
+//   z0 = a0 b0, z2 = a1 b1, m = (a0 + a1)(b0 + b1)  (the sums propagated to h + 1 clean blocks),
+// 3 products of ~h^2 block pairs instead of 4.  The three sub-products (split again while large
+// enough) are compressed on their own to <= 3 blocks per column before they are combined, so the
+// two subtracted copies add a few blocks per column, not a product's worth: -x enters as the
+// complement (deg x - x) with -deg x in a public constant, as in scalar_products.  Only for full
+// products (nblocks >= 2n: nothing truncated) whose blocks are all encrypted.
+static bool karatsuba_on() {
+    const char* v = getenv("FHE_KARATSUBA");
+    return !v || atoi(v) != 0;
+}
+static uint32_t kara_min() {
+    const char* v = getenv("FHE_KARA_MIN");
+    return v && atoi(v) >= 4 ? (uint32_t)atoi(v) : 16u;
+}
+// blocks below the top run of trivial zeros
+static uint32_t live_len(const Radix& r) {
+    uint32_t n = r.nblocks();
+    while (n > 0 && r.blocks[n - 1].trivial() && r.blocks[n - 1].value == 0) --n;
+    return n;
+}
+static bool kara_eligible(const Radix& a, const Radix& b, uint32_t nblocks) {
+    const uint32_t n = live_len(a);
+    if (!karatsuba_on() || n != live_len(b) || n < kara_min() || nblocks < 2 * n) return false;
+    // FHE_KARA_FORCE=1 (CPU tests): split publicly known operands too, so that the host-folding
+    // engine checks the split's algebra (offsets, complements, constants) on known values
+    const char* fv = getenv("FHE_KARA_FORCE");
+    const bool force = fv && atoi(fv) != 0;
+    for (const Radix* r : {&a, &b})
+        for (uint32_t k = 0; k < n; ++k) {
+            const Block& x = r->blocks[k];
+            if ((x.trivial() && !force) || x.lazy() || x.degree > 3) return false;
+        }
+    return true;
+}
+
+struct MulOp {
+    const Radix* a;
+    const Radix* b;
+    uint32_t nblocks;
+};
+static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<MulOp>& ops,
+                                                const std::vector<const Radix*>& addends);
+
 static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                             uint32_t nblocks, const std::vector<const Radix*>& addends) {
+    std::vector<MulOp> m;
+    for (auto& op : ops) m.push_back({op.first, op.second, nblocks});
+    return mul_problems_ops(e, m, addends);
+}
+
+// -x as a column entry: (deg - x) with -deg (times the column weight) into the public constant
+static void push_signed(Blocks& col, int64_t& kc, const Block& b, int sign) {
+    if (b.trivial()) {
+        kc += sign * (int64_t)b.value;
+        return;
+    }
+    if (sign > 0) {
+        col.push_back(b);
+        return;
+    }
+    const int32_t deg = (int32_t)b.degree;
+    if (b.lazy()) {  // flatten: -(sum c_t x_t + c) + deg
+        std::vector<Term> t;
+        for (const Term& x : *b.lin) t.push_back({x.b, -x.coef});
+        col.push_back(block_lazy(t, deg - b.lin_cst, b.degree));
+    } else {
+        col.push_back(block_lazy({{b, -1}}, deg, b.degree));
+    }
+    kc -= deg;
+}
+
+static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<MulOp>& ops,
+                                                const std::vector<const Radix*>& addends) {
+    std::vector<size_t> kara, plain;
+    for (size_t i = 0; i < ops.size(); ++i)
+        (kara_eligible(*ops[i].a, *ops[i].b, ops[i].nblocks) ? kara : plain).push_back(i);
+    std::vector<ColProblem> out(ops.size());
+    if (!kara.empty()) {
+        // halves and (memoized: compat's limb products share operands) normalized half sums
+        std::deque<Radix> store;
+        std::map<const Radix*, std::array<const Radix*, 3>> parts;  // lo, hi, lo + hi
+        auto halves = [&](const Radix* r) {
+            auto it = parts.find(r);
+            if (it != parts.end()) return;
+            const uint32_t n = live_len(*r), h = (n + 1) / 2;
+            Radix lo, hi;
+            lo.blocks.assign(r->blocks.begin(), r->blocks.begin() + h);
+            hi.blocks.assign(r->blocks.begin() + h, r->blocks.begin() + n);
+            store.push_back(std::move(lo));
+            const Radix* plo = &store.back();
+            store.push_back(std::move(hi));
+            parts[r] = {plo, &store.back(), nullptr};
+        };
+        for (size_t i : kara) {
+            halves(ops[i].a);
+            halves(ops[i].b);
+        }
+        // z0, z2 first (nothing to wait for: the eager head), then the sums, then m
+        std::vector<MulOp> zops;
+        for (size_t i : kara) {
+            const uint32_t n = live_len(*ops[i].a), h = (n + 1) / 2;
+            const auto &pa = parts[ops[i].a], &pb = parts[ops[i].b];
+            zops.push_back({pa[0], pb[0], 2 * h});
+            zops.push_back({pa[1], pb[1], 2 * (n - h)});
+        }
+        std::vector<ColProblem> zp = mul_problems_ops(e, zops, {});
+        for (auto& kv : parts) {
+            const uint32_t h = kv.second[0]->nblocks();
+            store.push_back(radix_sum(e, {kv.second[0], kv.second[1]}, h + 1));
+            kv.second[2] = &store.back();
+        }
+        std::vector<MulOp> mops;
+        for (size_t i : kara) {
+            const uint32_t h = parts[ops[i].a][0]->nblocks();
+            mops.push_back({parts[ops[i].a][2], parts[ops[i].b][2], 2 * h + 2});
+        }
+        std::vector<ColProblem> mp = mul_problems_ops(e, mops, {});
+        std::vector<ColProblem*> ptrs;
+        for (auto& p : zp) ptrs.push_back(&p);
+        for (auto& p : mp) ptrs.push_back(&p);
+        compress_columns(e, ptrs);
+        for (size_t j = 0; j < kara.size(); ++j) {
+            const size_t i = kara[j];
+            const uint32_t N = ops[i].nblocks, h = parts[ops[i].a][0]->nblocks();
+            ColProblem& P = out[i];
+            P.nblocks = N;
+            P.cols.assign(N, {});
+            std::vector<int64_t> kc(N + 1, 0);
+            auto add = [&](const ColProblem& Z, uint32_t off, int sign) {
+                for (uint32_t k = 0; k < Z.nblocks; ++k)
+                    for (const Block& b : Z.cols[k])
+                        if (k + off < N) push_signed(P.cols[k + off], kc[k + off], b, sign);
+            };
+            add(zp[2 * j], 0, 1);
+            add(zp[2 * j + 1], 2 * h, 1);
+            add(mp[j], h, 1);
+            add(zp[2 * j], h, -1);
+            add(zp[2 * j + 1], h, -1);
+            // the constant mod 4^N as base-4 digits (floor division carries the sign up)
+            for (uint32_t k = 0; k < N; ++k) {
+                const int64_t c = kc[k] >= 0 ? kc[k] / 4 : -((-kc[k] + 3) / 4);
+                kc[k] -= 4 * c;
+                kc[k + 1] += c;
+                if (kc[k]) P.cols[k].push_back(Block::make_trivial((uint32_t)kc[k]));
+            }
+        }
+    }
     std::vector<PbsItem> items;
     std::vector<uint32_t> cols_of;
     std::vector<std::vector<std::pair<uint32_t, Block>>> direct(ops.size());
@@ -1588,13 +1738,15 @@ static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pa
     // GPU starts ~1 ms into the call instead of after the whole batch's host work (6-16 ms for the
     // compat 256-bit mul's 32768 block products); the rest follows as the engine's eager batch.
     size_t est = 0;
-    for (auto& op : ops) est += (size_t)op.first->nblocks() * op.second->nblocks();
+    for (size_t i : plain) est += (size_t)ops[i].a->nblocks() * ops[i].b->nblocks();
     bool head = e.eager_head_ok() && !e.no_eager() && est >= 4 * Engine::kEagerHead;
     Blocks outs;
-    for (size_t i = 0; i < ops.size(); ++i) {
-        start[i] = outs.size() + items.size();
-        const Radix* pa = ops[i].first;
-        const Radix* pb = ops[i].second;
+    std::vector<size_t> first(ops.size(), 0), last(ops.size(), 0);
+    for (size_t i : plain) {
+        first[i] = outs.size() + items.size();
+        const Radix* pa = ops[i].a;
+        const Radix* pb = ops[i].b;
+        const uint32_t nblocks = ops[i].nblocks;
         auto all_trivial = [](const Radix& r) {
             for (const Block& b : r.blocks)
                 if (!b.trivial()) return false;
@@ -1603,9 +1755,11 @@ static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pa
         if (all_trivial(*pa) && !all_trivial(*pb)) std::swap(pa, pb);
         if (all_trivial(*pb) && !all_trivial(*pa) && recode_public()) {
             scalar_products(*pa, *pb, nblocks, direct[i]);
+            last[i] = first[i];
             continue;
         }
         add_products(*pa, *pb, nblocks, items, cols_of, direct[i]);
+        last[i] = outs.size() + items.size();
         if (head && items.size() >= Engine::kEagerHead) {
             outs = e.run(items);
             e.flush();
@@ -1613,22 +1767,22 @@ static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pa
             head = false;
         }
     }
-    start[ops.size()] = outs.size() + items.size();
     {
         Blocks rest = e.run(items);
         outs.insert(outs.end(), rest.begin(), rest.end());
     }
-    std::vector<ColProblem> probs(ops.size());
-    for (size_t i = 0; i < ops.size(); ++i) {
-        probs[i].nblocks = nblocks;
-        probs[i].cols.assign(nblocks, {});
-        for (size_t j = start[i]; j < start[i + 1]; ++j) probs[i].cols[cols_of[j]].push_back(outs[j]);
-        for (auto& d : direct[i]) probs[i].cols[d.first].push_back(d.second);
-        if (i < addends.size() && addends[i])
-            for (uint32_t k = 0; k < nblocks && k < addends[i]->nblocks(); ++k)
-                probs[i].cols[k].push_back(addends[i]->blocks[k]);
+    for (size_t i : plain) {
+        ColProblem& P = out[i];
+        P.nblocks = ops[i].nblocks;
+        P.cols.assign(P.nblocks, {});
+        for (size_t j = first[i]; j < last[i]; ++j) P.cols[cols_of[j]].push_back(outs[j]);
+        for (auto& d : direct[i]) P.cols[d.first].push_back(d.second);
     }
-    return probs;
+    for (size_t i = 0; i < ops.size() && i < addends.size(); ++i)
+        if (addends[i])
+            for (uint32_t k = 0; k < out[i].nblocks && k < addends[i]->nblocks(); ++k)
+                out[i].cols[k].push_back(addends[i]->blocks[k]);
+    return out;
 }
 
 Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {

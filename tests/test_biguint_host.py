@@ -81,3 +81,21 @@ def test_fast_and_mul_add():
         k = [rng.getrandbits(32) for _ in range(8)]
         assert R.from_limbs(host_mul(a, b, FAST)) == R.from_limbs(a) * R.from_limbs(b)
         assert host_mul(a, b, COMPAT, k) == R.biguint_add(k, R.biguint_mul(a, b))
+
+
+@pytest.mark.parametrize("kmin", [4, 7, 16])
+def test_karatsuba_split_algebra(monkeypatch, kmin):
+    """The Karatsuba split of full products (csrc/radix.cpp mul_problems_ops) forced onto publicly known
+    operands (FHE_KARA_FORCE): its offsets, complements and public constants, recursion down to kmin
+    blocks, odd halves and trimmed zero tops, against the reference limb loop in both modes."""
+    monkeypatch.setenv("FHE_KARA_FORCE", "1")
+    monkeypatch.setenv("FHE_KARA_MIN", str(kmin))
+    for a, b in _cases(77 + kmin, 12):
+        assert R.from_limbs(host_mul(a, b, FAST)) == R.from_limbs(a) * R.from_limbs(b)
+        assert host_mul(a, b, COMPAT) == R.biguint_mul(a, b)
+    full = [M - 1] * 8
+    assert R.from_limbs(host_mul(full, full, FAST)) == R.from_limbs(full) ** 2
+    assert host_mul(full, full, COMPAT) == R.biguint_mul(full, full)
+    k = [M - 1, 3, 0, M - 2]
+    assert host_mul(full, full, COMPAT, k) == R.biguint_add(k, R.biguint_mul(full, full))
+    assert R.from_limbs(host_mul(full, full, FAST, k)) == R.from_limbs(full) ** 2 + R.from_limbs(k)
