@@ -660,6 +660,99 @@ int fhe_host_radix_stats(int op, uint32_t bits, uint64_t* pbs, uint64_t* levels,
     });
 }
 
+// Simulated runs (no GPU, no key; Engine kSim): the operands are "encrypted" blocks whose plaintext
+// the engine shadows on the host, so the algorithms take every encrypted path (no trivial folding)
+// while each bootstrap is evaluated from its LUT and range-checked -- the end-to-end results of the
+// radix algorithms on the CPU.  *pbs / *levels (optional): the op's schedule, as fhe_host_*_stats.
+int fhe_host_sim_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k, size_t lk,
+                             int mode, uint32_t* out, size_t cap, size_t* n, uint64_t* pbs, uint64_t* levels) {
+    if ((la && !a) || (lb && !b) || (lk && !k) || !n || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
+    return guarded([&] {
+        fhe_ctx c;
+        Engine e(&c, Engine::kSim);
+        auto make = [&](const uint32_t* v, size_t n) {
+            BigUint r;
+            for (size_t i = 0; i < n; ++i) {
+                Radix d;
+                for (uint32_t q = 0; q < kLimbBlocks; ++q) d.blocks.push_back(e.sim_block((v[i] >> (2 * q)) & 3u, 3));
+                r.digits.push_back(std::move(d));
+            }
+            return r;
+        };
+        const BigUint A = make(a, la), B = make(b, lb);
+        const BigUint R = k ? biguint_mul_add(e, A, B, make(k, lk), mode) : biguint_mul(e, A, B, mode);
+        e.flush();
+        *n = R.digits.size();
+        engine_check(R.digits.size() <= cap || !out, "output buffer too small");
+        for (size_t i = 0; out && i < R.digits.size(); ++i) {
+            uint64_t v = 0;
+            for (uint32_t q = 0; q < R.digits[i].nblocks(); ++q) {
+                const int64_t h2 = e.sim_half2(R.digits[i].blocks[q]);
+                engine_check(h2 % 2 == 0 && h2 >= 0 && h2 < 8, "sim mul: an output block off its digit range");
+                v |= (uint64_t)(h2 / 2) << (2 * q);
+            }
+            out[i] = (uint32_t)v;
+        }
+        if (pbs) *pbs = e.pbs_count;
+        if (levels) *levels = e.levels;
+        return FHE_OK;
+    });
+}
+
+// One radix op (FHE_HOST_OP_*) on simulated operands a, b of `bits` (words LSB first, ceil(bits / 64)
+// each); out gets the result (MUL_FULL: 2 bits wide; LT / the comparison: 0 or 1 in out[0]); out2 the
+// remainder of DIVREM.
+int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t* b, uint64_t* out, uint64_t* out2,
+                       uint64_t* pbs, uint64_t* levels) {
+    if (!a || !b || !out || bits < 2 || bits % 2 || bits > FHE_RADIX_MAX_BITS) return FHE_ERR_INVALID;
+    if (op == FHE_HOST_OP_DIVREM && !out2) return FHE_ERR_INVALID;
+    return guarded([&] {
+        fhe_ctx c;
+        Engine e(&c, Engine::kSim);
+        const uint32_t nb = bits / 2;
+        auto make = [&](const uint64_t* w) {
+            Radix r;
+            for (uint32_t q = 0; q < nb; ++q) r.blocks.push_back(e.sim_block((uint32_t)(w[q / 32] >> (2 * (q % 32))) & 3u, 3));
+            return r;
+        };
+        const Radix A = make(a), B = make(b);
+        std::vector<Radix> keep;
+        switch (op) {
+        case FHE_HOST_OP_DIVREM: {
+            auto qr = radix_divrem(e, A, B);
+            keep = {qr.first, qr.second};
+            break;
+        }
+        case FHE_HOST_OP_MUL: keep = {radix_mul(e, A, B, nb)}; break;
+        case FHE_HOST_OP_ADD: keep = {radix_sum(e, {&A, &B}, nb)}; break;
+        case FHE_HOST_OP_SUB: keep = {radix_sub(e, A, B)}; break;
+        case FHE_HOST_OP_SHR: keep = {radix_shr(e, A, B)}; break;
+        case FHE_HOST_OP_LT: keep = {Radix{{radix_lt(e, A, B)}}}; break;
+        case FHE_HOST_OP_DIV_SCALAR: keep = {radix_scalar_div(e, A, BigConst{0xC0FFEE01u})}; break;
+        case FHE_HOST_OP_SHL: keep = {radix_shl(e, A, B)}; break;
+        case FHE_HOST_OP_MUL_FULL: keep = {radix_mul(e, A, B, 2 * nb)}; break;
+        case FHE_HOST_OP_AND: keep = {radix_bitand(e, A, B)}; break;
+        case FHE_HOST_OP_MIN: keep = {radix_min(e, A, B)}; break;
+        default: engine_check(false, "unknown host op");
+        }
+        e.flush();
+        auto put = [&](const Radix& r, uint64_t* w) {
+            const size_t words = (r.nblocks() + 31) / 32;
+            for (size_t i = 0; i < words; ++i) w[i] = 0;
+            for (uint32_t q = 0; q < r.nblocks(); ++q) {
+                const int64_t h2 = e.sim_half2(r.blocks[q]);
+                engine_check(h2 % 2 == 0 && h2 >= 0 && h2 < 8, "sim radix: an output block off its digit range");
+                w[q / 32] |= (uint64_t)(h2 / 2) << (2 * (q % 32));
+            }
+        };
+        put(keep[0], out);
+        if (op == FHE_HOST_OP_DIVREM) put(keep[1], out2);
+        if (pbs) *pbs = e.pbs_count;
+        if (levels) *levels = e.levels;
+        return FHE_OK;
+    });
+}
+
 int fhe_biguint_mul_add(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, const fhe_biguint* k, int mode,
                         fhe_biguint** out) {
     int rc = need_engine(c);

@@ -76,7 +76,7 @@ std::shared_ptr<Slot> BlockPool::alloc() {
 
 // ============================================================================ engine
 Engine::Engine(fhe_ctx* ctx, int host_mode) : ctx_(ctx), host_mode_(host_mode) {
-    pool_ = std::make_shared<BlockPool>(ctx->device, host_mode_ == kDry);
+    pool_ = std::make_shared<BlockPool>(ctx->device, host_mode_ == kDry || host_mode_ == kSim);
     if (host_mode_ == kDevice)
         for (auto& ev : desc_ev_) hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
     // FHE_TRACE_LEVELS=1: synchronize after every level and print its size and wall time (stderr);
@@ -104,8 +104,27 @@ int32_t Engine::depth_of(const Block& b) const {
     return d;
 }
 
+Block Engine::sim_block(uint32_t value, uint32_t degree) {
+    engine_check(host_mode_ == kSim && value <= degree, "sim_block outside a simulating engine");
+    Block b = dry_block(degree);
+    sim_[b.ptr()] = 2 * (int64_t)value;
+    return b;
+}
+
+int64_t Engine::sim_half2(const Block& b) const {
+    if (b.trivial()) return trivial_half2(b);
+    if (b.lazy()) {
+        int64_t v = 2 * (int64_t)b.lin_cst;
+        for (const Term& t : *b.lin) v += (int64_t)t.coef * sim_half2(t.b);
+        return v;
+    }
+    auto it = sim_.find(b.ptr());
+    engine_check(it != sim_.end(), "sim: a block without a plaintext shadow");
+    return it->second;
+}
+
 Block Engine::dry_block(uint32_t degree) {
-    engine_check(host_mode_ == kDry, "dry_block outside a dry engine");
+    engine_check(host_mode_ == kDry || host_mode_ == kSim, "dry_block outside a dry engine");
     Block b;
     b.slot = pool_->alloc();
     b.degree = degree;
@@ -287,6 +306,20 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         else
             engine_check(ctx_->register_lut(items[i].table.data(), &lut) == FHE_OK, "LUT registration");
         out[i].slot = pool_->alloc();
+        if (host_mode_ == kSim) {  // the plaintext shadow of this bootstrap
+            int64_t v2 = raw ? csts[i] : 2 * csts[i];
+            for (const Term& t : live[i]) v2 += (int64_t)t.coef * sim_half2(t.b);
+            int64_t o2;
+            if (raw) {
+                engine_check(v2 % 2 == 0 && v2 >= -32 && v2 < 32, "sim: raw PBS input outside [-16, 16)");
+                const int64_t v = v2 / 2;
+                o2 = v >= 0 ? items[i].half_table[v] : -items[i].half_table[v + 16];
+            } else {
+                engine_check(v2 % 2 == 0 && v2 >= 0 && v2 < 2 * (int64_t)mc, "sim: PBS input outside the message space");
+                o2 = 2 * (int64_t)(items[i].table[v2 / 2] % mc);
+            }
+            sim_[out[i].ptr()] = o2;
+        }
         Pending n;
         PbsDesc& d = n.d;
         std::memset(&d, 0, sizeof d);
@@ -523,7 +556,7 @@ void Engine::flush() {
     // a fanned-out level's round is one latency-kernel round on every rank
     const size_t round = (size_t)round_ * (size_t)std::max(1, ctx_->fanout_world());
     std::vector<std::vector<int32_t>> lv = schedule_levels(deps, sched_, round);
-    if (host_mode_ == kDry) {  // the schedule's statistics, nothing launched
+    if (host_mode_ == kDry || host_mode_ == kSim) {  // the schedule's statistics, nothing launched
         for (auto& l : lv) {
             pbs_count += l.size();
             levels += 1;
@@ -1503,7 +1536,8 @@ static void add_products(const Radix& a, const Radix& b, uint32_t nblocks, std::
 }
 
 static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
-                                            uint32_t nblocks, const std::vector<const Radix*>& addends);
+                                            uint32_t nblocks, const std::vector<const Radix*>& addends,
+                                            bool kara_ok);
 
 // An encrypted a times a PUBLIC b (every block of b trivial): no bootstrap at all, every product
 // entry is a lazy multiple of a block of a.  b's base-4 digits are recoded to {-1, 0, 1, 2} (a digit 3
@@ -1563,14 +1597,14 @@ static void scalar_products(const Radix& a, const Radix& b, uint32_t nblocks,
 
 std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                   uint32_t nblocks, const std::vector<const Radix*>& addends) {
-    std::vector<ColProblem> probs = mul_problems(e, ops, nblocks, addends);
+    std::vector<ColProblem> probs = mul_problems(e, ops, nblocks, addends, true);
     return propagate_many(e, probs);
 }
 
 std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
                                                         const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                                         uint32_t nblocks) {
-    std::vector<ColProblem> probs = mul_problems(e, ops, nblocks, {});
+    std::vector<ColProblem> probs = mul_problems(e, ops, nblocks, {}, false);
     std::vector<ColProblem*> ptrs;
     for (auto& p : probs) ptrs.push_back(&p);
     compress_columns(e, ptrs);
@@ -1580,21 +1614,30 @@ std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
 }
 
 // Karatsuba split of a full product of two encrypted n-block operands (n >= FHE_KARA_MIN blocks,
-// default 16; FHE_KARATSUBA=0 turns it off; both read per call for same-process A/Bs):
+// default 24; FHE_KARATSUBA=0 turns it off; both read per call for same-process A/Bs):
 //   a b = z0 + X^2 z2 + X (m - z0 - z2),  X = 4^h, h = ceil(n / 2),
 //   z0 = a0 b0, z2 = a1 b1, m = (a0 + a1)(b0 + b1)  (the sums propagated to h + 1 clean blocks),
 // 3 products of ~h^2 block pairs instead of 4.  The three sub-products (split again while large
 // enough) are compressed on their own to <= 3 blocks per column before they are combined, so the
 // two subtracted copies add a few blocks per column, not a product's worth: -x enters as the
-// complement (deg x - x) with -deg x in a public constant, as in scalar_products.  Only for full
-// products (nblocks >= 2n: nothing truncated) whose blocks are all encrypted.
+// complement (deg x - x) with -deg x in a public constant, as in scalar_products.
+//
+// Exactness.  A column set whose public constant is negative cannot hold the value itself (its
+// entries are nonnegative): the top-level product is only needed mod 4^N (the carry propagation
+// drops everything above), but a sub-product is shifted by X before it is subtracted, so its
+// representation must be exact.  A sub-product with nominal width N is therefore kept on N + 2
+// columns as R = value + q 4^N with q = ceil(C / 4^N) <= 14 PUBLIC (C = the complements' constants):
+// R < 4^(N+2), so its compression never drops a nonzero carry, and the consumer subtracts q 4^N
+// (shifted) in its own public constant.  Only for full products (N >= 2n and room for m at X:
+// nothing truncated) whose blocks are all encrypted, and not for the compat chain's limb products
+// (radix_mul_many_columns), whose consumer needs the columns to sum to the product itself.
 static bool karatsuba_on() {
     const char* v = getenv("FHE_KARATSUBA");
     return !v || atoi(v) != 0;
 }
 static uint32_t kara_min() {
     const char* v = getenv("FHE_KARA_MIN");
-    return v && atoi(v) >= 4 ? (uint32_t)atoi(v) : 16u;
+    return v && atoi(v) >= 6 ? (uint32_t)atoi(v) : 24u;
 }
 // blocks below the top run of trivial zeros
 static uint32_t live_len(const Radix& r) {
@@ -1603,8 +1646,8 @@ static uint32_t live_len(const Radix& r) {
     return n;
 }
 static bool kara_eligible(const Radix& a, const Radix& b, uint32_t nblocks) {
-    const uint32_t n = live_len(a);
-    if (!karatsuba_on() || n != live_len(b) || n < kara_min() || nblocks < 2 * n) return false;
+    const uint32_t n = live_len(a), h = (n + 1) / 2;
+    if (!karatsuba_on() || n != live_len(b) || n < kara_min() || nblocks < 2 * n || nblocks < 3 * h + 3) return false;
     // FHE_KARA_FORCE=1 (CPU tests): split publicly known operands too, so that the host-folding
     // engine checks the split's algebra (offsets, complements, constants) on known values
     const char* fv = getenv("FHE_KARA_FORCE");
@@ -1622,14 +1665,19 @@ struct MulOp {
     const Radix* b;
     uint32_t nblocks;
 };
+// exact == nullptr: columns mod 4^nblocks (a carry propagation follows); else exact column sets,
+// (*exact)[i] = q_i: op i's columns (nblocks + 2 of them for a split product) sum to its product
+// + q_i 4^nblocks
 static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<MulOp>& ops,
-                                                const std::vector<const Radix*>& addends);
+                                                const std::vector<const Radix*>& addends, bool kara_ok,
+                                                std::vector<int64_t>* exact);
 
 static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
-                                            uint32_t nblocks, const std::vector<const Radix*>& addends) {
+                                            uint32_t nblocks, const std::vector<const Radix*>& addends,
+                                            bool kara_ok) {
     std::vector<MulOp> m;
     for (auto& op : ops) m.push_back({op.first, op.second, nblocks});
-    return mul_problems_ops(e, m, addends);
+    return mul_problems_ops(e, m, addends, kara_ok, nullptr);
 }
 
 // -x as a column entry: (deg - x) with -deg (times the column weight) into the public constant
@@ -1654,13 +1702,15 @@ static void push_signed(Blocks& col, int64_t& kc, const Block& b, int sign) {
 }
 
 static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<MulOp>& ops,
-                                                const std::vector<const Radix*>& addends) {
+                                                const std::vector<const Radix*>& addends, bool kara_ok,
+                                                std::vector<int64_t>* exact) {
     std::vector<size_t> kara, plain;
     for (size_t i = 0; i < ops.size(); ++i)
-        (kara_eligible(*ops[i].a, *ops[i].b, ops[i].nblocks) ? kara : plain).push_back(i);
+        (kara_ok && kara_eligible(*ops[i].a, *ops[i].b, ops[i].nblocks) ? kara : plain).push_back(i);
     std::vector<ColProblem> out(ops.size());
+    if (exact) exact->assign(ops.size(), 0);
     if (!kara.empty()) {
-        // halves and (memoized: compat's limb products share operands) normalized half sums
+        // halves and (memoized by operand) normalized half sums
         std::deque<Radix> store;
         std::map<const Radix*, std::array<const Radix*, 3>> parts;  // lo, hi, lo + hi
         auto halves = [&](const Radix* r) {
@@ -1687,7 +1737,8 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
             zops.push_back({pa[0], pb[0], 2 * h});
             zops.push_back({pa[1], pb[1], 2 * (n - h)});
         }
-        std::vector<ColProblem> zp = mul_problems_ops(e, zops, {});
+        std::vector<int64_t> zq, mq;
+        std::vector<ColProblem> zp = mul_problems_ops(e, zops, {}, true, &zq);
         for (auto& kv : parts) {
             const uint32_t h = kv.second[0]->nblocks();
             store.push_back(radix_sum(e, {kv.second[0], kv.second[1]}, h + 1));
@@ -1698,7 +1749,7 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
             const uint32_t h = parts[ops[i].a][0]->nblocks();
             mops.push_back({parts[ops[i].a][2], parts[ops[i].b][2], 2 * h + 2});
         }
-        std::vector<ColProblem> mp = mul_problems_ops(e, mops, {});
+        std::vector<ColProblem> mp = mul_problems_ops(e, mops, {}, true, &mq);
         std::vector<ColProblem*> ptrs;
         for (auto& p : zp) ptrs.push_back(&p);
         for (auto& p : mp) ptrs.push_back(&p);
@@ -1706,26 +1757,47 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
         for (size_t j = 0; j < kara.size(); ++j) {
             const size_t i = kara[j];
             const uint32_t N = ops[i].nblocks, h = parts[ops[i].a][0]->nblocks();
+            const uint32_t W = exact ? N + 2 : N;  // columns kept
             ColProblem& P = out[i];
-            P.nblocks = N;
-            P.cols.assign(N, {});
-            std::vector<int64_t> kc(N + 1, 0);
-            auto add = [&](const ColProblem& Z, uint32_t off, int sign) {
+            P.nblocks = W;
+            P.cols.assign(W, {});
+            std::vector<int64_t> kc(N + 8, 0);
+            // value(Z) = sum of Z's columns - q_Z 4^(nominal width of Z)
+            auto add = [&](const ColProblem& Z, uint32_t nominal, int64_t q, uint32_t off, int sign) {
                 for (uint32_t k = 0; k < Z.nblocks; ++k)
-                    for (const Block& b : Z.cols[k])
-                        if (k + off < N) push_signed(P.cols[k + off], kc[k + off], b, sign);
+                    for (const Block& b : Z.cols[k]) {
+                        if (k + off < W)
+                            push_signed(P.cols[k + off], kc[k + off], b, sign);
+                        else
+                            engine_check(!exact && k + off >= N, "karatsuba: a column entry beyond the exact width");
+                    }
+                if (nominal + off < kc.size()) kc[nominal + off] -= sign * q;
             };
-            add(zp[2 * j], 0, 1);
-            add(zp[2 * j + 1], 2 * h, 1);
-            add(mp[j], h, 1);
-            add(zp[2 * j], h, -1);
-            add(zp[2 * j + 1], h, -1);
-            // the constant mod 4^N as base-4 digits (floor division carries the sign up)
-            for (uint32_t k = 0; k < N; ++k) {
+            add(zp[2 * j], zops[2 * j].nblocks, zq[2 * j], 0, 1);
+            add(zp[2 * j + 1], zops[2 * j + 1].nblocks, zq[2 * j + 1], 2 * h, 1);
+            add(mp[j], mops[j].nblocks, mq[j], h, 1);
+            add(zp[2 * j], zops[2 * j].nblocks, zq[2 * j], h, -1);
+            add(zp[2 * j + 1], zops[2 * j + 1].nblocks, zq[2 * j + 1], h, -1);
+            // the constant as base-4 digits below N (floor division carries the sign up) and the
+            // rest c (a multiple of 4^N): mod 4^N it is dropped; exact, c >= 0 is a trivial entry at
+            // column N and c < 0 becomes the public excess q = -c of the representation
+            for (uint32_t k = 0; k + 1 < kc.size(); ++k) {
                 const int64_t c = kc[k] >= 0 ? kc[k] / 4 : -((-kc[k] + 3) / 4);
                 kc[k] -= 4 * c;
                 kc[k + 1] += c;
-                if (kc[k]) P.cols[k].push_back(Block::make_trivial((uint32_t)kc[k]));
+                if (k < N && kc[k]) P.cols[k].push_back(Block::make_trivial((uint32_t)kc[k]));
+            }
+            if (exact) {
+                int64_t c = 0;
+                for (size_t k = kc.size(); k-- > N;) c = 4 * c + kc[k];
+                if (c >= 0) {
+                    engine_check(c <= 15, "karatsuba: constant above the exact width");
+                    if (c & 3) P.cols[N].push_back(Block::make_trivial((uint32_t)(c & 3)));
+                    if (c >> 2) P.cols[N + 1].push_back(Block::make_trivial((uint32_t)(c >> 2)));
+                } else {
+                    engine_check(-c <= 14, "karatsuba: excess above the exact width");
+                    (*exact)[i] = -c;
+                }
             }
         }
     }

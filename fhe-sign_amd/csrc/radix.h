@@ -17,6 +17,7 @@
 #include <stdexcept>
 #include <string>
 #include <utility>
+#include <unordered_map>
 #include <vector>
 
 #include "context.h"
@@ -121,10 +122,18 @@ public:
     //                publicly known values (fhe_host_biguint_mul);
     //   kDry      -- items on dry_block() inputs are recorded and scheduled like the real thing, nothing
     //                is launched: levels and bootstrap counts of an op (fhe_host_biguint_mul_stats).
-    enum HostMode { kDevice = 0, kHostFold = 1, kDry = 2 };
+    //   kSim      -- kDry plus a plaintext shadow: sim_block() inputs carry a value the algorithms
+    //                cannot see (they take every encrypted path), each bootstrap is evaluated on the
+    //                host from its LUT (raw items by their negacyclic half rule) and checked to stay in
+    //                its input range -- the radix algorithms' end-to-end results on the CPU
+    //                (fhe_host_sim_*), with the degree / noise bookkeeping of the real thing.
+    enum HostMode { kDevice = 0, kHostFold = 1, kDry = 2, kSim = 3 };
     explicit Engine(fhe_ctx* ctx, int host_mode = kDevice);
-    // kDry: an "encrypted" block of the given degree (a placeholder slot)
+    // kDry / kSim: an "encrypted" block of the given degree (a placeholder slot)
     Block dry_block(uint32_t degree);
+    // kSim: an "encrypted" block holding `value`; sim_value: a block's plaintext in half message steps
+    Block sim_block(uint32_t value, uint32_t degree);
+    int64_t sim_half2(const Block& b) const;
     // diagnostics: the dependency depth (levels) of a pending block's producer, 0 if none is pending
     int32_t depth_of(const Block& b) const;
     ~Engine();
@@ -166,6 +175,7 @@ public:
 private:
     fhe_ctx* ctx_;
     int host_mode_ = kDevice;
+    std::unordered_map<const uint64_t*, int64_t> sim_;  // kSim: slot -> plaintext (half steps)
     std::shared_ptr<BlockPool> pool_;
     uint64_t* d_up_ = nullptr;  // upload staging: n big LWEs, then n destination pointers
     size_t up_cap_ = 0;

@@ -138,6 +138,12 @@ _SIGNATURES = [
                                              C.POINTER(C.c_uint64), u32p, C.c_size_t]),
     ("fhe_host_radix_stats", C.c_int, [C.c_int, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), u32p,
                                        C.c_size_t]),
+    ("fhe_host_sim_biguint_mul", C.c_int, [u32p, C.c_size_t, u32p, C.c_size_t, u32p, C.c_size_t, C.c_int, u32p,
+                                           C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_uint64),
+                                           C.POINTER(C.c_uint64)]),
+    ("fhe_host_sim_radix", C.c_int, [C.c_int, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint64)]),
     ("fhe_biguint_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_from_digits", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_size_t)]),

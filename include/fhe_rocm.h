@@ -334,7 +334,20 @@ int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64
 #define FHE_HOST_OP_SHR 4        /* encrypted shift amount */
 #define FHE_HOST_OP_LT 5
 #define FHE_HOST_OP_DIV_SCALAR 6 /* a / 0xC0FFEE01 */
+#define FHE_HOST_OP_SHL 7        /* encrypted shift amount */
+#define FHE_HOST_OP_MUL_FULL 8   /* a * b, 2 * bits wide */
+#define FHE_HOST_OP_AND 9
+#define FHE_HOST_OP_MIN 10
 int fhe_host_radix_stats(int op, uint32_t bits, uint64_t* pbs, uint64_t* levels, uint32_t* level_sizes, size_t cap);
+/* Simulated runs (no GPU, no key): operands are "encrypted" blocks whose plaintext the engine shadows
+ * on the host, so every encrypted code path runs (no trivial folding) while each bootstrap is
+ * evaluated from its lookup table and range-checked.  The BigUintFHE mul / mul-add (limbs LSB first,
+ * as fhe_host_biguint_mul) and one radix op on `bits`-wide operands (words LSB first; out: the result,
+ * 2 * bits wide for MUL_FULL, the bit for LT; out2: DIVREM's remainder).  pbs / levels optional. */
+int fhe_host_sim_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k, size_t lk,
+                             int mode, uint32_t* out, size_t cap, size_t* n, uint64_t* pbs, uint64_t* levels);
+int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t* b, uint64_t* out, uint64_t* out2,
+                       uint64_t* pbs, uint64_t* levels);
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */

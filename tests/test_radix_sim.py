@@ -1,0 +1,146 @@
+"""Radix algorithms end to end on the CPU through the engine's simulating mode (Engine kSim,
+fhe_host_sim_*): the operands are "encrypted" blocks whose plaintext the engine shadows on the host, so
+every encrypted code path runs -- no trivial folding -- while each bootstrap is evaluated from its lookup
+table and range-checked, with the degree and noise bookkeeping of the GPU runs.  Checked against exact
+integer semantics (tfhe's for the radix ops: wrapping add/sub/mul, shift amounts mod the width, x / 0 =
+all ones, x % 0 = x) and against oracle/ref_semantics.py for the BigUintFHE limbs (src/biguint.rs:120-265,
+the compat mode's lost carries included).  The GPU tests run the same algorithms on ciphertexts."""
+import ctypes as C
+import random
+
+import pytest
+
+import ref_semantics as R
+from fhe_sign import _lib
+
+COMPAT, FAST = 0, 1
+DIVREM, MUL, ADD, SUB, SHR, LT, DIV_SCALAR, SHL, MUL_FULL, AND, MIN = range(11)
+M32 = 1 << 32
+
+
+def sim_radix(op, bits, a, b):
+    w = (bits + 63) // 64
+    A = (C.c_uint64 * w)(*[(a >> (64 * i)) & (2**64 - 1) for i in range(w)])
+    B = (C.c_uint64 * w)(*[(b >> (64 * i)) & (2**64 - 1) for i in range(w)])
+    out, out2 = (C.c_uint64 * (2 * w))(), (C.c_uint64 * w)()
+    pbs, lev = C.c_uint64(), C.c_uint64()
+    lib = _lib.load()
+    rc = lib.fhe_host_sim_radix(op, bits, A, B, out, out2, C.byref(pbs), C.byref(lev))
+    assert rc == 0, lib.fhe_last_error()
+    return sum(out[i] << (64 * i) for i in range(2 * w)), sum(out2[i] << (64 * i) for i in range(w))
+
+
+def sim_mul(a, b, mode, k=None):
+    A = (C.c_uint32 * max(1, len(a)))(*a)
+    B = (C.c_uint32 * max(1, len(b)))(*b)
+    K = (C.c_uint32 * max(1, len(k)))(*k) if k else None
+    cap = len(a) + len(b) + (len(k) if k else 0) + 2
+    out, n = (C.c_uint32 * cap)(), C.c_size_t()
+    kp = C.cast(K, C.POINTER(C.c_uint32)) if K is not None else None
+    lib = _lib.load()
+    rc = lib.fhe_host_sim_biguint_mul(A, len(a), B, len(b), kp, len(k) if k else 0, mode, out, cap, C.byref(n),
+                                      None, None)
+    assert rc == 0, lib.fhe_last_error()
+    return list(out[: n.value])
+
+
+def expect(op, bits, a, b):
+    M = 1 << bits
+    if op == DIVREM:
+        return (a // b, a % b) if b else (M - 1, a)
+    if op == SHR:
+        return a >> (b % bits)
+    if op == SHL:
+        return (a << (b % bits)) % M
+    return {MUL: lambda: a * b % M, ADD: lambda: (a + b) % M, SUB: lambda: (a - b) % M, LT: lambda: int(a < b),
+            DIV_SCALAR: lambda: a // 0xC0FFEE01, MUL_FULL: lambda: a * b, AND: lambda: a & b,
+            MIN: lambda: min(a, b)}[op]()
+
+
+def operands(bits, rng, count):
+    M = 1 << bits
+    edge = [0, 1, 2, 3, M - 1, M - 2, M // 2, M // 2 - 1, (M - 1) // 3]
+    out = [(x, y) for x in (0, 1, M - 1) for y in (0, 1, M - 1)]
+    for _ in range(count):
+        kind = rng.randrange(4)
+        if kind == 0:
+            out.append((rng.getrandbits(bits), rng.getrandbits(bits)))
+        elif kind == 1:
+            out.append((rng.choice(edge), rng.getrandbits(bits)))
+        elif kind == 2:
+            out.append((rng.getrandbits(bits), rng.getrandbits(max(1, bits // 3))))
+        else:
+            out.append((rng.choice(edge), rng.choice(edge)))
+    return out
+
+
+@pytest.mark.parametrize("bits", [2, 8, 16, 32, 64, 128, 256])
+@pytest.mark.parametrize("op", [MUL, ADD, SUB, LT, DIV_SCALAR, MUL_FULL, AND, MIN])
+def test_radix_ops_simulated(bits, op):
+    rng = random.Random(1000 * op + bits)
+    for a, b in operands(bits, rng, 6 if bits >= 128 else 14):
+        got, _ = sim_radix(op, bits, a, b)
+        assert got == expect(op, bits, a, b), (op, bits, hex(a), hex(b))
+
+
+@pytest.mark.parametrize("bits", [2, 8, 16, 32, 64, 256])
+@pytest.mark.parametrize("op", [SHR, SHL])
+@pytest.mark.parametrize("four_way", ["1", "0"])
+def test_encrypted_shifts_simulated(monkeypatch, bits, op, four_way):
+    """Both barrel shifters (4-way stages by amount blocks, default; FHE_BARREL4=0 the 2-way one):
+    every amount below the width at small widths, the amount's high bits ignored (mod the width)."""
+    monkeypatch.setenv("FHE_BARREL4", four_way)
+    rng = random.Random(bits + 7 * op)
+    M = 1 << bits
+    amounts = range(bits) if bits <= 16 else [0, 1, 2, 3, 4, 7, 8, 31, bits // 2 + 1, bits - 1]
+    for s in amounts:
+        for a in (rng.getrandbits(bits), M - 1):
+            for amt in (s, s + bits * rng.randrange(1, max(2, M // bits))):
+                got, _ = sim_radix(op, bits, a, amt % M)
+                assert got == expect(op, bits, a, amt % M), (op, bits, hex(a), amt)
+
+
+@pytest.mark.parametrize("bits", [2, 8, 32, 64])
+def test_encrypted_divrem_simulated(bits):
+    rng = random.Random(bits)
+    cases = operands(bits, rng, 10) + [(rng.getrandbits(bits), 0), (0, 0), ((1 << bits) - 1, 1)]
+    for a, b in cases:
+        assert sim_radix(DIVREM, bits, a, b) == expect(DIVREM, bits, a, b), (bits, hex(a), hex(b))
+
+
+def test_encrypted_divrem_256_simulated():
+    """The 256-bit / encrypted divisor (869 levels) on a few operand shapes, the zero divisor included."""
+    rng = random.Random(256)
+    M = 1 << 256
+    for a, b in [(rng.getrandbits(256), rng.getrandbits(37) + 1), (M - 1, rng.getrandbits(256) | 1), (M - 1, 0),
+                 (rng.getrandbits(255), (1 << 128) + 1)]:
+        assert sim_radix(DIVREM, 256, a, b) == expect(DIVREM, 256, a, b)
+
+
+def _limbs(rng, n):
+    special = [0, 1, M32 - 1, M32 - 2, M32 // 2, 0xFFFF0000, M32 - 16, 15, 16]
+    return [rng.choice(special) if rng.random() < 0.4 else rng.getrandbits(32) for _ in range(n)]
+
+
+@pytest.mark.parametrize("kara", [None, "6", "off"])
+def test_biguint_mul_simulated(monkeypatch, kara):
+    """BigUintFHE mul / mul-add on simulated limbs: compat (the reference's limbs, lost carries included)
+    and fast (the true product) across limb shapes, with the Karatsuba split at its default threshold,
+    recursing down to 6 blocks, and off."""
+    if kara == "off":
+        monkeypatch.setenv("FHE_KARATSUBA", "0")
+    elif kara:
+        monkeypatch.setenv("FHE_KARA_MIN", kara)
+    rng = random.Random(5 if kara is None else 6)
+    shapes = [(1, 1), (2, 2), (1, 8), (8, 1), (3, 5), (8, 8)]
+    for la, lb in shapes:
+        a, b = _limbs(rng, la), _limbs(rng, lb)
+        assert sim_mul(a, b, COMPAT) == R.biguint_mul(a, b), (la, lb)
+        assert R.from_limbs(sim_mul(a, b, FAST)) == R.from_limbs(a) * R.from_limbs(b), (la, lb)
+    full = [M32 - 1] * 8
+    assert sim_mul(full, full, COMPAT) == R.biguint_mul(full, full)
+    assert R.from_limbs(sim_mul(full, full, FAST)) == R.from_limbs(full) ** 2
+    k = _limbs(rng, 8)
+    a, b = _limbs(rng, 8), _limbs(rng, 8)
+    assert sim_mul(a, b, COMPAT, k) == R.biguint_add(k, R.biguint_mul(a, b))
+    assert R.from_limbs(sim_mul(a, b, FAST, k)) == R.from_limbs(a) * R.from_limbs(b) + R.from_limbs(k)
