@@ -111,7 +111,11 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
     std::vector<std::pair<const Radix*, const Radix*>> ops;
     for (size_t i = 0; i < la; ++i)
         for (size_t j = 0; j < lb; ++j) ops.push_back({&a64[i], &b64[j]});
-    std::vector<std::vector<Blocks>> PC = radix_mul_many_columns(e, ops, 2 * kLimbBlocks);
+    // (Karatsuba-split products come with a 33rd column and a public excess q: their columns sum to
+    // P + q 2^64, i.e. hi(P) = hi_cs + c_P + 2^32 (column 32 - q); a MID addend takes column 32 - q
+    // into the limb's overflow O below)
+    std::vector<int64_t> excess;
+    std::vector<std::vector<Blocks>> PC = radix_mul_many_columns(e, ops, 2 * kLimbBlocks, &excess);
     {
         // entries must be fresh-noise blocks for the accumulation's noise budget (lazy multiples of a
         // public block -- only from trivially encrypted limbs -- are refreshed)
@@ -220,8 +224,15 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
                     const size_t l = dst[k].l, p = dst[k].p;
                     const Block& O0 = p ? PF[l][p - 1].O : kBias;
                     std::vector<Term> t{{O0, 1}, {outs[k], 1}};
-                    if (adds[l][p].second == 0) t.push_back({cP[adds[l][p].first], -1});
-                    oitems.push_back(raw_item(t, 0, [](uint32_t v) { return v; }, 15));
+                    int32_t half = 0;
+                    const size_t prod = adds[l][p].first;
+                    if (adds[l][p].second == 0) {
+                        t.push_back({cP[prod], -1});
+                    } else if (PC[prod].size() > 2 * kLimbBlocks) {
+                        for (const Block& b : PC[prod][2 * kLimbBlocks]) t.push_back({b, 1});
+                        half = -2 * (int32_t)excess[prod];
+                    }
+                    oitems.push_back(raw_item(t, half, [](uint32_t v) { return v; }, 15));
                     odst.push_back({l, p});
                 }
             }

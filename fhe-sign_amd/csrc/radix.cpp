@@ -1601,18 +1601,6 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
     return propagate_many(e, probs);
 }
 
-std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
-                                                        const std::vector<std::pair<const Radix*, const Radix*>>& ops,
-                                                        uint32_t nblocks) {
-    std::vector<ColProblem> probs = mul_problems(e, ops, nblocks, {}, false);
-    std::vector<ColProblem*> ptrs;
-    for (auto& p : probs) ptrs.push_back(&p);
-    compress_columns(e, ptrs);
-    std::vector<std::vector<Blocks>> res;
-    for (auto& p : probs) res.push_back(std::move(p.cols));
-    return res;
-}
-
 // Karatsuba split of a full product of two encrypted n-block operands (n >= FHE_KARA_MIN blocks,
 // default 24; FHE_KARATSUBA=0 turns it off; both read per call for same-process A/Bs):
 //   a b = z0 + X^2 z2 + X (m - z0 - z2),  X = 4^h, h = ceil(n / 2),
@@ -1645,9 +1633,14 @@ static uint32_t live_len(const Radix& r) {
     while (n > 0 && r.blocks[n - 1].trivial() && r.blocks[n - 1].value == 0) --n;
     return n;
 }
-static bool kara_eligible(const Radix& a, const Radix& b, uint32_t nblocks) {
+// the compat chain's 16-block limb products (FHE_KARA_COMPAT_MIN, default 16; above 16: unsplit)
+static uint32_t kara_compat_min() {
+    const char* v = getenv("FHE_KARA_COMPAT_MIN");
+    return v && atoi(v) >= 6 ? (uint32_t)atoi(v) : 16u;
+}
+static bool kara_eligible(const Radix& a, const Radix& b, uint32_t nblocks, uint32_t min_n) {
     const uint32_t n = live_len(a), h = (n + 1) / 2;
-    if (!karatsuba_on() || n != live_len(b) || n < kara_min() || nblocks < 2 * n || nblocks < 3 * h + 3) return false;
+    if (!karatsuba_on() || n != live_len(b) || n < min_n || nblocks < 2 * n || nblocks < 3 * h + 3) return false;
     // FHE_KARA_FORCE=1 (CPU tests): split publicly known operands too, so that the host-folding
     // engine checks the split's algebra (offsets, complements, constants) on known values
     const char* fv = getenv("FHE_KARA_FORCE");
@@ -1670,14 +1663,14 @@ struct MulOp {
 // + q_i 4^nblocks
 static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<MulOp>& ops,
                                                 const std::vector<const Radix*>& addends, bool kara_ok,
-                                                std::vector<int64_t>* exact);
+                                                std::vector<int64_t>* exact, uint32_t min_n);
 
 static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,
                                             uint32_t nblocks, const std::vector<const Radix*>& addends,
                                             bool kara_ok) {
     std::vector<MulOp> m;
     for (auto& op : ops) m.push_back({op.first, op.second, nblocks});
-    return mul_problems_ops(e, m, addends, kara_ok, nullptr);
+    return mul_problems_ops(e, m, addends, kara_ok, nullptr, kara_min());
 }
 
 // -x as a column entry: (deg - x) with -deg (times the column weight) into the public constant
@@ -1703,10 +1696,10 @@ static void push_signed(Blocks& col, int64_t& kc, const Block& b, int sign) {
 
 static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<MulOp>& ops,
                                                 const std::vector<const Radix*>& addends, bool kara_ok,
-                                                std::vector<int64_t>* exact) {
+                                                std::vector<int64_t>* exact, uint32_t min_n) {
     std::vector<size_t> kara, plain;
     for (size_t i = 0; i < ops.size(); ++i)
-        (kara_ok && kara_eligible(*ops[i].a, *ops[i].b, ops[i].nblocks) ? kara : plain).push_back(i);
+        (kara_ok && kara_eligible(*ops[i].a, *ops[i].b, ops[i].nblocks, min_n) ? kara : plain).push_back(i);
     std::vector<ColProblem> out(ops.size());
     if (exact) exact->assign(ops.size(), 0);
     if (!kara.empty()) {
@@ -1738,7 +1731,7 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
             zops.push_back({pa[1], pb[1], 2 * (n - h)});
         }
         std::vector<int64_t> zq, mq;
-        std::vector<ColProblem> zp = mul_problems_ops(e, zops, {}, true, &zq);
+        std::vector<ColProblem> zp = mul_problems_ops(e, zops, {}, true, &zq, min_n);
         for (auto& kv : parts) {
             const uint32_t h = kv.second[0]->nblocks();
             store.push_back(radix_sum(e, {kv.second[0], kv.second[1]}, h + 1));
@@ -1749,7 +1742,7 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
             const uint32_t h = parts[ops[i].a][0]->nblocks();
             mops.push_back({parts[ops[i].a][2], parts[ops[i].b][2], 2 * h + 2});
         }
-        std::vector<ColProblem> mp = mul_problems_ops(e, mops, {}, true, &mq);
+        std::vector<ColProblem> mp = mul_problems_ops(e, mops, {}, true, &mq, min_n);
         std::vector<ColProblem*> ptrs;
         for (auto& p : zp) ptrs.push_back(&p);
         for (auto& p : mp) ptrs.push_back(&p);
@@ -1855,6 +1848,34 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
             for (uint32_t k = 0; k < out[i].nblocks && k < addends[i]->nblocks(); ++k)
                 out[i].cols[k].push_back(addends[i]->blocks[k]);
     return out;
+}
+
+std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
+                                                        const std::vector<std::pair<const Radix*, const Radix*>>& ops,
+                                                        uint32_t nblocks, std::vector<int64_t>* excess) {
+    std::vector<ColProblem> probs;
+    if (excess) {  // exact column sets, Karatsuba-split where eligible (see mul_problems_ops)
+        std::vector<MulOp> m;
+        for (auto& op : ops) m.push_back({op.first, op.second, nblocks});
+        probs = mul_problems_ops(e, m, {}, true, excess, kara_compat_min());
+    } else {
+        probs = mul_problems(e, ops, nblocks, {}, false);
+    }
+    std::vector<ColProblem*> ptrs;
+    for (auto& p : probs) ptrs.push_back(&p);
+    compress_columns(e, ptrs);
+    std::vector<std::vector<Blocks>> res;
+    for (size_t i = 0; i < probs.size(); ++i) {
+        ColProblem& p = probs[i];
+        if (p.nblocks > nblocks + 1) {
+            // R = value + q 4^N < (1 + q) 4^N: with q <= 2 column N + 1 holds 0 (whatever its entries)
+            // and column N at most q
+            engine_check((*excess)[i] <= 2, "column product: excess above one headroom column");
+            p.cols.resize(nblocks + 1);
+        }
+        res.push_back(std::move(p.cols));
+    }
+    return res;
 }
 
 Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {

@@ -267,10 +267,13 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
                                   uint32_t nblocks, const std::vector<const Radix*>& addends = {});
 // The same products summed into columns and compressed only (each column a sum <= 6, <= 7 at
 // position 0, of <= 3 blocks; no carry propagation): the columns' value is the product mod 4^nblocks,
-// exactly the product when it fits (non-negative entries cannot wrap below it).
+// exactly the product when it fits (non-negative entries cannot wrap below it).  With `excess`,
+// full products may be Karatsuba-split: product i then has nblocks + 1 columns summing to the product
+// + (*excess)[i] 4^nblocks (a public q <= 2; column nblocks holds at most q), else nblocks columns
+// and q = 0.
 std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
                                                         const std::vector<std::pair<const Radix*, const Radix*>>& ops,
-                                                        uint32_t nblocks);
+                                                        uint32_t nblocks, std::vector<int64_t>* excess = nullptr);
 // a * b + c (wrapping at nblocks), one carry propagation.
 Radix radix_mul_add(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks);
 Radix radix_scalar_and(Engine& e, const Radix& a, const BigConst& mask);
