@@ -1605,10 +1605,11 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
 // default 24; FHE_KARATSUBA=0 turns it off; both read per call for same-process A/Bs):
 //   a b = z0 + X^2 z2 + X (m - z0 - z2),  X = 4^h, h = ceil(n / 2),
 //   z0 = a0 b0, z2 = a1 b1, m = (a0 + a1)(b0 + b1)  (the sums propagated to h + 1 clean blocks),
-// 3 products of ~h^2 block pairs instead of 4.  The three sub-products (split again while large
-// enough) are compressed on their own to <= 3 blocks per column before they are combined, so the
-// two subtracted copies add a few blocks per column, not a product's worth: -x enters as the
-// complement (deg x - x) with -deg x in a public constant, as in scalar_products.
+// 3 products of ~h^2 block pairs instead of 4.  z0 and z2 (split again while large enough) are
+// compressed on their own to <= 3 blocks per column before they are combined, so the two subtracted
+// copies add a few blocks per column, not a product's worth (-x enters as the complement
+// (deg x - x) with -deg x in a public constant, as in scalar_products); m, which enters once, joins
+// the combination raw (compressing it apart cost 2-3 % more bootstraps and 6 more levels at 256 bits).
 //
 // Exactness.  A column set whose public constant is negative cannot hold the value itself (its
 // entries are nonnegative): the top-level product is only needed mod 4^N (the carry propagation
@@ -1744,8 +1745,7 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
         }
         std::vector<ColProblem> mp = mul_problems_ops(e, mops, {}, true, &mq, min_n);
         std::vector<ColProblem*> ptrs;
-        for (auto& p : zp) ptrs.push_back(&p);
-        for (auto& p : mp) ptrs.push_back(&p);
+        for (auto& p : zp) ptrs.push_back(&p);  // m enters uncompressed (once, no copy)
         compress_columns(e, ptrs);
         for (size_t j = 0; j < kara.size(); ++j) {
             const size_t i = kara[j];
