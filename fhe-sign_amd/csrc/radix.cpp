@@ -328,7 +328,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         int64_t dcst = csts[i];
         const int64_t unit = raw ? 2 : 1;
         terms.clear();
-        const size_t cap = raw ? (size_t)kMaxWideTerms : (size_t)kMaxTerms;
+        const size_t cap = (size_t)kMaxWideTerms;  // > kMaxTerms: staged as a wide combination
         auto put = [&](const Block& b, int32_t coef) {
             for (TermExt& u : terms)
                 if (u.src == b.ptr()) {
@@ -1166,7 +1166,10 @@ bool greedy_level(std::vector<PNode>& nodes, std::vector<int>& latest, uint32_t 
 }
 }  // namespace
 
-static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const std::vector<std::vector<uint32_t>>& want) {
+// top8 (optional): per problem also 8 x the carry out of its top position (a second bootstrap of the
+// same input with the table scaled: degree 8, fresh noise) -- radix_divrem's selectors
+static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const std::vector<std::vector<uint32_t>>& want,
+                                        Blocks* top8 = nullptr) {
     const size_t P = in.size();
     std::vector<std::vector<PNode>> nodes(P);
     std::vector<std::vector<int>> result(P);
@@ -1279,6 +1282,24 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
             for (auto& t : n.terms) stack.push_back(t.first);
         }
     }
+    std::vector<int> top8_id(P, -1);
+    if (top8)
+        for (size_t p = 0; p < P; ++p) {
+            const uint32_t m = (uint32_t)in[p].size();
+            engine_check(m > 0, "top carry of an empty problem");
+            const int id = result[p][m - 1];
+            PNode n;
+            if (id >= (int)m) {  // a computed carry node: the same input, table x 8
+                n = nodes[p][id];
+                for (auto& v : n.table) v *= 8;
+            } else {  // position 0 is the top: its input block is the carry bit itself
+                n = PNode{0, true, 1, {{id, 1}}, lut1([](uint32_t v) { return 8 * (v & 1); })};
+                levels = std::max(levels, 1);
+            }
+            n.need = true;
+            top8_id[p] = (int)nodes[p].size();
+            nodes[p].push_back(std::move(n));
+        }
     std::vector<std::vector<Block>> val(P);
     for (size_t p = 0; p < P; ++p) {
         val[p].resize(nodes[p].size());
@@ -1304,6 +1325,10 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
     std::vector<Blocks> res(P);
     for (size_t p = 0; p < P; ++p)
         for (size_t k = 0; k < in[p].size(); ++k) res[p].push_back(val[p][result[p][k]]);
+    if (top8) {
+        top8->clear();
+        for (size_t p = 0; p < P; ++p) top8->push_back(val[p][top8_id[p]]);
+    }
     return res;
 }
 
@@ -1311,7 +1336,8 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
 // position k, k < nblocks - 1.  A problem with one extra empty top column yields its carry out.
 // `with`: extra items that run in the state level (their outputs in *with_out).
 static std::vector<Blocks> propagate_carries(Engine& e, std::vector<ColProblem>& probs,
-                                             const std::vector<PbsItem>* with = nullptr, Blocks* with_out = nullptr) {
+                                             const std::vector<PbsItem>* with = nullptr, Blocks* with_out = nullptr,
+                                             Blocks* top8 = nullptr) {
     std::vector<ColProblem*> ptrs;
     for (auto& p : probs) {
         p.cols.resize(p.nblocks);
@@ -1341,7 +1367,7 @@ static std::vector<Blocks> propagate_carries(Engine& e, std::vector<ColProblem>&
         cur[pi].assign(outs.begin() + o, outs.begin() + o + m);
         o += m;
     }
-    return carry_prefix(e, std::move(cur), {});
+    return carry_prefix(e, std::move(cur), {}, top8);
 }
 
 // out_k = (v_k + c_{k-1}) mod 4 for k < upto (the final level of a carry propagation)
@@ -2400,6 +2426,12 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
     }
     std::vector<std::vector<uint32_t>> sel(4);
     for (uint32_t c = 0; c < 4; ++c) sel[c] = lut1([c](uint32_t v) { return (v >> 2) == c ? v & 3 : 0u; });
+    static const auto sel_hi = lut1([](uint32_t v) { return v >= 8 ? (v - 8) & 3 : 0u; });
+    // FHE_DIV_MERGED (same-process A/Bs): 2 (default) selectors from the prefix's scaled top carries,
+    // 1 selectors in a level of their own, 0 the subtractions' separate final level
+    const char* mv = getenv("FHE_DIV_MERGED");
+    const int mode = mv ? atoi(mv) : 2;
+    const bool merged2 = mode >= 2, merged = mode == 1;
     Blocks r;  // remainder, w - 1 blocks before step i
     Radix q;
     q.blocks.resize(n);
@@ -2416,28 +2448,100 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
             probs[c].cols[0].push_back(Block::make_trivial(1));
             probs[c].cols[w] = {P[c][w]};
         }
-        std::vector<Blocks> cur = propagate_carries(e, probs);
-        std::vector<PbsItem> items;
-        for (int c = 0; c < 3; ++c) final_items(probs[c], cur[c], w, items);
-        {
+        Blocks G;  // 8 ge_c (merged2)
+        std::vector<Blocks> cur = propagate_carries(e, probs, nullptr, nullptr, merged2 ? &G : nullptr);
+        Blocks h;
+        if (merged2) {
+            // selectors without a level of their own: the prefix's top nodes also give G_c = 8 ge_c, and
+            // as ge_1 >= ge_2 >= ge_3, 8 [q == c] = G_c - G_(c+1) (G_0 = 8, G_4 = 0) -- a difference the
+            // degree bookkeeping cannot bound, so the selects are raw items (actual input in [0, 15],
+            // noise <= 8); the digit q = ge_1 + ge_2 + ge_3 is off the critical path
+            std::vector<PbsItem> hs;
+            for (uint32_t k = 0; k < w; ++k)
+                for (uint32_t c = 0; c < 4; ++c) {
+                    std::vector<Term> t;
+                    int32_t cst = 0;
+                    if (c == 0)
+                        cst = 8;
+                    else
+                        t.push_back({G[c - 1], 1});
+                    if (c < 3) t.push_back({G[c], -1});
+                    if (c == 0) {
+                        t.push_back({r4[k], 1});
+                    } else {
+                        for (auto& b : probs[c - 1].cols[k]) t.push_back({b, 1});
+                        if (k > 0) t.push_back({cur[c - 1][k - 1], 1});
+                    }
+                    PbsItem it;
+                    it.raw = true;
+                    it.terms = std::move(t);
+                    it.half_cst = 2 * cst;
+                    it.half_table.resize(16);
+                    for (uint32_t v = 0; v < 16; ++v) it.half_table[v] = 2 * (int32_t)sel_hi[v];
+                    it.raw_degree = 3;
+                    hs.push_back(std::move(it));
+                }
+            PbsItem qi;
+            qi.terms = {{cur[0][w], 1}, {cur[1][w], 1}, {cur[2][w], 1}};
+            qi.table = LUT_ID;
+            hs.push_back(qi);
+            h = e.run(hs);
+            q.blocks[i] = h.back();
+            h.pop_back();
+        } else if (merged) {
+            // the quotient digit and the selectors S_c = 8 [q == c] (a PBS output of degree 8 and
+            // fresh noise), then r_k = sum_c f(S_c + x_ck) with x_0k = r4_k and x_ck the UNREDUCED
+            // column sum + carry in of subtraction c (<= 7): f(v) = (v - 8) mod 4 for v >= 8, else 0 --
+            // the subtractions' final level folded into the select (input <= 15, noise <= 7)
+            std::vector<PbsItem> items;
             PbsItem qi;
             qi.terms = {{cur[0][w], 1}, {cur[1][w], 1}, {cur[2][w], 1}};
             qi.table = LUT_ID;
             items.push_back(qi);
-        }
-        Blocks o = e.run(items);
-        const Block qb = o[3 * w];
-        q.blocks[i] = qb;
-        // r_k = sum over c of [q == c] cand_c[k], exactly one term nonzero
-        std::vector<PbsItem> hs;
-        for (uint32_t k = 0; k < w; ++k)
             for (uint32_t c = 0; c < 4; ++c) {
-                PbsItem it;
-                it.terms = {{qb, 4}, {c == 0 ? r4[k] : o[(c - 1) * w + k], 1}};
-                it.table = sel[c];
-                hs.push_back(it);
+                qi.table = lut1([c](uint32_t v) { return v == c ? 8u : 0u; });
+                items.push_back(qi);
             }
-        Blocks h = e.run(hs);
+            Blocks o = e.run(items);
+            q.blocks[i] = o[0];
+            std::vector<PbsItem> hs;
+            for (uint32_t k = 0; k < w; ++k)
+                for (uint32_t c = 0; c < 4; ++c) {
+                    PbsItem it;
+                    it.terms = {{o[1 + c], 1}};
+                    if (c == 0) {
+                        it.terms.push_back({r4[k], 1});
+                    } else {
+                        for (auto& b : probs[c - 1].cols[k]) it.terms.push_back({b, 1});
+                        if (k > 0) it.terms.push_back({cur[c - 1][k - 1], 1});
+                    }
+                    it.table = sel_hi;
+                    hs.push_back(it);
+                }
+            h = e.run(hs);
+        } else {
+            std::vector<PbsItem> items;
+            for (int c = 0; c < 3; ++c) final_items(probs[c], cur[c], w, items);
+            {
+                PbsItem qi;
+                qi.terms = {{cur[0][w], 1}, {cur[1][w], 1}, {cur[2][w], 1}};
+                qi.table = LUT_ID;
+                items.push_back(qi);
+            }
+            Blocks o = e.run(items);
+            const Block qb = o[3 * w];
+            q.blocks[i] = qb;
+            // r_k = sum over c of [q == c] cand_c[k], exactly one term nonzero
+            std::vector<PbsItem> hs;
+            for (uint32_t k = 0; k < w; ++k)
+                for (uint32_t c = 0; c < 4; ++c) {
+                    PbsItem it;
+                    it.terms = {{qb, 4}, {c == 0 ? r4[k] : o[(c - 1) * w + k], 1}};
+                    it.table = sel[c];
+                    hs.push_back(it);
+                }
+            h = e.run(hs);
+        }
         // r_k = sum of the four half-selects (exactly one nonzero): kept lazy (noise 4), it enters
         // the next step's columns and half-selects directly -- no cleaning level per step
         r.assign(w, Block());
