@@ -1164,6 +1164,50 @@ bool greedy_level(std::vector<PNode>& nodes, std::vector<int>& latest, uint32_t 
     }
     return any;
 }
+
+// One Sklansky level (radix 3) over positions [0, m): with sub-blocks of sb = 3^(t-1) positions, every
+// unresolved position in the upper two sub-blocks of its block of 3 sb chains its own window (its
+// sub-block so far) with the tops of the sub-blocks below it in the block -- fan-out is free, so only
+// 2/3 of the positions take a bootstrap per level where the greedy (Kogge-Stone) form takes all.
+bool sklansky_level(std::vector<PNode>& nodes, std::vector<int>& latest, uint32_t m, int t, uint32_t sb) {
+    const std::vector<int> snap = latest;
+    bool any = false;
+    for (uint32_t k = 0; k < m; ++k) {
+        const PNode& own = nodes[snap[k]];
+        if (own.done) continue;
+        any = true;
+        const uint32_t j = (k / sb) % 3, base = k - k % (3 * sb);
+        PNode n{own.lo, false, t, {{snap[k], 0}}, {}};
+        int states = 1;
+        for (int jj = (int)j - 1; jj >= 0; --jj) {
+            const int below = snap[base + (uint32_t)jj * sb + sb - 1];
+            const PNode& b = nodes[below];
+            engine_check(b.done || b.lo == base + (uint32_t)jj * sb, "sklansky: sub-block window");
+            if (b.done) {
+                n.terms.push_back({below, 1});
+                n.lo = 0;
+                n.done = true;
+                break;
+            }
+            n.terms.push_back({below, 0});
+            n.lo = b.lo;
+            ++states;
+        }
+        // a resolved carry right below the window joins as well (the chain's fourth input), as in the
+        // greedy form: the block resolves a level earlier when the block below it already has
+        if (!n.done && n.lo > 0 && nodes[snap[n.lo - 1]].done) {
+            n.terms.push_back({snap[n.lo - 1], 1});
+            n.lo = 0;
+            n.done = true;
+        }
+        if (states == 1 && !n.done) continue;  // lowest sub-block, nothing resolved below: unchanged
+        for (int i = 0; i < states; ++i) n.terms[i].second = 1 << (states - 1 - i);
+        n.table = chain_table(states, n.done);
+        latest[k] = (int)nodes.size();
+        nodes.push_back(std::move(n));
+    }
+    return any;
+}
 }  // namespace
 
 // top8 (optional): per problem also 8 x the carry out of its top position (a second bootstrap of the
@@ -1182,11 +1226,34 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
             base.push_back({k, k == 0, 0, {}, {}});
             latest.push_back((int)k);
         }
-        // generic plan over all positions
+        // generic plan over all positions (FHE_PREFIX=ks: the greedy Kogge-Stone form)
         std::vector<PNode> gen = base;
         std::vector<int> glat = latest;
         int glev = 0;
-        while (greedy_level(gen, glat, m, glev + 1)) ++glev;
+        // the first s levels Sklansky, the rest greedy: the fewest levels, then the fewest nodes, over
+        // every s (host planning only; FHE_PREFIX=ks: s = 0)
+        const char* pv = getenv("FHE_PREFIX");
+        const bool ks_only = pv && strcmp(pv, "ks") == 0;
+        for (int s_sk = 0;; ++s_sk) {
+            std::vector<PNode> nd = base;
+            std::vector<int> lat = latest;
+            int lev = 0;
+            uint32_t sb = 1;
+            bool more = true;
+            while (more && lev < s_sk) {
+                more = sklansky_level(nd, lat, m, lev + 1, sb);
+                if (more) ++lev;
+                sb *= 3;
+            }
+            const bool sk_done = !more;
+            while (greedy_level(nd, lat, m, lev + 1)) ++lev;
+            if (s_sk == 0 || lev < glev || (lev == glev && nd.size() < gen.size())) {
+                gen = std::move(nd);
+                glat = std::move(lat);
+                glev = lev;
+            }
+            if (ks_only || sk_done) break;
+        }
         // top propagate/kill run [G, m)
         uint32_t G = m;
         while (G > 1 && in[p][G - 1].degree <= 1) --G;
