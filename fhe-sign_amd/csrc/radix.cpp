@@ -2442,7 +2442,7 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
     const uint32_t n = a.nblocks(), W = n + 1;
     Radix d1 = radix_resize(d, W);
     Radix d2 = radix_sum(e, {&d1, &d1}, W);
-    Radix d3 = radix_sum(e, {&d2, &d1}, W);
+    Radix d3 = radix_sum(e, {&d1, &d1, &d1}, W);  // beside d2, not after it
     static const auto LUT_ID = lut1([](uint32_t v) { return v & 3; });
     static const auto LUT_ZERO = lut1([](uint32_t v) { return v == 0 ? 1u : 0u; });
     std::vector<Blocks> nd(3), zf(3);  // complements 3 - (c d)_k, zero flags [(c d)_k == 0]
