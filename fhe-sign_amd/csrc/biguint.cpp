@@ -81,6 +81,39 @@ BigUint biguint_mul_add(Engine& e, const BigUint& A, const BigUint& B, const Big
     return biguint_add(e, K, p, mode);
 }
 
+std::vector<Blocks> biguint_mul_add_columns(Engine& e, const BigUint& A, const BigUint& B, const BigUint& K, int mode,
+                                            uint32_t* nblocks) {
+    const size_t la = A.digits.size(), lb = B.digits.size(), lk = K.digits.size();
+    std::vector<const Radix*> pk;
+    for (auto& d : K.digits) pk.push_back(&d);
+    const Radix wk = concat(pk);
+    if (la == 0 || lb == 0) {  // k itself
+        *nblocks = wk.nblocks();
+        std::vector<Blocks> cols(*nblocks);
+        for (uint32_t j = 0; j < *nblocks; ++j) cols[j] = {wk.blocks[j]};
+        return cols;
+    }
+    const size_t len = std::max(lk, la + lb) + 1;
+    *nblocks = (uint32_t)len * kLimbBlocks;
+    if (mode == kFast || la == 1 || lb == 1) {  // an exact product: k joins its columns
+        std::vector<const Radix*> pa, pb;
+        for (auto& d : A.digits) pa.push_back(&d);
+        for (auto& d : B.digits) pb.push_back(&d);
+        return radix_mul_add_columns(e, concat(pa), concat(pb), wk, *nblocks);
+    }
+    // the compat product's limbs (lost carries included), then k + P left unpropagated
+    const BigUint P = mul_impl(e, A, B, mode, true);
+    std::vector<const Radix*> pp;
+    for (auto& d : P.digits) pp.push_back(&d);
+    const Radix wp = concat(pp);
+    std::vector<Blocks> cols(*nblocks);
+    for (uint32_t j = 0; j < *nblocks; ++j) {
+        if (j < wk.nblocks()) cols[j].push_back(wk.blocks[j]);
+        if (j < wp.nblocks()) cols[j].push_back(wp.blocks[j]);
+    }
+    return cols;
+}
+
 static BigUint mul_impl(Engine& e, const BigUint& A, const BigUint& B, int mode, bool keep_lazy) {
     const size_t la = A.digits.size(), lb = B.digits.size();
     BigUint out;

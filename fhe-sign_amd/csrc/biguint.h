@@ -26,6 +26,12 @@ BigUint biguint_add(Engine& e, const BigUint& a, const BigUint& b, int mode);
 BigUint biguint_mul(Engine& e, const BigUint& a, const BigUint& b, int mode);
 // k + a * b, limbs identical to biguint_add(k, biguint_mul(a, b)) (src/schnorr.rs:274)
 BigUint biguint_mul_add(Engine& e, const BigUint& a, const BigUint& b, const BigUint& k, int mode);
+// The value of biguint_mul_add's limbs (k + the mode's product) left in column form for decryption:
+// cols[j] = blocks summing into position j (weight 4^j), *nblocks positions; the value is
+// sum_j sum cols[j] 4^j mod 4^nblocks.  No final carry propagation: the decryption resolves the
+// carries on the host, as tfhe-rs's decrypt_radix does for blocks with carries.
+std::vector<Blocks> biguint_mul_add_columns(Engine& e, const BigUint& a, const BigUint& b, const BigUint& k, int mode,
+                                            uint32_t* nblocks);
 // kCompat limbs by the carry-count chain (compat_chain.cpp), for 2 <= min(la, lb) <= 8
 bool compat_chain_applies(size_t la, size_t lb);
 BigUint compat_chain_mul(Engine& e, const BigUint& a, const BigUint& b);

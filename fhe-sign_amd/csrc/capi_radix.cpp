@@ -1,5 +1,7 @@
 // capi_radix.cpp -- C ABI for radix integers (FheUint<N>) and BigUintFHE.
+#include <algorithm>
 #include <cstring>
+#include <unordered_map>
 #include <memory>
 #include <string>
 #include <stdexcept>
@@ -15,6 +17,11 @@ struct fhe_radix {
 
 struct fhe_biguint {
     fhe::BigUint v;
+};
+
+struct fhe_columns {
+    std::vector<fhe::Blocks> cols;
+    uint32_t nblocks = 0;
 };
 
 using namespace fhe;
@@ -94,6 +101,45 @@ int unop(fhe_ctx* c, const fhe_radix* a, fhe_radix** out, F&& f) {
 }
 
 }  // namespace
+
+// sum_j sum cols[j] 4^j mod 4^nblocks into words (LSB first), each column entry's value from val():
+// trivial blocks as they are, lazy blocks as their linear combination of slot blocks
+template <class V>
+static void column_value(const std::vector<Blocks>& cols, uint32_t nblocks, V&& val, uint64_t* words, size_t nwords) {
+    std::vector<uint64_t> acc((2 * (size_t)nblocks + 63) / 64 + 2, 0);
+    auto add_at = [&](uint32_t j, int64_t v) {  // acc += v 4^j (every entry's value is >= 0)
+        engine_check(v >= 0, "column value below zero");
+        unsigned __int128 add = (unsigned __int128)(uint64_t)v << ((2 * j) % 64);
+        uint64_t carry = 0;
+        for (size_t w = (2 * (size_t)j) / 64; w < acc.size() && (add || carry); ++w) {
+            const unsigned __int128 s2 = (unsigned __int128)acc[w] + (uint64_t)add + carry;
+            acc[w] = (uint64_t)s2;
+            carry = (uint64_t)(s2 >> 64);
+            add >>= 64;
+        }
+    };
+    for (uint32_t j = 0; j < nblocks && j < cols.size(); ++j) {
+        int64_t v = 0;
+        for (const Block& b : cols[j]) {
+            if (b.trivial()) {
+                v += b.value;
+            } else if (b.lazy()) {
+                v += b.lin_cst;
+                for (const Term& t : *b.lin) v += (int64_t)t.coef * val(t.b);
+            } else {
+                v += val(b);
+            }
+        }
+        add_at(j, v);
+    }
+    const uint32_t bits = 2 * nblocks;
+    for (size_t w = 0; w < nwords; ++w) {
+        uint64_t x = w < acc.size() ? acc[w] : 0;
+        if (64 * w >= bits) x = 0;
+        else if (64 * (w + 1) > bits) x &= (bits % 64) ? ((1ull << (bits % 64)) - 1) : ~0ull;
+        words[w] = x;
+    }
+}
 
 extern "C" {
 
@@ -660,6 +706,80 @@ int fhe_host_radix_stats(int op, uint32_t bits, uint64_t* pbs, uint64_t* levels,
     });
 }
 
+// k + a * b in column form for decryption (biguint_mul_add_columns): the FHE work of the mode's
+// mul-add without its final carry propagation, which the decryption resolves on the host
+int fhe_biguint_mul_add_columns(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, const fhe_biguint* k, int mode,
+                                fhe_columns** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !b || !k || !out || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
+    return guarded([&] {
+        auto* r = new fhe_columns();
+        r->cols = biguint_mul_add_columns(*c->engine, a->v, b->v, k->v, mode, &r->nblocks);
+        *out = r;
+        return FHE_OK;
+    });
+}
+
+// m * a + k (m, k public words) in column form, value mod 2^(a's bits): the public-operand signer
+int fhe_radix_scalar_mul_add_columns(fhe_ctx* c, const fhe_radix* a, const uint64_t* m, size_t nm, const uint64_t* k,
+                                     size_t nk, fhe_columns** out) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!a || !out || (!m && nm) || (!k && nk)) return FHE_ERR_INVALID;
+    const BigConst vm = words_of(m, nm), vk = words_of(k, nk);
+    return guarded([&] {
+        auto* r = new fhe_columns();
+        const uint32_t nb = a->r.nblocks();
+        r->cols = radix_mul_add_columns(*c->engine, a->r, radix_trivial(vm, nb), radix_trivial(vk, nb), nb);
+        r->nblocks = nb;
+        *out = r;
+        return FHE_OK;
+    });
+}
+
+int fhe_columns_bits(const fhe_columns* x, uint32_t* bits) {
+    if (!x || !bits) return FHE_ERR_INVALID;
+    *bits = 2 * x->nblocks;
+    return FHE_OK;
+}
+
+int fhe_columns_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_columns* x, uint64_t* words, size_t nwords) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!ck || !x || !words || nwords * 64 < 2 * (size_t)x->nblocks) {
+        set_error("invalid arguments to fhe_columns_decrypt");
+        return FHE_ERR_INVALID;
+    }
+    return guarded([&] {
+        // every slot block (lazy entries: their terms) in one download
+        std::vector<const Block*> enc;
+        std::vector<const uint64_t*> keys;
+        auto want = [&](const Block& b) {
+            if (std::find(keys.begin(), keys.end(), b.ptr()) != keys.end()) return;
+            keys.push_back(b.ptr());
+            enc.push_back(&b);
+        };
+        for (const Blocks& col : x->cols)
+            for (const Block& b : col) {
+                if (b.trivial()) continue;
+                if (b.lazy())
+                    for (const Term& t : *b.lin) want(t.b);
+                else
+                    want(b);
+            }
+        std::vector<uint64_t> cts(enc.size() * kBigCt);
+        c->engine->download_many(enc, cts.data());
+        std::unordered_map<const uint64_t*, int64_t> vals;
+        for (size_t i = 0; i < enc.size(); ++i)
+            vals[keys[i]] = (int64_t)decode_block(ck->params, decrypt_phase_big(ck, cts.data() + i * kBigCt));
+        column_value(x->cols, x->nblocks, [&](const Block& b) { return vals.at(b.ptr()); }, words, nwords);
+        return FHE_OK;
+    });
+}
+
+void fhe_columns_destroy(fhe_columns* x) { delete x; }
+
 // Simulated runs (no GPU, no key; Engine kSim): the operands are "encrypted" blocks whose plaintext
 // the engine shadows on the host, so the algorithms take every encrypted path (no trivial folding)
 // while each bootstrap is evaluated from its LUT and range-checked -- the end-to-end results of the
@@ -693,6 +813,42 @@ int fhe_host_sim_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, si
             }
             out[i] = (uint32_t)v;
         }
+        if (pbs) *pbs = e.pbs_count;
+        if (levels) *levels = e.levels;
+        return FHE_OK;
+    });
+}
+
+// biguint_mul_add_columns on simulated limbs: the column form's value (words LSB first, nwords >=
+// its bits / 64) -- what fhe_columns_decrypt returns
+int fhe_host_sim_biguint_mul_add_columns(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k,
+                                         size_t lk, int mode, uint64_t* words, size_t nwords, uint32_t* bits,
+                                         uint64_t* pbs, uint64_t* levels) {
+    if ((la && !a) || (lb && !b) || (lk && !k) || !words || !bits || (mode != kCompat && mode != kFast))
+        return FHE_ERR_INVALID;
+    return guarded([&] {
+        fhe_ctx c;
+        Engine e(&c, Engine::kSim);
+        auto make = [&](const uint32_t* v, size_t n) {
+            BigUint r;
+            for (size_t i = 0; i < n; ++i) {
+                Radix d;
+                for (uint32_t q = 0; q < kLimbBlocks; ++q) d.blocks.push_back(e.sim_block((v[i] >> (2 * q)) & 3u, 3));
+                r.digits.push_back(std::move(d));
+            }
+            return r;
+        };
+        const BigUint A = make(a, la), B = make(b, lb), K = make(k, lk);
+        uint32_t nb = 0;
+        const std::vector<Blocks> cols = biguint_mul_add_columns(e, A, B, K, mode, &nb);
+        e.flush();
+        *bits = 2 * nb;
+        engine_check(nwords * 64 >= 2 * (size_t)nb, "sim columns: word buffer too small");
+        column_value(cols, nb, [&](const Block& x) {
+            const int64_t h2 = e.sim_half2(x);
+            engine_check(h2 % 2 == 0 && h2 >= 0 && h2 < 32, "sim columns: a block off its message range");
+            return h2 / 2;
+        }, words, nwords);
         if (pbs) *pbs = e.pbs_count;
         if (levels) *levels = e.levels;
         return FHE_OK;

@@ -1975,6 +1975,13 @@ Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {
     return radix_mul_many(e, {{&a, &b}}, nblocks)[0];
 }
 
+std::vector<Blocks> radix_mul_add_columns(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks) {
+    std::vector<ColProblem> probs = mul_problems(e, {{&a, &b}}, nblocks, {&c}, true);
+    std::vector<ColProblem*> ptrs{&probs[0]};
+    compress_columns(e, ptrs);
+    return std::move(probs[0].cols);
+}
+
 Radix radix_mul_add(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks) {
     return radix_mul_many(e, {{&a, &b}}, nblocks, {&c})[0];
 }

@@ -276,6 +276,9 @@ std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
                                                         uint32_t nblocks, std::vector<int64_t>* excess = nullptr);
 // a * b + c (wrapping at nblocks), one carry propagation.
 Radix radix_mul_add(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks);
+// a * b + c as compressed columns (each <= 3 blocks summing <= 6), value mod 4^nblocks; no carry
+// propagation (a decryption's input)
+std::vector<Blocks> radix_mul_add_columns(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks);
 Radix radix_scalar_and(Engine& e, const Radix& a, const BigConst& mask);
 Radix radix_scalar_shr(Engine& e, const Radix& a, uint32_t bits);
 Radix radix_scalar_shl(Engine& e, const Radix& a, uint32_t bits);

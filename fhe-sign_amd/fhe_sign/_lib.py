@@ -144,6 +144,16 @@ _SIGNATURES = [
     ("fhe_host_sim_radix", C.c_int, [C.c_int, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                      C.POINTER(C.c_uint64)]),
+    ("fhe_host_sim_biguint_mul_add_columns", C.c_int, [u32p, C.c_size_t, u32p, C.c_size_t, u32p, C.c_size_t, C.c_int,
+                                                       C.POINTER(C.c_uint64), C.c_size_t, u32p, C.POINTER(C.c_uint64),
+                                                       C.POINTER(C.c_uint64)]),
+    ("fhe_biguint_mul_add_columns", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                              C.POINTER(C.c_void_p)]),
+    ("fhe_radix_scalar_mul_add_columns", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t,
+                                                   C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_columns_bits", C.c_int, [C.c_void_p, u32p]),
+    ("fhe_columns_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t]),
+    ("fhe_columns_destroy", None, [C.c_void_p]),
     ("fhe_biguint_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_from_digits", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_biguint_decrypt", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, u32p, C.c_size_t, C.POINTER(C.c_size_t)]),

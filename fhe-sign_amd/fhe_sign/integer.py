@@ -381,6 +381,22 @@ class BigUintFHE:
         check(load().fhe_biguint_mul_add(_ctx().handle, self._h, other._h, addend._h, mode, C.byref(h)))
         return BigUintFHE(h)
 
+    def mul_add_value(self, other, addend, client_key, mode: int = COMPAT) -> int:
+        """the value of mul_add's limbs, computed in column form (fhe_biguint_mul_add_columns: no final
+        carry propagation) and decrypted with its carries resolved on the host -- what the signer does"""
+        lib = load()
+        h = C.c_void_p()
+        check(lib.fhe_biguint_mul_add_columns(_ctx().handle, self._h, other._h, addend._h, mode, C.byref(h)))
+        try:
+            bits = C.c_uint32()
+            check(lib.fhe_columns_bits(h, C.byref(bits)))
+            n = (bits.value + 63) // 64
+            w = np.zeros(n, np.uint64)
+            check(lib.fhe_columns_decrypt(_ctx().handle, client_key.handle, h, ptr(w), n))
+        finally:
+            lib.fhe_columns_destroy(h)
+        return sum(int(x) << (64 * i) for i, x in enumerate(w))
+
     __add__ = add
     __mul__ = mul
 

@@ -348,6 +348,9 @@ int fhe_host_sim_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, si
                              int mode, uint32_t* out, size_t cap, size_t* n, uint64_t* pbs, uint64_t* levels);
 int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t* b, uint64_t* out, uint64_t* out2,
                        uint64_t* pbs, uint64_t* levels);
+int fhe_host_sim_biguint_mul_add_columns(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k,
+                                         size_t lk, int mode, uint64_t* words, size_t nwords, uint32_t* bits,
+                                         uint64_t* pbs, uint64_t* levels);
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */
@@ -377,6 +380,18 @@ int fhe_biguint_mul(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, in
  * is exact (fast mode or a one-limb factor), one fewer otherwise */
 int fhe_biguint_mul_add(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, const fhe_biguint* k, int mode,
                         fhe_biguint** out);
+/* k + a * b (the limbs' value of fhe_biguint_mul_add) left in column form for decryption: the same
+ * FHE work without the final carry propagation; fhe_columns_decrypt resolves the carries on the host
+ * (as tfhe-rs's decrypt_radix does for blocks holding carries) and returns the value mod 2^bits. */
+typedef struct fhe_columns fhe_columns;
+int fhe_biguint_mul_add_columns(fhe_ctx* ctx, const fhe_biguint* a, const fhe_biguint* b, const fhe_biguint* k, int mode,
+                                fhe_columns** out);
+/* m * a + k (m, k public words) in column form, value mod 2^(a's bits) */
+int fhe_radix_scalar_mul_add_columns(fhe_ctx* ctx, const fhe_radix* a, const uint64_t* m, size_t nm, const uint64_t* k,
+                                     size_t nk, fhe_columns** out);
+int fhe_columns_bits(const fhe_columns* x, uint32_t* bits);
+int fhe_columns_decrypt(fhe_ctx* ctx, const fhe_client_key* ck, const fhe_columns* x, uint64_t* words, size_t nwords);
+void fhe_columns_destroy(fhe_columns* x);
 /* serialization of the limb vector (format of fhe_radix_serialize; every limb is a 32-bit radix) */
 int fhe_biguint_serialize(fhe_ctx* ctx, const fhe_biguint* x, uint8_t* buf, size_t cap, size_t* len);
 int fhe_biguint_deserialize(fhe_ctx* ctx, const uint8_t* buf, size_t len, fhe_biguint** out);

@@ -213,6 +213,25 @@ def test_biguint_mul_add_equals_mul_then_add(keys):
     assert a.mul_add(b, zero, COMPAT).decrypt_limbs(ck) == R.biguint_mul(q["a"], q["b"])
 
 
+def test_biguint_mul_add_columns_value(keys):
+    """The signer's column form (fhe_biguint_mul_add_columns + fhe_columns_decrypt: k + a*b without its
+    final carry propagation, carries resolved by the decryption) gives the value of mul_add's limbs:
+    the 8x1 signer shape, the 8x8 compat product with the F7 lost carry, fast, a zero addend."""
+    ck, _ = keys
+    v = json.load(open(os.path.join(G, "sign_vectors.json")))["vectors"][0]
+    e, d, k = _big(ck, v["e"]), _big(ck, v["d"]), _big(ck, v["k"])
+    assert e.mul_add_value(d, k, ck) == R.from_limbs(v["sum"])
+    q = json.load(open(os.path.join(G, "biguint_vectors.json")))["quirk_mul"][0]
+    rng = random.Random(0xC015)
+    kl = R.to_u32_digits(rng.getrandbits(256))
+    a, b, kk = _big(ck, q["a"]), _big(ck, q["b"]), _big(ck, kl)
+    assert a.mul_add_value(b, kk, ck, COMPAT) == R.from_limbs(R.biguint_add(kl, R.biguint_mul(q["a"], q["b"])))
+    want = R.from_limbs(kl) + R.from_limbs(q["a"]) * R.from_limbs(q["b"])
+    assert a.mul_add_value(b, kk, ck, FAST) == want
+    zero = BigUintFHE.new(0, ck)
+    assert a.mul_add_value(b, zero, ck, COMPAT) == R.from_limbs(R.biguint_mul(q["a"], q["b"]))
+
+
 def test_deferred_graph_lifetimes_and_raw_pbs(keys):
     """The engine defers bootstraps until a host read (csrc/radix.h Engine): operands and results
     dropped before that read keep what the pending graph still needs, raw fhe_pbs_batch calls in

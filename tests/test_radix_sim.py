@@ -144,3 +144,33 @@ def test_biguint_mul_simulated(monkeypatch, kara):
     a, b = _limbs(rng, 8), _limbs(rng, 8)
     assert sim_mul(a, b, COMPAT, k) == R.biguint_add(k, R.biguint_mul(a, b))
     assert R.from_limbs(sim_mul(a, b, FAST, k)) == R.from_limbs(a) * R.from_limbs(b) + R.from_limbs(k)
+
+
+def sim_mul_add_columns(a, b, k, mode):
+    A = (C.c_uint32 * max(1, len(a)))(*a)
+    B = (C.c_uint32 * max(1, len(b)))(*b)
+    K = (C.c_uint32 * max(1, len(k)))(*k)
+    words, bits = (C.c_uint64 * 16)(), C.c_uint32()
+    lib = _lib.load()
+    rc = lib.fhe_host_sim_biguint_mul_add_columns(A, len(a), B, len(b), K, len(k), mode, words, 16, C.byref(bits),
+                                                  None, None)
+    assert rc == 0, lib.fhe_last_error()
+    return sum(words[i] << (64 * i) for i in range(16)), bits.value
+
+
+@pytest.mark.parametrize("mode", [COMPAT, FAST])
+def test_mul_add_columns_simulated(mode):
+    """k + a * b left in column form (the signer's FHE block without its final carry propagation): the
+    columns' value, carries resolved on the host as the decryption does, equals the limbs' value of
+    the normalized mul-add -- compat's lost carries included (8 x 8 limbs of all ones)."""
+    rng = random.Random(11 + mode)
+    shapes = [(8, 1, 8), (1, 8, 8), (8, 8, 8), (2, 3, 1), (8, 8, 0), (3, 2, 5)]
+    for la, lb, lk in shapes:
+        a, b, k = _limbs(rng, la), _limbs(rng, lb), _limbs(rng, lk)
+        val, bits = sim_mul_add_columns(a, b, k, mode)
+        want = sim_mul(a, b, mode, k) if lk else sim_mul(a, b, mode)
+        assert val == R.from_limbs(want), (la, lb, lk)
+        assert bits == 32 * (max(lk, la + lb) + 1)
+    full = [M32 - 1] * 8
+    val, _ = sim_mul_add_columns(full, full, [M32 - 1] * 8, mode)
+    assert val == R.from_limbs(sim_mul(full, full, mode, [M32 - 1] * 8))
