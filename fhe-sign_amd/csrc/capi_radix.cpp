@@ -661,7 +661,15 @@ int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64
             return r;
         };
         const BigUint A = make(la), B = make(lb);
-        BigUint R = lk ? biguint_mul_add(e, A, B, make(lk), mode) : biguint_mul(e, A, B, mode);
+        // FHE_STATS_COLUMNS=1: the signer's column form (biguint_mul_add_columns) instead
+        const char* cv = getenv("FHE_STATS_COLUMNS");
+        BigUint R;
+        std::vector<Blocks> cols;
+        uint32_t nb = 0;
+        if (cv && atoi(cv) != 0)
+            cols = biguint_mul_add_columns(e, A, B, make(lk), mode, &nb);
+        else
+            R = lk ? biguint_mul_add(e, A, B, make(lk), mode) : biguint_mul(e, A, B, mode);
         e.flush();
         *pbs = e.pbs_count;
         *levels = e.levels;

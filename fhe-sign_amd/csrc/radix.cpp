@@ -974,6 +974,10 @@ Radix radix_resize(const Radix& a, uint32_t nblocks) {
 struct ColProblem {
     std::vector<Blocks> cols;  // cols[k]: blocks summing into position k
     uint32_t nblocks;
+    // compression target (compress_columns): every column a sum <= lim (lim0 at position 0) of
+    // <= max_cnt blocks -- the carry propagation's input by default; a decryption's input only needs
+    // each column to fit one block's message and carry space (radix_mul_add_columns)
+    uint32_t lim0 = 7, lim = 6, max_cnt = 3;
 };
 
 static uint32_t col_degree(const Blocks& c) {
@@ -1020,9 +1024,10 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
                 Blocks c;
                 for (Block& b : P.cols[k])
                     if (!(b.trivial() && b.value == 0)) c.push_back(b);
-                const uint32_t lim = k == 0 ? 7 : 6;
+                const uint32_t lim = k == 0 ? P.lim0 : P.lim;
                 uint32_t out_deg = 0, out_noise = 0, out_cnt = 0;
-                if (col_degree(c) + in_deg <= lim && c.size() + in_cnt <= 3 && col_noise(c) + in_noise <= kMaxNoise - 1) {
+                if (col_degree(c) + in_deg <= lim && c.size() + in_cnt <= P.max_cnt &&
+                    col_noise(c) + in_noise <= kMaxNoise - 1) {
                     for (auto& b : c) next[pi][k].push_back(b);
                     in_deg = in_noise = in_cnt = 0;
                     continue;
@@ -1977,6 +1982,12 @@ Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {
 
 std::vector<Blocks> radix_mul_add_columns(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks) {
     std::vector<ColProblem> probs = mul_problems(e, {{&a, &b}}, nblocks, {&c}, true);
+    // compressed until each column fits one block (value <= 15): the columns are then the blocks of a
+    // radix ciphertext with carries, each the (lazy) sum of its column (FHE_COLUMNS_LIM: the bound)
+    const char* lv = getenv("FHE_COLUMNS_LIM");
+    const uint32_t lim = lv ? (uint32_t)std::max(6, std::min(15, atoi(lv))) : 15u;
+    probs[0].lim0 = probs[0].lim = lim;
+    probs[0].max_cnt = 6;
     std::vector<ColProblem*> ptrs{&probs[0]};
     compress_columns(e, ptrs);
     return std::move(probs[0].cols);
