@@ -881,6 +881,7 @@ int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t*
         };
         const Radix A = make(a), B = make(b);
         std::vector<Radix> keep;
+        std::vector<Blocks> cols;
         switch (op) {
         case FHE_HOST_OP_DIVREM: {
             auto qr = radix_divrem(e, A, B);
@@ -897,9 +898,25 @@ int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t*
         case FHE_HOST_OP_MUL_FULL: keep = {radix_mul(e, A, B, 2 * nb)}; break;
         case FHE_HOST_OP_AND: keep = {radix_bitand(e, A, B)}; break;
         case FHE_HOST_OP_MIN: keep = {radix_min(e, A, B)}; break;
+        case FHE_HOST_OP_SCALAR_MAC_COLUMNS: {  // a * m + m, m = b public: the public signer's column form
+            BigConst m((bits + 63) / 64);
+            for (size_t w = 0; w < m.size(); ++w) m[w] = b[w];
+            cols = radix_mul_add_columns(e, A, radix_trivial(m, nb), radix_trivial(m, nb), nb);
+            break;
+        }
         default: engine_check(false, "unknown host op");
         }
         e.flush();
+        if (op == FHE_HOST_OP_SCALAR_MAC_COLUMNS) {
+            column_value(cols, nb, [&](const Block& x) {
+                const int64_t h2 = e.sim_half2(x);
+                engine_check(h2 % 2 == 0 && h2 >= 0 && h2 < 32, "sim columns: a block off its message range");
+                return h2 / 2;
+            }, out, (bits + 63) / 64);
+            if (pbs) *pbs = e.pbs_count;
+            if (levels) *levels = e.levels;
+            return FHE_OK;
+        }
         auto put = [&](const Radix& r, uint64_t* w) {
             const size_t words = (r.nblocks() + 31) / 32;
             for (size_t i = 0; i < words; ++i) w[i] = 0;

@@ -174,3 +174,14 @@ def test_mul_add_columns_simulated(mode):
     full = [M32 - 1] * 8
     val, _ = sim_mul_add_columns(full, full, [M32 - 1] * 8, mode)
     assert val == R.from_limbs(sim_mul(full, full, mode, [M32 - 1] * 8))
+
+
+@pytest.mark.parametrize("bits", [8, 64, 290])
+def test_scalar_mac_columns_simulated(bits):
+    """The public-operand signer's column form (a * m + m with m public, recoded digits, no carry
+    propagation): its value mod 2^bits."""
+    rng = random.Random(bits)
+    M = 1 << bits
+    for a, m in operands(bits, rng, 6):
+        got, _ = sim_radix(11, bits, a, m)
+        assert got == (a * m + m) % M, (bits, hex(a), hex(m))
