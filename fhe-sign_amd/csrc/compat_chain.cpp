@@ -24,6 +24,7 @@
 // whose negacyclic half gives -1/2 for inputs in [-16, 0) -- so the block holds s = beta - 1/2 and
 // every linear use of it adds the 1/2 back as a half-step constant.  The sign input k - g - 1 lies in
 // [-16, 14].
+#include <chrono>
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -94,11 +95,17 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
     const size_t la = A.digits.size(), lb = B.digits.size(), L = la + lb;
     // FHE_CHAIN_PHASES=1 (diagnostic, dry runs): flush and print the bootstrap count after each phase
     static const bool phases = getenv("FHE_CHAIN_PHASES") && atoi(getenv("FHE_CHAIN_PHASES"));
+    const auto t0 = std::chrono::steady_clock::now();
     auto phase = [&](const char* what) {
-        if (!phases || getenv("FHE_CHAIN_NOFLUSH")) return;
+        if (!phases) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (getenv("FHE_CHAIN_NOFLUSH")) {  // host time only
+            fprintf(stderr, "[compat chain] %-28s host %7.1f ms\n", what, ms);
+            return;
+        }
         e.flush();
-        fprintf(stderr, "[compat chain] %-28s %8llu PBS %4llu levels\n", what, (unsigned long long)e.pbs_count,
-                (unsigned long long)e.levels);
+        fprintf(stderr, "[compat chain] %-28s %8llu PBS %4llu levels  host %7.1f ms\n", what,
+                (unsigned long long)e.pbs_count, (unsigned long long)e.levels, ms);
     };
     engine_check(compat_chain_applies(la, lb), "compat chain: limb counts");
     // ---- the 64-bit products a_i * b_j: one batched multiplication, columns compressed but not
