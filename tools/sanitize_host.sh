@@ -4,7 +4,8 @@
 # CPU tests that exercise the host code paths with untrusted or intricate memory handling --
 # the validating deserializers (corrupted / truncated / oversized inputs), key generation and
 # encryption, the BIP-340 signer, the level scheduler and progress marks, and the host-fold / dry
-# engine runs of the BigUintFHE mul (the compat carry-count chain) -- against it.  CPU only: no GPU, and
+# engine runs of the BigUintFHE mul (the compat carry-count chain) and the simulated runs of every radix
+# algorithm (Karatsuba, division, shifts, the column form) -- against it.  CPU only: no GPU, and
 # GPU-side sanitizers are not available on the GPU pool.
 # Usage: tools/sanitize_host.sh [log]   (default log: profiles/r5/sanitize_host_r5.log)
 set -euo pipefail
@@ -27,7 +28,8 @@ RT=$(/opt/rocm/lib/llvm/bin/clang -print-file-name=libclang_rt.asan-x86_64.so)
   UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
   FHE_ROCM_LIB="$PWD/fhe-sign_amd/lib_asan/libfhe_rocm.so" \
     python -m pytest -q -p no:cacheprovider -m "not gpu" tests/test_serialize.py tests/test_keys.py \
-      tests/test_schnorr.py tests/test_scheduler.py tests/test_abi.py tests/test_biguint_host.py 2>&1 || st=$?
+      tests/test_schnorr.py tests/test_scheduler.py tests/test_abi.py tests/test_biguint_host.py \
+      tests/test_radix_sim.py 2>&1 || st=$?
   echo "# exit status: $st"
 } | tee "$LOG"
 grep -q "ERROR: AddressSanitizer\|runtime error:" "$LOG" && { echo "sanitizer findings, see $LOG"; exit 1; }
