@@ -688,7 +688,8 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"batched programmable bootstrap (KS+MS+BR+SE) of {B} 2_2 radix blocks per GPU "
-                        "= one PBS level of BigUintFHE 256-bit mul (configs[1]; 32768 = its widest level)",
+                        "(configs[1]: 32768 = the 256-bit BigUintFHE mul's block products, 128 x 128 pairs x "
+                        "low/high; the r5 Karatsuba-split mul launches them as levels of <= 16384)",
             "batch_pbs_per_gpu": B,
             "params": cl["params"],
             "parallelism": f"replicas x{world}",
