@@ -688,8 +688,9 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"batched programmable bootstrap (KS+MS+BR+SE) of {B} 2_2 radix blocks per GPU "
-                        "(configs[1]: 32768 = the 256-bit BigUintFHE mul's block products, 128 x 128 pairs x "
-                        "low/high; the r5 Karatsuba-split mul launches them as levels of <= 16384)",
+                        "(configs[1]: 32768 = the schoolbook block products of the 256-bit BigUintFHE mul, "
+                        "128 x 128 pairs x low/high; r5's Karatsuba split bootstraps 26.8k (compat) / 13.8k "
+                        "(fast) products, in levels of <= 16384)",
             "batch_pbs_per_gpu": B,
             "params": cl["params"],
             "parallelism": f"replicas x{world}",
