@@ -18,7 +18,7 @@ if os.environ.get("FHE_PROBE_BR"):  # throughput kernel: 4 = br_qy (classic defa
     ctx.set_br_kernel(int(os.environ["FHE_PROBE_BR"]))
 lid = ctx.lut([(m + 1) % 16 for m in range(16)])
 cts = np.stack([ck.encrypt_block(m % 16) for m in range(64)])
-cts = np.ascontiguousarray(np.concatenate([cts] * (B // 64)))
+cts = np.ascontiguousarray(np.concatenate([cts] * max(1, -(-B // 64)))[:B])
 d_in = ctx.alloc(cts.nbytes); d_out = ctx.alloc(cts.nbytes); d_lut = ctx.alloc(B * 4)
 ctx.h2d(d_in, cts); ctx.h2d(d_lut, np.full(B, lid, np.uint32))
 ctx.enable_timing(True)
