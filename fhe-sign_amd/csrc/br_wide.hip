@@ -423,6 +423,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 
         // ---- forward transform (twisted: no twist multiply): A (stages 0,1) -> B -> C -> D
         // (wave-private) -> E (cross-wave)
+        if (G == 1 && p == 1) __builtin_amdgcn_s_setprio(0);  // end of the p = 1 priority window (below)
         ct2(x, ZT[0], ZT[1]);
         xpose_AB(x);                 // A -> B: regs <-> lane bits 5,4
         ct2(x, ZT[2], ZT[3]);
@@ -518,6 +519,13 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the monomial DMA
         if constexpr (G == 1) WSTAMP(7);
         __syncthreads();
+        // Classic: the p = 1 wave of each SIMD is the critical one (it reaches barrier X ~1.6k ticks
+        // after its p = 0 partner, which issues first by age and then waits: profiles/r5/wide_stamps_r5.txt),
+        // so it takes issue priority from here through its inverse, loop tail and next digits, and gives
+        // it back where its forward transform starts (latency-bound, 1.3k ticks alone or shared).
+        // B = 1: 2.08 -> 2.00 ms, B = 256: 2.33 -> 2.26 ms (profiles/r5/wide_prio_ab*_r5.txt); the same
+        // window in the multi-bit kernel (key bundle before the digits) costs 40 %, so it is classic only.
+        if (G == 1 && p == 1) __builtin_amdgcn_s_setprio(2);
         if constexpr (G == 1) WSTAMP(8);
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = inv[xD ^ fx(4 * r)];
