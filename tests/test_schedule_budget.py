@@ -1,0 +1,64 @@
+"""Schedule budgets of the hot-path ops (dry engine, no GPU): the bootstraps and launch levels each op is
+scheduled into (fhe_host_radix_stats / fhe_host_biguint_mul_stats) may not grow past the round-5
+figures -- the op latencies on the GPU follow the level counts (one latency round of ~2.0-2.4 ms each,
+DESIGN.md 5-6), so a change that adds levels shows up here before any GPU run.  Budgets carry a small
+margin over the measured schedule; lowering one when an op improves is the intended maintenance."""
+import ctypes as C
+
+import pytest
+
+from fhe_sign import _lib
+
+DIVREM, MUL, ADD, SUB, SHR, LT, DIV_SCALAR = range(7)
+COMPAT, FAST = 0, 1
+
+
+def radix_stats(op, bits):
+    p, lev = C.c_uint64(), C.c_uint64()
+    lib = _lib.load()
+    assert lib.fhe_host_radix_stats(op, bits, C.byref(p), C.byref(lev), None, 0) == 0, lib.fhe_last_error()
+    return p.value, lev.value
+
+
+def mul_stats(la, lb, lk, mode):
+    p, lev = C.c_uint64(), C.c_uint64()
+    lib = _lib.load()
+    assert lib.fhe_host_biguint_mul_stats(la, lb, lk, mode, C.byref(p), C.byref(lev), None, 0) == 0, \
+        lib.fhe_last_error()
+    return p.value, lev.value
+
+
+# (op, bits): (max bootstraps, max levels) -- measured r5: 127,580/735, 26,166/14, 624/7, 624/7, 2,050/6,
+# 194/7, 14,541/13 at 256 bits
+RADIX_BUDGET = {
+    (DIVREM, 256): (130_000, 735), (DIVREM, 32): (2_050, 75),
+    (MUL, 256): (26_700, 14), (ADD, 256): (640, 7), (SUB, 256): (640, 7),
+    (SHR, 256): (2_100, 6), (SHR, 32): (180, 5), (LT, 256): (200, 7), (DIV_SCALAR, 256): (14_900, 13),
+}
+
+
+@pytest.mark.parametrize("key", sorted(RADIX_BUDGET))
+def test_radix_op_schedule_budget(key):
+    pbs, levels = radix_stats(*key)
+    max_pbs, max_levels = RADIX_BUDGET[key]
+    assert levels <= max_levels and pbs <= max_pbs, (key, pbs, levels)
+
+
+def test_biguint_mul_schedule_budget():
+    """256-bit BigUintFHE mul: compat (the reference's limbs, carry-count chain, Karatsuba limb products)
+    and fast (true product, Karatsuba twice): r5 59,611 PBS / 44 levels and 30,103 / 29."""
+    pbs, levels = mul_stats(8, 8, 0, COMPAT)
+    assert levels <= 44 and pbs <= 61_000, (pbs, levels)
+    pbs, levels = mul_stats(8, 8, 0, FAST)
+    assert levels <= 29 and pbs <= 31_000, (pbs, levels)
+
+
+def test_signer_column_form_schedule_budget(monkeypatch):
+    """sign_fhe_with_k0's FHE block k + e*d' on vector 0's shape (8 x 1 limbs + 8): the column form the
+    signer uses (FHE_STATS_COLUMNS: biguint_mul_add_columns) against the normalized mul-add."""
+    monkeypatch.setenv("FHE_STATS_COLUMNS", "1")
+    pbs, levels = mul_stats(8, 1, 8, COMPAT)
+    assert levels <= 4 and pbs <= 6_500, (pbs, levels)
+    monkeypatch.setenv("FHE_STATS_COLUMNS", "0")
+    pbs_n, levels_n = mul_stats(8, 1, 8, COMPAT)
+    assert levels_n > levels and pbs_n > pbs
