@@ -2520,7 +2520,138 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
     Blocks r;  // remainder, w - 1 blocks before step i
     Radix q;
     q.blocks.resize(n);
-    for (int i = (int)n - 1; i >= 0; --i) {
+    // ---- leading radix-16 steps (two quotient blocks each) while the remainder is narrow: fifteen
+    // subtractions r16 - c d (c = 1..15) sharing their carry levels, the same selector trick with 16
+    // candidates (S_c = G_c - G_(c+1)), q = sum of the 15 borrow bits split into two blocks.  At width
+    // w <= 16 every level stays within one latency round (states 15 (w + 1), selects 16 w), and a step
+    // costs the 2 + P levels of ONE radix-4 step for two quotient blocks.  Its multiples need only d's
+    // low 16 blocks (c d mod 4^16, public-scalar products) and the flags [c d < 4^w] = [d's blocks >= 16
+    // zero] and [d_low <= floor((4^w - 1) / c)] (comparisons with public constants): a setup that fills
+    // the early steps' idle rounds.  FHE_DIV_R16 = the number of leading dividend blocks so handled
+    // (even, <= 16; 0: radix-4 throughout).
+    const char* hv = getenv("FHE_DIV_R16");
+    uint32_t lead = std::min<uint32_t>(hv ? (uint32_t)std::max(0, atoi(hv)) : 16u, 256u);
+    lead = std::min(lead, n) & ~1u;
+    if (lead > 0) {
+        const uint32_t L = lead;
+        // exact low multiples m_c = c (d mod 4^L) on L + 2 blocks (< 15 4^L): their low L blocks are
+        // (c d)_k, k < L, and with d's blocks >= L zero, [c d < 4^w] = [blocks w..L+1 of m_c all zero]
+        const Radix dl = radix_resize(radix_resize(d, L), L + 2);
+        std::vector<Blocks> nd16(16);  // nd16[c][k] = 3 - (c d)_k, k < L (lazy complements)
+        std::vector<Radix> mc(16);
+        for (uint32_t c = 1; c < 16; ++c) {
+            mc[c] = c == 1 ? dl : radix_scalar_mul(e, dl, BigConst{c});
+            for (uint32_t k = 0; k < L; ++k) nd16[c].push_back(block_lazy({{mc[c].blocks[k], -1}}, 3, 3));
+        }
+        // P16[c][w] = 3 [c d < 4^w] (w even): pairwise ANDs of the zero flags of m_c's blocks 2..L+1,
+        // then one lookup over the pairs from w on with P[0][L] = 3 [d's blocks >= L all zero]
+        std::vector<std::vector<Block>> P16(16, std::vector<Block>(L + 1));
+        {
+            std::vector<PbsItem> items;
+            for (uint32_t c = 1; c < 16; ++c)
+                for (uint32_t j = 1; j <= L / 2; ++j) {  // pair j: blocks 2j, 2j + 1
+                    PbsItem it;
+                    it.terms = {{mc[c].blocks[2 * j], 1}, {mc[c].blocks[2 * j + 1], 1}};
+                    it.table = lut1([](uint32_t v) { return v == 0 ? 1u : 0u; });
+                    items.push_back(it);
+                }
+            Blocks pr = e.run(items);
+            // suffix AND over the L / 2 pair flags, kMaxTerms at a time (as P above), the last round
+            // also taking P[0][L]: SF[c][j] = 3 [pairs j.. all zero and d's blocks >= L zero]
+            const uint32_t np = L / 2;
+            std::vector<Blocks> SF(16);
+            for (uint32_t c = 1; c < 16; ++c) SF[c].assign(pr.begin() + (c - 1) * np, pr.begin() + c * np);
+            uint32_t sp = 1;
+            for (bool done = false; !done;) {
+                const bool last = sp * kMaxTerms >= np;
+                items.clear();
+                for (uint32_t c = 1; c < 16; ++c)
+                    for (uint32_t j = 0; j < np; ++j) {
+                        PbsItem it;
+                        uint32_t cnt = 0;
+                        for (uint32_t t = 0; t < (uint32_t)kMaxTerms && j + t * sp < np; ++t, ++cnt)
+                            it.terms.push_back({SF[c][j + t * sp], 1});
+                        uint32_t full = cnt;
+                        if (last) {  // with P[0][L] in {0, 3}
+                            it.terms.push_back({P[0][L], 1});
+                            full += 3;
+                        }
+                        const uint32_t mul = last ? 3u : 1u;
+                        it.table = lut1([full, mul](uint32_t v) { return v == full ? mul : 0u; });
+                        items.push_back(it);
+                    }
+                Blocks o = e.run(items);
+                for (uint32_t c = 1; c < 16; ++c) SF[c].assign(o.begin() + (c - 1) * np, o.begin() + c * np);
+                sp *= kMaxTerms;
+                done = last;
+            }
+            for (uint32_t c = 1; c < 16; ++c)
+                for (uint32_t w = 2; w <= L; w += 2) P16[c][w] = SF[c][w / 2 - 1];
+        }
+        static const auto LUT_Q = lut1([](uint32_t v) { return v; });
+        for (uint32_t st = 0; st < lead / 2; ++st) {
+            const int i = (int)n - 1 - 2 * (int)st;  // blocks i (high) and i - 1 enter
+            const uint32_t w = 2 * st + 2;
+            Blocks r16(w);
+            r16[0] = a.blocks[i - 1];
+            r16[1] = a.blocks[i];
+            for (uint32_t k = 2; k < w; ++k) r16[k] = r[k - 2];
+            std::vector<ColProblem> probs(15);
+            for (uint32_t c = 1; c < 16; ++c) {
+                ColProblem& pc = probs[c - 1];
+                pc.nblocks = w + 2;
+                pc.cols.assign(w + 2, {});
+                for (uint32_t k = 0; k < w; ++k) pc.cols[k] = {r16[k], nd16[c][k]};
+                pc.cols[0].push_back(Block::make_trivial(1));
+                pc.cols[w] = {P16[c][w]};
+            }
+            Blocks G;  // G[c - 1] = 8 ge_c
+            std::vector<Blocks> cur = propagate_carries(e, probs, nullptr, nullptr, &G);
+            std::vector<PbsItem> hs;
+            for (uint32_t k = 0; k < w; ++k)
+                for (uint32_t c = 0; c < 16; ++c) {
+                    std::vector<Term> t;
+                    int32_t cst = 0;
+                    if (c == 0)
+                        cst = 8;
+                    else
+                        t.push_back({G[c - 1], 1});
+                    if (c < 15) t.push_back({G[c], -1});
+                    if (c == 0) {
+                        t.push_back({r16[k], 1});
+                    } else {
+                        for (auto& b : probs[c - 1].cols[k]) t.push_back({b, 1});
+                        if (k > 0) t.push_back({cur[c - 1][k - 1], 1});
+                    }
+                    PbsItem it;
+                    it.raw = true;
+                    it.terms = std::move(t);
+                    it.half_cst = 2 * cst;
+                    it.half_table.resize(16);
+                    for (uint32_t v = 0; v < 16; ++v) it.half_table[v] = 2 * (int32_t)sel_hi[v];
+                    it.raw_degree = 3;
+                    hs.push_back(std::move(it));
+                }
+            {
+                PbsItem qi;
+                for (uint32_t c = 1; c < 16; ++c) qi.terms.push_back({cur[c - 1][w], 1});
+                qi.table = lut1([](uint32_t v) { return v >> 2; });
+                hs.push_back(qi);
+                qi.table = lut1([](uint32_t v) { return v & 3u; });
+                hs.push_back(qi);
+            }
+            Blocks h = e.run(hs);
+            q.blocks[i] = h[16 * w];
+            q.blocks[i - 1] = h[16 * w + 1];
+            r.assign(w, Block());
+            for (uint32_t k = 0; k < w; ++k) {
+                std::vector<Term> t;
+                for (uint32_t c = 0; c < 16; ++c) t.push_back({h[16 * k + c], 1});
+                r[k] = block_lazy(t, 0, 3);
+            }
+        }
+    }
+    for (int i = (int)n - 1 - (int)lead; i >= 0; --i) {
         const uint32_t w = n - (uint32_t)i;
         Blocks r4(w);
         r4[0] = a.blocks[i];
