@@ -2530,7 +2530,7 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
     // the early steps' idle rounds.  FHE_DIV_R16 = the number of leading dividend blocks so handled
     // (even, <= 16; 0: radix-4 throughout).
     const char* hv = getenv("FHE_DIV_R16");
-    uint32_t lead = std::min<uint32_t>(hv ? (uint32_t)std::max(0, atoi(hv)) : 16u, 256u);
+    uint32_t lead = std::min<uint32_t>(hv ? (uint32_t)std::max(0, atoi(hv)) : 32u, 256u);
     lead = std::min(lead, n) & ~1u;
     if (lead > 0) {
         const uint32_t L = lead;
