@@ -2524,11 +2524,12 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
     // subtractions r16 - c d (c = 1..15) sharing their carry levels, the same selector trick with 16
     // candidates (S_c = G_c - G_(c+1)), q = sum of the 15 borrow bits split into two blocks.  At width
     // w <= 16 every level stays within one latency round (states 15 (w + 1), selects 16 w), and a step
-    // costs the 2 + P levels of ONE radix-4 step for two quotient blocks.  Its multiples need only d's
-    // low 16 blocks (c d mod 4^16, public-scalar products) and the flags [c d < 4^w] = [d's blocks >= 16
-    // zero] and [d_low <= floor((4^w - 1) / c)] (comparisons with public constants): a setup that fills
-    // the early steps' idle rounds.  FHE_DIV_R16 = the number of leading dividend blocks so handled
-    // (even, <= 16; 0: radix-4 throughout).
+    // costs the 2 + P levels of ONE radix-4 step for two quotient blocks.  Its multiples need only
+    // d mod 4^L (L = lead: exact products c (d mod 4^L) on L + 2 blocks, public-scalar: one propagation) and
+    // the flags [c d < 4^w] = [d's blocks >= L zero] and [blocks w..L+1 of c (d mod 4^L) zero]: a setup
+    // that fills the early steps' idle rounds.  FHE_DIV_R16 = the number of leading dividend blocks so
+    // handled (read per call; rounded down to even, capped at the width; default 32, 0: radix-4
+    // throughout; same-process A/B in DESIGN.md 6).
     const char* hv = getenv("FHE_DIV_R16");
     uint32_t lead = std::min<uint32_t>(hv ? (uint32_t)std::max(0, atoi(hv)) : 32u, 256u);
     lead = std::min(lead, n) & ~1u;

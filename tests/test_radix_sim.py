@@ -185,3 +185,28 @@ def test_scalar_mac_columns_simulated(bits):
     for a, m in operands(bits, rng, 6):
         got, _ = sim_radix(11, bits, a, m)
         assert got == (a * m + m) % M, (bits, hex(a), hex(m))
+
+
+@pytest.mark.parametrize("lead", ["0", "2", "6", "16", "256"])
+@pytest.mark.parametrize("bits", [16, 32, 64])
+def test_encrypted_divrem_radix16_lead_simulated(monkeypatch, lead, bits):
+    """The leading radix-16 steps (FHE_DIV_R16 = dividend blocks taken two at a time before the radix-4
+    steps; 256 = every step) on divisors whose multiples c*d (c = 1..15) sit at the window boundaries
+    4^w of the early steps, where the [c*d < 4^w] flags (d's high blocks zero and the exact low multiple
+    c*(d mod 4^L) below 4^w) decide the candidate set."""
+    monkeypatch.setenv("FHE_DIV_R16", lead)
+    rng = random.Random(bits * 31 + int(lead))
+    M = 1 << bits
+    divisors = {1, 2, 3, 5, 15, 16, 17, M - 1, M // 2, M // 2 + 1}
+    for w in (1, 2, 3, 4, 6):
+        for c in (1, 3, 5, 7, 11, 15):
+            for delta in (-1, 0, 1):
+                d = (4 ** w) // c + delta
+                if 0 < d < M:
+                    divisors.add(d)
+    divisors = sorted(divisors)
+    rng.shuffle(divisors)
+    for d in divisors[:14]:
+        for a in (M - 1, rng.getrandbits(bits), d * rng.randrange(1, 16) + rng.randrange(d)):
+            a %= M
+            assert sim_radix(DIVREM, bits, a, d) == expect(DIVREM, bits, a, d), (lead, bits, hex(a), hex(d))
