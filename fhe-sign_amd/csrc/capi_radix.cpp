@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <cstring>
 #include <unordered_map>
+#include <unordered_set>
 #include <memory>
 #include <string>
 #include <stdexcept>
@@ -502,7 +503,7 @@ int fhe_biguint_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint32_t* limbs, s
     if (rc) return rc;
     if (!ck || !out || (n && !limbs)) return FHE_ERR_INVALID;
     return guarded([&] {
-        auto* b = new fhe_biguint();
+        auto b = std::make_unique<fhe_biguint>();
         std::vector<uint64_t> ct(n * kLimbBlocks * kBigCt), pts(n * kLimbBlocks);
         for (size_t i = 0; i < n; ++i)
             for (uint32_t k = 0; k < kLimbBlocks; ++k)
@@ -514,7 +515,7 @@ int fhe_biguint_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint32_t* limbs, s
             r.blocks.assign(all.begin() + i * kLimbBlocks, all.begin() + (i + 1) * kLimbBlocks);
             b->v.digits.push_back(std::move(r));
         }
-        *out = b;
+        *out = b.release();
         return FHE_OK;
     });
 }
@@ -593,9 +594,9 @@ int fhe_biguint_add(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, int 
     if (rc) return rc;
     if (!a || !b || !out) return FHE_ERR_INVALID;
     return guarded([&] {
-        auto* r = new fhe_biguint();
+        auto r = std::make_unique<fhe_biguint>();
         r->v = biguint_add(*c->engine, a->v, b->v, mode);
-        *out = r;
+        *out = r.release();
         return FHE_OK;
     });
 }
@@ -605,9 +606,9 @@ int fhe_biguint_mul(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, int 
     if (rc) return rc;
     if (!a || !b || !out) return FHE_ERR_INVALID;
     return guarded([&] {
-        auto* r = new fhe_biguint();
+        auto r = std::make_unique<fhe_biguint>();
         r->v = biguint_mul(*c->engine, a->v, b->v, mode);
-        *out = r;
+        *out = r.release();
         return FHE_OK;
     });
 }
@@ -722,9 +723,9 @@ int fhe_biguint_mul_add_columns(fhe_ctx* c, const fhe_biguint* a, const fhe_bigu
     if (rc) return rc;
     if (!a || !b || !k || !out || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
     return guarded([&] {
-        auto* r = new fhe_columns();
+        auto r = std::make_unique<fhe_columns>();
         r->cols = biguint_mul_add_columns(*c->engine, a->v, b->v, k->v, mode, &r->nblocks);
-        *out = r;
+        *out = r.release();
         return FHE_OK;
     });
 }
@@ -737,11 +738,11 @@ int fhe_radix_scalar_mul_add_columns(fhe_ctx* c, const fhe_radix* a, const uint6
     if (!a || !out || (!m && nm) || (!k && nk)) return FHE_ERR_INVALID;
     const BigConst vm = words_of(m, nm), vk = words_of(k, nk);
     return guarded([&] {
-        auto* r = new fhe_columns();
+        auto r = std::make_unique<fhe_columns>();
         const uint32_t nb = a->r.nblocks();
         r->cols = radix_mul_add_columns(*c->engine, a->r, radix_trivial(vm, nb), radix_trivial(vk, nb), nb);
         r->nblocks = nb;
-        *out = r;
+        *out = r.release();
         return FHE_OK;
     });
 }
@@ -763,8 +764,9 @@ int fhe_columns_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_columns*
         // every slot block (lazy entries: their terms) in one download
         std::vector<const Block*> enc;
         std::vector<const uint64_t*> keys;
+        std::unordered_set<const uint64_t*> seen;
         auto want = [&](const Block& b) {
-            if (std::find(keys.begin(), keys.end(), b.ptr()) != keys.end()) return;
+            if (!seen.insert(b.ptr()).second) return;
             keys.push_back(b.ptr());
             enc.push_back(&b);
         };
@@ -940,9 +942,9 @@ int fhe_biguint_mul_add(fhe_ctx* c, const fhe_biguint* a, const fhe_biguint* b, 
     if (rc) return rc;
     if (!a || !b || !k || !out) return FHE_ERR_INVALID;
     return guarded([&] {
-        auto* r = new fhe_biguint();
+        auto r = std::make_unique<fhe_biguint>();
         r->v = biguint_mul_add(*c->engine, a->v, b->v, k->v, mode);
-        *out = r;
+        *out = r.release();
         return FHE_OK;
     });
 }
