@@ -704,7 +704,11 @@ int fhe_host_radix_stats(int op, uint32_t bits, uint64_t* pbs, uint64_t* levels,
         case FHE_HOST_OP_SUB: keep = {radix_sub(e, A, B)}; break;
         case FHE_HOST_OP_SHR: keep = {radix_shr(e, A, B)}; break;
         case FHE_HOST_OP_LT: keep = {Radix{{radix_lt(e, A, B)}}}; break;
-        case FHE_HOST_OP_DIV_SCALAR: keep = {radix_scalar_div(e, A, BigConst{0xC0FFEE01u})}; break;
+        case FHE_HOST_OP_DIV_SCALAR: {  // FHE_STATS_DIVISOR (hex, <= 64 bits): another divisor's schedule
+            const char* dv = getenv("FHE_STATS_DIVISOR");
+            keep = {radix_scalar_div(e, A, BigConst{dv ? strtoull(dv, nullptr, 16) : 0xC0FFEE01u})};
+            break;
+        }
         default: engine_check(false, "unknown host op");
         }
         e.flush();
@@ -871,7 +875,7 @@ int fhe_host_sim_biguint_mul_add_columns(const uint32_t* a, size_t la, const uin
 int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t* b, uint64_t* out, uint64_t* out2,
                        uint64_t* pbs, uint64_t* levels) {
     if (!a || !b || !out || bits < 2 || bits % 2 || bits > FHE_RADIX_MAX_BITS) return FHE_ERR_INVALID;
-    if (op == FHE_HOST_OP_DIVREM && !out2) return FHE_ERR_INVALID;
+    if ((op == FHE_HOST_OP_DIVREM || op == FHE_HOST_OP_DIVREM_CLEAR) && !out2) return FHE_ERR_INVALID;
     return guarded([&] {
         fhe_ctx c;
         Engine e(&c, Engine::kSim);
@@ -900,6 +904,12 @@ int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t*
         case FHE_HOST_OP_MUL_FULL: keep = {radix_mul(e, A, B, 2 * nb)}; break;
         case FHE_HOST_OP_AND: keep = {radix_bitand(e, A, B)}; break;
         case FHE_HOST_OP_MIN: keep = {radix_min(e, A, B)}; break;
+        case FHE_HOST_OP_DIVREM_CLEAR: {  // a / b, a % b with b public (sim only)
+            BigConst d((bits + 63) / 64);
+            for (size_t w = 0; w < d.size(); ++w) d[w] = b[w];
+            keep = {radix_scalar_div(e, A, d), radix_scalar_rem(e, A, d)};
+            break;
+        }
         case FHE_HOST_OP_SCALAR_MAC_COLUMNS: {  // a * m + m, m = b public: the public signer's column form
             BigConst m((bits + 63) / 64);
             for (size_t w = 0; w < m.size(); ++w) m[w] = b[w];
@@ -929,7 +939,7 @@ int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t*
             }
         };
         put(keep[0], out);
-        if (op == FHE_HOST_OP_DIVREM) put(keep[1], out2);
+        if (op == FHE_HOST_OP_DIVREM || op == FHE_HOST_OP_DIVREM_CLEAR) put(keep[1], out2);
         if (pbs) *pbs = e.pbs_count;
         if (levels) *levels = e.levels;
         return FHE_OK;

@@ -2157,6 +2157,228 @@ static void choose_multiplier(const BigConst& d, uint32_t N, BigConst* m, uint32
     *sh = shpost;
 }
 
+// ---- scalar division by a residue split (divisors narrow against the dividend)
+// a = sum_p a_p 4^p with 4^p = Q_p d + R_p (public) gives a = d T + S, T = sum_p a_p Q_p and
+// S = sum_p a_p R_p < 3 n d, so q = T + floor(S / d) and r = S mod d.  T is a triangle of public-
+// scalar entries (Q_p has ~p - dl/2 base-4 digits: ~(n - dl/2)^2 / 2 entries against the multiplier
+// method's n (n + 1)) and is compressed on its own, off the critical path.  S is narrow (N_S =
+// dl + log2(3n) bits): its columns are compressed exactly (plain digits, no negative constant, so
+// nothing wraps) and split by one level into clean blocks lo_k + 4 hi_k; with m, sh the multiplier of
+// d for width N_S and K = N_S + sh, h = ceil(K / 2), floor(S / d) = floor(S m' / 4^h), m' = m 2^(2h - K),
+// so ONE propagation of V = T 4^h + S m' gives q = floor(V / 4^h) (V's blocks from h on).  256-bit
+// / u32: 14.5k -> 8.3k bootstraps, 13 -> 17 levels (dry schedule); same-process A/B 114 -> 78 ms
+// (DESIGN.md 6).  The remainder needs S only (S propagated, divided by the multiplier method,
+// r = S - d floor(S / d)).
+// FHE_SCALAR_DIV_RESIDUE (read per call): 0 off, 1 wherever valid, unset = the size rule (dividends of
+// >= 64 blocks: the dry model and the A/B favour the split there for every divisor width it admits).
+static bool residue_split(uint32_t n, uint32_t dl) {
+    if (dl + 12 > n) return false;  // S would not be narrow (the size rule implies it)
+    const char* v = getenv("FHE_SCALAR_DIV_RESIDUE");
+    if (v) return atoi(v) != 0;
+    return n >= 64;
+}
+
+// entries c_p a_p at the positions of c_p's base-4 digits (no 4^p shift).  recode: digits in
+// {-1, 0, 1, 2} with -x entered as 3 - x, as scalar_products, and the public constant reduced mod
+// 4^nblocks into trivial entries (the columns then sum to the value mod 4^nblocks); with `excess` the
+// -3's are left out instead and returned, E = sum 3 4^q (the columns sum to value + E exactly, every
+// entry and constant nonnegative); plain: digits 0..3 as x, 2x, 3x (the columns sum to the value)
+static void const_products(const Radix& a, const std::vector<BigConst>& c, uint32_t nblocks, std::vector<Blocks>& cols,
+                           bool recode, BigConst* excess = nullptr) {
+    std::vector<int64_t> kc(nblocks + 1, 0), ex(nblocks + 1, 0);
+    for (uint32_t p = 0; p < a.nblocks() && p < c.size(); ++p) {
+        const Block& x = a.blocks[p];
+        const uint32_t nd = (big_bitlen(c[p]) + 1) / 2;
+        int32_t carry = 0;
+        for (uint32_t q = 0; q <= nd && q < nblocks; ++q) {
+            int32_t v = (q < nd ? (int32_t)((c[p][(2 * q) / 64] >> ((2 * q) % 64)) & 3u) : 0) + carry;
+            carry = 0;
+            if (recode && v >= 3) {
+                v -= 4;
+                carry = 1;
+            }
+            if (v == 0) continue;
+            if (x.trivial()) {
+                kc[q] += (int64_t)v * x.value;
+                continue;
+            }
+            engine_check(x.degree <= 3 && !x.lazy(), "scalar division needs clean operands");
+            if (v == 1) {
+                cols[q].push_back(x);
+            } else if (v > 1) {
+                cols[q].push_back(block_lazy({{x, v}}, 0, (uint32_t)v * x.degree));
+            } else {
+                cols[q].push_back(block_lazy({{x, -1}}, 3, 3));
+                if (excess)
+                    ex[q] += 3;
+                else
+                    kc[q] -= 3;
+            }
+        }
+    }
+    if (excess) {  // E = sum_q ex[q] 4^q
+        BigConst E;
+        for (uint32_t q = nblocks + 1; q-- > 0;) {
+            E = big_add(big_add(E, E), big_add(E, E));
+            E = big_add(E, BigConst{(uint64_t)ex[q]});
+        }
+        *excess = E;
+    }
+    for (uint32_t k = 0; k < nblocks; ++k) {
+        int64_t cy = kc[k] >= 0 ? kc[k] / 4 : -((-kc[k] + 3) / 4);
+        kc[k] -= 4 * cy;
+        kc[k + 1] += cy;
+        if (kc[k]) cols[k].push_back(Block::make_trivial((uint32_t)kc[k]));
+    }
+    engine_check((recode && !excess) || kc[nblocks] == 0, "scalar division: exact columns overflow their width");
+}
+
+static BigConst big_mul(const BigConst& x, const BigConst& y) {
+    BigConst r(x.size() + y.size() + 1, 0);
+    for (size_t i = 0; i < x.size(); ++i) {
+        unsigned __int128 c = 0;
+        for (size_t j = 0; j < y.size(); ++j) {
+            c += (unsigned __int128)x[i] * y[j] + r[i + j];
+            r[i + j] = (uint64_t)c;
+            c >>= 64;
+        }
+        for (size_t k = i + y.size(); c; ++k) {
+            c += r[k];
+            r[k] = (uint64_t)c;
+            c >>= 64;
+        }
+    }
+    return big_norm(r);
+}
+
+// q (rem == nullptr) or r (into *rem) by the residue split; d >= 3 and not a power of two
+static Radix scalar_div_residue(Engine& e, const Radix& a, const BigConst& d, Radix* rem) {
+    const uint32_t n = a.nblocks();
+    std::vector<BigConst> Q(n), R(n);
+    BigConst q, r{1};  // 4^0 = 0 d + 1
+    auto shl2 = [](const BigConst& v) { return big_add(big_add(v, v), big_add(v, v)); };
+    for (uint32_t p = 0; p < n; ++p) {
+        Q[p] = big_norm(q);
+        R[p] = big_norm(r);
+        BigConst r4 = shl2(r);  // 4^(p+1) = 4 q d + 4 r
+        uint64_t c = 0;
+        while (big_cmp(r4, d) >= 0) {
+            big_sub_inplace(r4, d);
+            r4 = big_norm(r4);
+            ++c;
+        }
+        q = big_add(shl2(q), BigConst{c});
+        r = r4;
+    }
+    const BigConst bound = big_mul(d, BigConst{3ull * n});  // S < 3 n d
+    const uint32_t NS = big_bitlen(bound), ws = (NS + 1) / 2;
+    // S + E, E = the recoded products' public excess (<= sum_p 4 R_p < 4 n d): exact on we blocks
+    const uint32_t we = (big_bitlen(big_mul(d, BigConst{8ull * n})) + 1) / 2;
+    if (rem) {
+        std::vector<ColProblem> ps(1);
+        ps[0].nblocks = ws;
+        ps[0].cols.assign(ws, {});
+        const_products(a, R, ws, ps[0].cols, true);
+        const Radix S = propagate_many(e, ps)[0];
+        const Radix qs = radix_scalar_div(e, S, d);  // S is narrow: the multiplier method
+        *rem = radix_resize(radix_sub(e, S, radix_scalar_mul(e, qs, d)), n);
+        return Radix{};
+    }
+    // T's columns: compressed on their own (nothing on the S path waits for them)
+    ColProblem PT;
+    PT.nblocks = n;
+    PT.cols.assign(n, {});
+    const_products(a, Q, n, PT.cols, true);
+    // S's columns, exact: compressed, then each column sum v_k (<= 7) split into lo_k, hi_k
+    ColProblem PS;
+    PS.nblocks = we;
+    PS.cols.assign(we, {});
+    BigConst E;
+    const_products(a, R, we, PS.cols, true, &E);
+    // FHE_RESIDUE_PHASES: bootstraps per phase (each phase flushed on its own: diagnostics only)
+    static const bool dbg = getenv("FHE_RESIDUE_PHASES") != nullptr;
+    uint64_t p0 = 0;
+    auto phase = [&](const char* what) {
+        if (!dbg) return;
+        e.flush();
+        if (what) fprintf(stderr, "[residue] %-12s %llu PBS\n", what, (unsigned long long)(e.pbs_count - p0));
+        p0 = e.pbs_count;
+    };
+    phase(nullptr);
+    std::vector<ColProblem*> pt{&PT};
+    compress_columns(e, pt);
+    phase("T compress");
+    std::vector<ColProblem*> psv{&PS};
+    compress_columns(e, psv);
+    phase("S compress");
+    static const auto LO = lut1([](uint32_t v) { return v & 3; });
+    static const auto HI = lut1([](uint32_t v) { return (v >> 2) & 3; });
+    Radix L, H;
+    L.blocks.assign(we, Block::make_trivial(0));
+    H.blocks.assign(we, Block::make_trivial(0));
+    std::vector<PbsItem> items;
+    std::vector<uint32_t> at;
+    for (uint32_t k = 0; k < we; ++k) {
+        const Blocks& col = PS.cols[k];
+        if (!col_live(col)) continue;
+        if (col.size() == 1 && !col[0].lazy() && col[0].degree <= 3) {
+            L.blocks[k] = col[0];
+            continue;
+        }
+        PbsItem it;
+        uint32_t cst = 0;
+        for (const Block& b : col) {
+            if (b.trivial()) cst += b.value;
+            else it.terms.push_back({b, 1});
+        }
+        it.cst = cst;
+        engine_check(col_degree(col) <= 15, "scalar division: S column above one block");
+        it.table = LO;
+        items.push_back(it);
+        it.table = HI;
+        items.push_back(it);
+        at.push_back(k);
+    }
+    const Blocks outs = e.run(items);
+    for (size_t i = 0; i < at.size(); ++i) {
+        L.blocks[at[i]] = outs[2 * i];
+        if (at[i] + 1 < we) H.blocks[at[i] + 1] = outs[2 * i + 1];  // S + E < 4^we: the top hi is 0
+    }
+    // V = T 4^h + (L + H) m'
+    BigConst m;
+    uint32_t sh;
+    choose_multiplier(d, NS, &m, &sh);
+    const uint32_t K = NS + sh, h = (K + 1) / 2;
+    const BigConst mp = (2 * h > K) ? big_add(m, m) : m;
+    const uint32_t W = n + h, mb = (big_bitlen(mp) + 1) / 2 + 1;
+    const Radix mr = radix_trivial(mp, mb);
+    std::vector<ColProblem> pv(1);
+    pv[0].nblocks = W;
+    pv[0].cols.assign(W, {});
+    std::vector<std::pair<uint32_t, Block>> direct;
+    scalar_products(L, mr, W, direct);
+    scalar_products(H, mr, W, direct);
+    for (auto& dcol : direct) pv[0].cols[dcol.first].push_back(dcol.second);
+    // - E m' mod 4^W as public digits
+    {
+        BigConst c = big_pow2(2 * W);
+        big_sub_inplace(c, big_mul(E, mp));
+        c = big_norm(c);
+        for (uint32_t k = 0; k < W; ++k) {
+            const uint32_t dg = (uint32_t)(((2 * k) / 64 < c.size() ? c[(2 * k) / 64] >> ((2 * k) % 64) : 0) & 3u);
+            if (dg) pv[0].cols[k].push_back(Block::make_trivial(dg));
+        }
+    }
+    for (uint32_t k = 0; k < n; ++k)
+        for (const Block& b : PT.cols[k]) pv[0].cols[k + h].push_back(b);
+    phase("S split");
+    const Radix v = propagate_many(e, pv)[0];
+    phase("final");
+    Radix out;
+    out.blocks.assign(v.blocks.begin() + h, v.blocks.begin() + h + n);
+    return out;
+}
+
 Radix radix_scalar_div(Engine& e, const Radix& a, const BigConst& dd) {
     const uint32_t n = a.nblocks(), N = 2 * n;
     const BigConst d = big_norm(dd);
@@ -2165,6 +2387,7 @@ Radix radix_scalar_div(Engine& e, const Radix& a, const BigConst& dd) {
     if (dl == 1) return a;                                                   // d = 1
     if (big_cmp(d, big_pow2(dl - 1)) == 0) return radix_scalar_shr(e, a, dl - 1);  // 2^k
     if (dl > N) return radix_trivial(0, 0, n);                               // d >= 2^N > a
+    if (residue_split(n, dl)) return scalar_div_residue(e, a, d, nullptr);
     BigConst m;
     uint32_t sh;
     choose_multiplier(d, N, &m, &sh);
@@ -2768,7 +2991,15 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
     return {q, radix_clean(e, Radix{r})};
 }
 
-Radix radix_scalar_rem(Engine& e, const Radix& a, const BigConst& d) {
+Radix radix_scalar_rem(Engine& e, const Radix& a, const BigConst& dd) {
+    const BigConst d = big_norm(dd);
+    engine_check(!d.empty(), "division by zero");
+    const uint32_t dl = big_bitlen(d);
+    if (dl > 1 && big_cmp(d, big_pow2(dl - 1)) != 0 && residue_split(a.nblocks(), dl)) {
+        Radix r;
+        scalar_div_residue(e, a, d, &r);
+        return r;
+    }
     Radix q = radix_scalar_div(e, a, d);
     Radix qd = radix_scalar_mul(e, q, d);
     return radix_sub(e, a, qd);

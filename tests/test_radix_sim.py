@@ -210,3 +210,29 @@ def test_encrypted_divrem_radix16_lead_simulated(monkeypatch, lead, bits):
         for a in (M - 1, rng.getrandbits(bits), d * rng.randrange(1, 16) + rng.randrange(d)):
             a %= M
             assert sim_radix(DIVREM, bits, a, d) == expect(DIVREM, bits, a, d), (lead, bits, hex(a), hex(d))
+
+
+DIVREM_CLEAR = 12
+
+
+@pytest.mark.parametrize("residue", ["0", "1", None])
+@pytest.mark.parametrize("bits", [32, 128, 256])
+def test_scalar_divrem_simulated(monkeypatch, residue, bits):
+    """a / d and a % d for PUBLIC divisors (radix_scalar_div / _rem): the multiplier method
+    (FHE_SCALAR_DIV_RESIDUE=0), the residue split a = d T + S wherever it is valid (1) and the size rule
+    (unset), on divisors from 3 up to beyond the residue split's range, odd and even, 2^k +- 1."""
+    if residue is None:
+        monkeypatch.delenv("FHE_SCALAR_DIV_RESIDUE", raising=False)
+    else:
+        monkeypatch.setenv("FHE_SCALAR_DIV_RESIDUE", residue)
+    rng = random.Random(bits * 7 + (int(residue) if residue else 5))
+    M = 1 << bits
+    divisors = [3, 5, 6, 7, 10, 12, 255, 257, 1000003, 0xC0FFEE01, (1 << 31) - 1, (1 << 32) - 5,
+                rng.getrandbits(20) | 1, rng.getrandbits(40) | 3, rng.getrandbits(bits // 2) | 1]
+    for d in divisors:
+        d %= M
+        if d < 2:
+            continue
+        for a in (M - 1, 0, d - 1, d, rng.getrandbits(bits), d * rng.getrandbits(max(1, bits - d.bit_length()))):
+            a %= M
+            assert sim_radix(DIVREM_CLEAR, bits, a, d) == (a // d, a % d), (residue, bits, hex(a), hex(d))
