@@ -136,3 +136,20 @@ def test_public_scalar_recoding(keys):
     for d in (3, 5, 0xFFFFFFFF, (1 << 64) - 59, (1 << 127) + 1):
         assert (A / d).decrypt(ck) == a // d, hex(d)
         assert (A % d).decrypt(ck) == a % d, hex(d)
+
+
+@pytest.mark.parametrize("method", ["residue", "multiplier"])
+def test_div256_residue_split(keys, method, monkeypatch):
+    """Division by a public divisor, 256-bit dividends: the residue split a = d T + S (default for >= 64
+    blocks; csrc/radix.cpp scalar_div_residue) and the multiplier method (FHE_SCALAR_DIV_RESIDUE=0), on
+    divisors across the split's range (3 up to 116 bits, even ones, 2^k +- 1) and dividends at the
+    edges: quotient and remainder equal floor division."""
+    monkeypatch.setenv("FHE_SCALAR_DIV_RESIDUE", "1" if method == "residue" else "0")
+    ck, _ = keys
+    rng = random.Random(0x5E51)
+    for a, d in [(M256, 3), (rng.getrandbits(256), 10), (rng.getrandbits(256), (1 << 32) - 5),
+                 (12345 * 1000003 + 77, 1000003), (rng.getrandbits(256), rng.getrandbits(64) | 1 << 63),
+                 (rng.getrandbits(256), rng.getrandbits(116) | 1 << 115)]:
+        A = FheUint256.try_encrypt(a, ck)
+        assert (A / d).decrypt(ck) == a // d, (method, hex(d))
+        assert (A % d).decrypt(ck) == a % d, (method, hex(d))
