@@ -875,17 +875,21 @@ int fhe_host_sim_biguint_mul_add_columns(const uint32_t* a, size_t la, const uin
 int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t* b, uint64_t* out, uint64_t* out2,
                        uint64_t* pbs, uint64_t* levels) {
     if (!a || !b || !out || bits < 2 || bits % 2 || bits > FHE_RADIX_MAX_BITS) return FHE_ERR_INVALID;
-    if ((op == FHE_HOST_OP_DIVREM || op == FHE_HOST_OP_DIVREM_CLEAR) && !out2) return FHE_ERR_INVALID;
+    const bool two = op == FHE_HOST_OP_DIVREM || op == FHE_HOST_OP_DIVREM_CLEAR || op == FHE_HOST_OP_DIVREM_CLEAR_MIXED;
+    if (two && !out2) return FHE_ERR_INVALID;
     return guarded([&] {
         fhe_ctx c;
         Engine e(&c, Engine::kSim);
         const uint32_t nb = bits / 2;
-        auto make = [&](const uint64_t* w) {
+        auto make = [&](const uint64_t* w, bool odd_trivial) {
             Radix r;
-            for (uint32_t q = 0; q < nb; ++q) r.blocks.push_back(e.sim_block((uint32_t)(w[q / 32] >> (2 * (q % 32))) & 3u, 3));
+            for (uint32_t q = 0; q < nb; ++q) {
+                const uint32_t v = (uint32_t)(w[q / 32] >> (2 * (q % 32))) & 3u;
+                r.blocks.push_back(odd_trivial && (q & 1) ? Block::make_trivial(v) : e.sim_block(v, 3));
+            }
             return r;
         };
-        const Radix A = make(a), B = make(b);
+        const Radix A = make(a, op == FHE_HOST_OP_DIVREM_CLEAR_MIXED), B = make(b, false);
         std::vector<Radix> keep;
         std::vector<Blocks> cols;
         switch (op) {
@@ -904,7 +908,8 @@ int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t*
         case FHE_HOST_OP_MUL_FULL: keep = {radix_mul(e, A, B, 2 * nb)}; break;
         case FHE_HOST_OP_AND: keep = {radix_bitand(e, A, B)}; break;
         case FHE_HOST_OP_MIN: keep = {radix_min(e, A, B)}; break;
-        case FHE_HOST_OP_DIVREM_CLEAR: {  // a / b, a % b with b public (sim only)
+        case FHE_HOST_OP_DIVREM_CLEAR:
+        case FHE_HOST_OP_DIVREM_CLEAR_MIXED: {  // a / b, a % b with b public (sim only)
             BigConst d((bits + 63) / 64);
             for (size_t w = 0; w < d.size(); ++w) d[w] = b[w];
             keep = {radix_scalar_div(e, A, d), radix_scalar_rem(e, A, d)};
@@ -939,7 +944,7 @@ int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t*
             }
         };
         put(keep[0], out);
-        if (op == FHE_HOST_OP_DIVREM || op == FHE_HOST_OP_DIVREM_CLEAR) put(keep[1], out2);
+        if (two) put(keep[1], out2);
         if (pbs) *pbs = e.pbs_count;
         if (levels) *levels = e.levels;
         return FHE_OK;

@@ -2199,7 +2199,10 @@ static void const_products(const Radix& a, const std::vector<BigConst>& c, uint3
             }
             if (v == 0) continue;
             if (x.trivial()) {
-                kc[q] += (int64_t)v * x.value;
+                if (excess && v < 0)
+                    ex[q] += (int64_t)x.value;  // -x.value left out: the excess takes it
+                else
+                    kc[q] += (int64_t)v * x.value;
                 continue;
             }
             engine_check(x.degree <= 3 && !x.lazy(), "scalar division needs clean operands");

@@ -340,6 +340,7 @@ int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64
 #define FHE_HOST_OP_MIN 10
 #define FHE_HOST_OP_SCALAR_MAC_COLUMNS 11 /* a * b + b, b public, in column form (sim only) */
 #define FHE_HOST_OP_DIVREM_CLEAR 12       /* a / b and a % b, b public (sim only) */
+#define FHE_HOST_OP_DIVREM_CLEAR_MIXED 13 /* the same with a's odd blocks trivial (sim only) */
 int fhe_host_radix_stats(int op, uint32_t bits, uint64_t* pbs, uint64_t* levels, uint32_t* level_sizes, size_t cap);
 /* Simulated runs (no GPU, no key): operands are "encrypted" blocks whose plaintext the engine shadows
  * on the host, so every encrypted code path runs (no trivial folding) while each bootstrap is

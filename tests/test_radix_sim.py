@@ -212,7 +212,7 @@ def test_encrypted_divrem_radix16_lead_simulated(monkeypatch, lead, bits):
             assert sim_radix(DIVREM, bits, a, d) == expect(DIVREM, bits, a, d), (lead, bits, hex(a), hex(d))
 
 
-DIVREM_CLEAR = 12
+DIVREM_CLEAR, DIVREM_CLEAR_MIXED = 12, 13
 
 
 @pytest.mark.parametrize("residue", ["0", "1", None])
@@ -236,3 +236,5 @@ def test_scalar_divrem_simulated(monkeypatch, residue, bits):
         for a in (M - 1, 0, d - 1, d, rng.getrandbits(bits), d * rng.getrandbits(max(1, bits - d.bit_length()))):
             a %= M
             assert sim_radix(DIVREM_CLEAR, bits, a, d) == (a // d, a % d), (residue, bits, hex(a), hex(d))
+            # a's odd blocks trivial (public constants inside the dividend: the exact columns' excess)
+            assert sim_radix(DIVREM_CLEAR_MIXED, bits, a, d) == (a // d, a % d), (residue, bits, hex(a), hex(d))
