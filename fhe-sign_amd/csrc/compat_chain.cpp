@@ -122,7 +122,12 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
     // P + q 2^64, i.e. hi(P) = hi_cs + c_P + 2^32 (column 32 - q); a MID addend takes column 32 - q
     // into the limb's overflow O below)
     std::vector<int64_t> excess;
-    std::vector<std::vector<Blocks>> PC = radix_mul_many_columns(e, ops, 2 * kLimbBlocks, &excess);
+    // the high half (hi(P) columns) is read only by the prefix sums, whose inputs take a previous prefix
+    // column (<= 6) plus the product column: <= 9 there suffices (FHE_CHAIN_HI_LIM, read per call)
+    const char* hv = getenv("FHE_CHAIN_HI_LIM");
+    const uint32_t hi_lim = hv ? (uint32_t)std::max(6, std::min(9, atoi(hv))) : 9u;
+    std::vector<std::vector<Blocks>> PC = radix_mul_many_columns(e, ops, 2 * kLimbBlocks, &excess, kLimbBlocks, hi_lim);
+    phase("product columns");
     {
         // entries must be fresh-noise blocks for the accumulation's noise budget (lazy multiples of a
         // public block -- only from trivially encrypted limbs -- are refreshed)
@@ -141,6 +146,7 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
             for (size_t k = 0; k < outs.size(); ++k) *at[k] = outs[k];
         }
     }
+    phase("refresh");
     Blocks cP;
     {
         std::vector<std::vector<Blocks>> lo(PC.size());

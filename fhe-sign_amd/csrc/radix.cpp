@@ -978,6 +978,9 @@ struct ColProblem {
     // <= max_cnt blocks -- the carry propagation's input by default; a decryption's input only needs
     // each column to fit one block's message and carry space (radix_mul_add_columns)
     uint32_t lim0 = 7, lim = 6, max_cnt = 3;
+    // columns >= hi_from: their own target (a consumer that reads them through a wider input, e.g. the
+    // compat chain's prefix sums: radix_mul_many_columns lim_hi)
+    uint32_t hi_from = ~0u, lim_hi = 6, max_cnt_hi = 3;
 };
 
 static uint32_t col_degree(const Blocks& c) {
@@ -1024,9 +1027,11 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
                 Blocks c;
                 for (Block& b : P.cols[k])
                     if (!(b.trivial() && b.value == 0)) c.push_back(b);
-                const uint32_t lim = k == 0 ? P.lim0 : P.lim;
+                const bool hi_col = k >= P.hi_from;
+                const uint32_t lim = k == 0 ? P.lim0 : hi_col ? P.lim_hi : P.lim;
+                const uint32_t max_cnt = hi_col ? P.max_cnt_hi : P.max_cnt;
                 uint32_t out_deg = 0, out_noise = 0, out_cnt = 0;
-                if (col_degree(c) + in_deg <= lim && c.size() + in_cnt <= P.max_cnt &&
+                if (col_degree(c) + in_deg <= lim && c.size() + in_cnt <= max_cnt &&
                     col_noise(c) + in_noise <= kMaxNoise - 1) {
                     for (auto& b : c) next[pi][k].push_back(b);
                     in_deg = in_noise = in_cnt = 0;
@@ -1843,7 +1848,15 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
         }
         std::vector<ColProblem> mp = mul_problems_ops(e, mops, {}, true, &mq, min_n);
         std::vector<ColProblem*> ptrs;
-        for (auto& p : zp) ptrs.push_back(&p);  // m enters uncompressed (once, no copy)
+        // z0, z2 compressed to column sums <= 8 of <= 4 blocks (FHE_KARA_ZLIM, read once; 6 = the
+        // propagation's own target): the combination re-compresses them anyway, and the looser target
+        // saves a round's lo/hi pairs (dry: fast 256-bit mul 30.1k -> 29.8k, compat 58.3k -> 57.6k)
+        static const uint32_t zlim = getenv("FHE_KARA_ZLIM") ? (uint32_t)std::max(6, std::min(12, atoi(getenv("FHE_KARA_ZLIM")))) : 8u;
+        for (auto& p : zp) {  // m enters uncompressed (once, no copy)
+            p.lim = p.lim0 = zlim;
+            p.max_cnt = zlim > 6 ? 4 : 3;
+            ptrs.push_back(&p);
+        }
         compress_columns(e, ptrs);
         for (size_t j = 0; j < kara.size(); ++j) {
             const size_t i = kara[j];
@@ -1950,7 +1963,8 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
 
 std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
                                                         const std::vector<std::pair<const Radix*, const Radix*>>& ops,
-                                                        uint32_t nblocks, std::vector<int64_t>* excess) {
+                                                        uint32_t nblocks, std::vector<int64_t>* excess,
+                                                        uint32_t hi_from, uint32_t lim_hi) {
     std::vector<ColProblem> probs;
     if (excess) {  // exact column sets, Karatsuba-split where eligible (see mul_problems_ops)
         std::vector<MulOp> m;
@@ -1960,7 +1974,14 @@ std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
         probs = mul_problems(e, ops, nblocks, {}, false);
     }
     std::vector<ColProblem*> ptrs;
-    for (auto& p : probs) ptrs.push_back(&p);
+    for (auto& p : probs) {
+        if (lim_hi) {
+            p.hi_from = hi_from;
+            p.lim_hi = lim_hi;
+            p.max_cnt_hi = 4;
+        }
+        ptrs.push_back(&p);
+    }
     compress_columns(e, ptrs);
     std::vector<std::vector<Blocks>> res;
     for (size_t i = 0; i < probs.size(); ++i) {

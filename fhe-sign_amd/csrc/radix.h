@@ -270,10 +270,12 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
 // exactly the product when it fits (non-negative entries cannot wrap below it).  With `excess`,
 // full products may be Karatsuba-split: product i then has nblocks + 1 columns summing to the product
 // + (*excess)[i] 4^nblocks (a public q <= 2; column nblocks holds at most q), else nblocks columns
-// and q = 0.
+// and q = 0.  lim_hi > 0: the columns from hi_from on only compressed to sums <= lim_hi of <= 4 blocks
+// (for a consumer that reads them through a wider input).
 std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
                                                         const std::vector<std::pair<const Radix*, const Radix*>>& ops,
-                                                        uint32_t nblocks, std::vector<int64_t>* excess = nullptr);
+                                                        uint32_t nblocks, std::vector<int64_t>* excess = nullptr,
+                                                        uint32_t hi_from = 0, uint32_t lim_hi = 0);
 // a * b + c (wrapping at nblocks), one carry propagation.
 Radix radix_mul_add(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks);
 // a * b + c as compressed columns (each <= 3 blocks summing <= 6), value mod 4^nblocks; no carry
