@@ -92,6 +92,11 @@ constexpr int XT_SZ = 20 + 68;
 #ifndef QY_PEARLY
 #define QY_PEARLY 0
 #endif
+// the late key slices ((q & 3) >= QY_KSPLIT): 0 (default) issued after the B' -> E barrier; 1 right
+// after the B' stores, before it (x is dead there, so the slices take its registers: same peak)
+#ifndef QY_KLATE_PRE
+#define QY_KLATE_PRE 0
+#endif
 
 template <int K, class F>
 FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
@@ -374,6 +379,13 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
             issue(4, Ga);
             __builtin_amdgcn_sched_barrier(0);
         }
+#if QY_KLATE_PRE
+        if constexpr (G == 1) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if ((q & 3) >= QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        }
+#endif
         cplx e0 = make_double2(1.0, 0.0);
         if constexpr (G == 1) {
             e0 = cmul(Ebn, Fn);  // exact when kk = 0 (Fn = E[0] = 1)
@@ -388,11 +400,13 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
         // ---- phase E: both polynomials at this wave's points, stages 8 (b1), 9 (b0)
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
+#if !QY_KLATE_PRE
         if constexpr (G == 1) {
 #pragma unroll
             for (int q = 0; q < 16; ++q)
                 if ((q & 3) >= QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
         }
+#endif
 #pragma unroll
         for (int r = 0; r < 8; ++r)
             if (!(r & 2)) dit_bfly(x[r], x[r + 2], z8);
