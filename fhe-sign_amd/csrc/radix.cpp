@@ -2296,8 +2296,22 @@ static Radix scalar_div_residue(Engine& e, const Radix& a, const BigConst& d, Ra
     }
     const BigConst bound = big_mul(d, BigConst{3ull * n});  // S < 3 n d
     const uint32_t NS = big_bitlen(bound), ws = (NS + 1) / 2;
-    // S + E, E = the recoded products' public excess (<= sum_p 4 R_p < 4 n d): exact on we blocks
-    const uint32_t we = (big_bitlen(big_mul(d, BigConst{8ull * n})) + 1) / 2;
+    // S + E, E = the recoded products' public excess: at most 3 4^q for every digit -1 at position q of
+    // a recoded R_p (E_max below), so S + E < 3 n d + E_max fits we blocks exactly
+    BigConst emax;
+    for (uint32_t p = 0; p < n; ++p) {
+        const uint32_t nd = (big_bitlen(R[p]) + 1) / 2;
+        int32_t carry = 0;
+        for (uint32_t qd = 0; qd <= nd; ++qd) {
+            int32_t v = (qd < nd ? (int32_t)((R[p][(2 * qd) / 64] >> ((2 * qd) % 64)) & 3u) : 0) + carry;
+            carry = v >= 3 ? 1 : 0;
+            if (v == 3) {
+                BigConst t = big_pow2(2 * qd);
+                emax = big_add(emax, big_add(t, big_add(t, t)));
+            }
+        }
+    }
+    const uint32_t we = (big_bitlen(big_add(bound, emax)) + 1) / 2;
     if (rem) {
         std::vector<ColProblem> ps(1);
         ps[0].nblocks = ws;
