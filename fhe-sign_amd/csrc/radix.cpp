@@ -2469,7 +2469,9 @@ Radix radix_sub(Engine& e, const Radix& a, const Radix& b) {
 }
 
 // carry out of the top of a + ~b + 1  (1 iff a >= b)
-static Block carry_out_ge(Engine& e, const Radix& a, const Radix& b) {
+// plus_one = false: the carry out of a + ~b, i.e. [a - b - 1 >= 0] = [a > b] -- a strict comparison
+// at the same cost, so a < b needs no negation level (radix_lt: [b > a])
+static Block carry_out_ge(Engine& e, const Radix& a, const Radix& b, bool plus_one = true) {
     const uint32_t n = std::max(a.nblocks(), b.nblocks());
     std::vector<PbsItem> items;
     // states of (a_k + 3 - b_k [+1 at k = 0]) directly from a and b (no complement materialized)
@@ -2478,7 +2480,7 @@ static Block carry_out_ge(Engine& e, const Radix& a, const Radix& b) {
         const Block bk = k < b.nblocks() ? b.blocks[k] : Block::make_trivial(0);
         PbsItem it;
         it.terms = {{ak, 1}, {bk, -1}};
-        it.cst = 3 + (k == 0 ? 1 : 0);
+        it.cst = 3 + (k == 0 && plus_one ? 1 : 0);
         it.table = k == 0 ? LUT_GEN() : LUT_STATE();
         items.push_back(it);
     }
@@ -2486,11 +2488,7 @@ static Block carry_out_ge(Engine& e, const Radix& a, const Radix& b) {
     return carry_prefix(e, {cur}, {{n - 1}})[0][n - 1];
 }
 
-Block radix_lt(Engine& e, const Radix& a, const Radix& b) {
-    Block ge = carry_out_ge(e, a, b);
-    std::vector<PbsItem> items{item1(ge, lut1([](uint32_t v) { return v ? 0u : 1u; }))};
-    return e.run(items)[0];
-}
+Block radix_lt(Engine& e, const Radix& a, const Radix& b) { return carry_out_ge(e, b, a, false); }  // [b > a]
 
 // out_k = cond ? x_k : y_k   (two half-selects per block, summed, then one cleaning bootstrap)
 Radix radix_select(Engine& e, const Block& cond, const Radix& x, const Radix& y) {
@@ -2518,8 +2516,9 @@ Radix radix_select(Engine& e, const Block& cond, const Radix& x, const Radix& y)
     return r;
 }
 
-Radix radix_min(Engine& e, const Radix& a, const Radix& b) { return radix_select(e, radix_lt(e, a, b), a, b); }
-Radix radix_max(Engine& e, const Radix& a, const Radix& b) { return radix_select(e, radix_lt(e, a, b), b, a); }
+// min = a < b ? a : b = a >= b ? b : a (and max alike): the select reads [a >= b] itself
+Radix radix_min(Engine& e, const Radix& a, const Radix& b) { return radix_select(e, carry_out_ge(e, a, b), b, a); }
+Radix radix_max(Engine& e, const Radix& a, const Radix& b) { return radix_select(e, carry_out_ge(e, a, b), a, b); }
 
 // Barrel shifter (amount taken mod the bit width, tfhe semantics).  Each stage: out_k =
 // c ? x_{k+s} : x_k as two half-selects whose sum feeds the next stage's lookups directly

@@ -29,13 +29,13 @@ def mul_stats(la, lb, lk, mode):
 
 
 # (op, bits): (max bootstraps, max levels) -- measured r5: 139,578/660 (32 leading radix-16 blocks),
-# 26,166/14, 624/7, 624/7, 2,050/6, 194/7, 8,309/17 (residue split; 14,541/13 by the multiplier) at 256
+# 26,166/14, 624/7, 624/7, 2,050/6, 193/6 (strict comparison, no negation level), 8,309/17 (residue split; 14,541/13 by the multiplier) at 256
 # bits; the 32-bit division trades bootstraps
 # for levels (5,444/43 against 1,997/75 radix-4 only)
 RADIX_BUDGET = {
     (DIVREM, 256): (141_000, 660), (DIVREM, 32): (5_600, 43),
     (MUL, 256): (26_700, 14), (ADD, 256): (640, 7), (SUB, 256): (640, 7),
-    (SHR, 256): (2_100, 6), (SHR, 32): (180, 5), (LT, 256): (200, 7), (DIV_SCALAR, 256): (8_500, 17),
+    (SHR, 256): (2_100, 6), (SHR, 32): (180, 5), (LT, 256): (200, 6), (DIV_SCALAR, 256): (8_500, 17),
 }
 
 
