@@ -132,7 +132,8 @@ def test_biguint_mul_simulated(monkeypatch, kara):
     elif kara:
         monkeypatch.setenv("FHE_KARA_MIN", kara)
     rng = random.Random(5 if kara is None else 6)
-    shapes = [(1, 1), (2, 2), (1, 8), (8, 1), (3, 5), (8, 8)]
+    # 2 <= min <= 8: the carry-count chain; 1 or > 8 limbs (9 x 9, 12 x 4): the wave form; 0: zero
+    shapes = [(1, 1), (2, 2), (1, 8), (8, 1), (3, 5), (8, 8), (9, 9), (12, 4), (0, 3), (3, 0)]
     for la, lb in shapes:
         a, b = _limbs(rng, la), _limbs(rng, lb)
         assert sim_mul(a, b, COMPAT) == R.biguint_mul(a, b), (la, lb)
