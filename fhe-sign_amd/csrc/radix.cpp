@@ -52,6 +52,10 @@ BlockPool::~BlockPool() {
     for (void* c : chunks_) (void)hipFree(c);
 }
 
+// pool growth (FHE_TRACE_LEVELS prints it with the host time of run())
+static double g_pool_grow_ns = 0.0;
+static size_t g_pool_grows = 0;
+
 std::shared_ptr<Slot> BlockPool::alloc() {
     if (dry_) {
         auto s = std::make_shared<Slot>();
@@ -62,7 +66,10 @@ std::shared_ptr<Slot> BlockPool::alloc() {
     if (free_.empty()) {
         const size_t per = 1024;  // 16 MiB chunks
         void* c = nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
         hip_check(hipMalloc(&c, per * kBigCt * 8), "block pool hipMalloc");
+        g_pool_grow_ns += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
+        ++g_pool_grows;
         chunks_.push_back(c);
         for (size_t i = 0; i < per; ++i) free_.push_back((uint64_t*)c + (per - 1 - i) * kBigCt);
         total_ += per;
@@ -475,9 +482,12 @@ void Engine::flush() {
     if (pending_.empty()) return;
     const auto f0 = std::chrono::steady_clock::now();
     if (trace_) {
-        fprintf(stderr, "[host] %zu run() calls, %.3f ms inside run() since the last flush\n", run_calls_, run_ns_ * 1e-6);
+        fprintf(stderr, "[host] %zu run() calls, %.3f ms inside run() since the last flush (pool grown %zu x, %.3f ms)\n",
+                run_calls_, run_ns_ * 1e-6, g_pool_grows, g_pool_grow_ns * 1e-6);
         run_ns_ = 0.0;
         run_calls_ = 0;
+        g_pool_grows = 0;
+        g_pool_grow_ns = 0.0;
     }
     // Dead nodes: an output slot referenced by nothing but its own node (no later node reads it, no
     // block of the program holds it -- e.g. a carry-chain state whose every consumer folded to a
