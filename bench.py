@@ -702,6 +702,9 @@ def main():
         res["biguint256_mul_seconds"] = ops["biguint256_mul_compat"]["seconds"]
         res["sign_fhe_with_k0_seconds"] = ops["sign_fhe_with_k0_v0_compat"]["seconds"]
         res["div256_seconds"] = ops["div256_by_u32"]["seconds"]
+        # reference-equivalent op/s (the reference's operations per second on one GPU,
+        # independent of how many bootstraps this build spends on them)
+        res["reference_equivalent_ops_per_s"] = {k: 1.0 / v["seconds"] for k, v in ops.items() if v["seconds"] > 0}
         # published reference CPU numbers for the same operations (README.md:104-114;
         # c5.24xlarge, likely a debug build) -- context only, not the headline metric
         readme = {"fheuint32_add": 25.965747001, "fheuint32_mul": 76.051254698, "fheuint32_div5": 1121.134781795,
