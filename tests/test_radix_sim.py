@@ -239,3 +239,19 @@ def test_scalar_divrem_simulated(monkeypatch, residue, bits):
             assert sim_radix(DIVREM_CLEAR, bits, a, d) == (a // d, a % d), (residue, bits, hex(a), hex(d))
             # a's odd blocks trivial (public constants inside the dividend: the exact columns' excess)
             assert sim_radix(DIVREM_CLEAR_MIXED, bits, a, d) == (a // d, a % d), (residue, bits, hex(a), hex(d))
+
+
+@pytest.mark.parametrize("bits", [512, 4096])
+def test_radix_ops_max_width_simulated(bits):
+    """The widest radix (FHE_RADIX_MAX_BITS = 4096, 2048 blocks) and 512 bits: add / sub / lt / and /
+    min / encrypted shr and a public-divisor division (the residue split at these widths), every
+    bootstrap simulated; 512-bit products too."""
+    rng = random.Random(bits)
+    M = 1 << bits
+    ops = [ADD, SUB, LT, AND, MIN, SHR] + ([MUL, DIV_SCALAR] if bits == 512 else [])
+    for op in ops:
+        for a, b in [(M - 1, M - 1), (rng.getrandbits(bits), rng.getrandbits(bits)), (0, M - 1)]:
+            if op == SHR:
+                b = rng.randrange(bits)
+            got, _ = sim_radix(op, bits, a, b)
+            assert got == expect(op, bits, a, b), (op, bits)
