@@ -100,7 +100,7 @@ def test_max_width_ops(keys):
     """The widest radix the ABI accepts (FHE_RADIX_MAX_BITS = 4096 bits, 2048 blocks per operand):
     add, sub, lt, min and encrypted shr, exact tfhe semantics on random and all-ones operands (division
     at this width is a 1.6M-bootstrap triangle: its algorithm is checked at 512 bits in
-    test_radix_sim.py and at 256 bits here and in test_div_gpu.py)."""
+    test_radix_sim.py and at 256 bits in test_div_gpu.py)."""
     from fhe_sign import FheUint
     ck, _ = keys
     B = 4096
