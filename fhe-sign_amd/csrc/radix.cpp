@@ -2803,6 +2803,7 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
     const char* hv = getenv("FHE_DIV_R16");
     uint32_t lead = std::min<uint32_t>(hv ? (uint32_t)std::max(0, atoi(hv)) : 32u, 256u);
     lead = std::min(lead, n) & ~1u;
+    if (mode == 0) lead = 0;  // the leading steps hand over a lazy remainder only the merged steps absorb
     if (lead > 0) {
         const uint32_t L = lead;
         // exact low multiples m_c = c (d mod 4^L) on L + 2 blocks (< 15 4^L): their low L blocks are

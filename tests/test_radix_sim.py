@@ -255,3 +255,15 @@ def test_radix_ops_max_width_simulated(bits):
                 b = rng.randrange(bits)
             got, _ = sim_radix(op, bits, a, b)
             assert got == expect(op, bits, a, b), (op, bits)
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_encrypted_divrem_step_forms_simulated(monkeypatch, mode):
+    """The encrypted division's step forms (FHE_DIV_MERGED, same-process A/B switch): 2 (default)
+    selectors from scaled prefix tops, 1 selectors in their own level, 0 the subtractions' separate final
+    level (no leading radix-16 steps in that form) -- every form exact, the zero divisor included."""
+    monkeypatch.setenv("FHE_DIV_MERGED", mode)
+    rng = random.Random(40 + int(mode))
+    for bits in (8, 32, 64):
+        for a, b in [(rng.getrandbits(bits), rng.getrandbits(bits // 2) | 1), ((1 << bits) - 1, 3), (7, 0)]:
+            assert sim_radix(DIVREM, bits, a, b) == expect(DIVREM, bits, a, b), (mode, bits, a, b)
