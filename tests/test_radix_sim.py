@@ -6,6 +6,7 @@ integer semantics (tfhe's for the radix ops: wrapping add/sub/mul, shift amounts
 all ones, x % 0 = x) and against oracle/ref_semantics.py for the BigUintFHE limbs (src/biguint.rs:120-265,
 the compat mode's lost carries included).  The GPU tests run the same algorithms on ciphertexts."""
 import ctypes as C
+import os
 import random
 
 import pytest
@@ -267,3 +268,19 @@ def test_encrypted_divrem_step_forms_simulated(monkeypatch, mode):
     for bits in (8, 32, 64):
         for a, b in [(rng.getrandbits(bits), rng.getrandbits(bits // 2) | 1), ((1 << bits) - 1, 3), (7, 0)]:
             assert sim_radix(DIVREM, bits, a, b) == expect(DIVREM, bits, a, b), (mode, bits, a, b)
+
+
+@pytest.mark.parametrize("switch", ["FHE_KARA_ZLIM=6", "FHE_KARA_ZLIM=12", "FHE_CHAIN_HI_LIM=6", "FHE_COMPAT_WAVES=1",
+                                    "FHE_SCALAR_RECODE=0", "FHE_PREFIX=ks", "FHE_COMPRESS_PASS=0",
+                                    "FHE_COLUMNS_LIM=6", "FHE_SCHED=1", "FHE_ROUND=128", "FHE_NO_EAGER=1"])
+def test_environment_switches_simulated(switch):
+    """each A/B switch (several are read once per process, hence a subprocess) leaves
+    the results exact (tests/switch_check.py, quick form)."""
+    import subprocess
+    import sys as _sys
+    k, v = switch.split("=")
+    env = dict(os.environ, **{k: v})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([_sys.executable, os.path.join(root, "tests", "switch_check.py"), "quick"], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
