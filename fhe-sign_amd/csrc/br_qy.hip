@@ -115,7 +115,10 @@ FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
 // pattern's 16 key slices at a time -- then the MAC with no (e - 1) factor after it; the last forward
 // stage as t = zeta c, (a + t, a - t).  Two workgroups per CU.
 template <int G>
-__global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const uint64_t* __restrict__ ms, int ms_stride,
+#ifndef QY_WG_PER_CU
+#define QY_WG_PER_CU 3  // classic: three 4-wave workgroups per CU (164 VGPRs); variant builds only
+#endif
+__global__ __launch_bounds__(256, G == 1 ? QY_WG_PER_CU : 2) void k_blind_rotate_qy(const uint64_t* __restrict__ ms, int ms_stride,
                                                             const PbsDesc* __restrict__ desc,
                                                             const uint32_t* __restrict__ lut_idx,
                                                             const uint64_t* __restrict__ luts,
