@@ -132,11 +132,43 @@ FHE_DEV void xpose_dpp_banked(cplx& X, cplx& Y) {
     X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
     Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
 }
+#ifndef WIDE_SWZ
+#define WIDE_SWZ 0
+#endif
+// (variant builds, WIDE_SWZ=1) the same exchange through ds_swizzle (lane ^ SH within 32 lanes, on the LDS
+// crossbar, no memory) and one select per output dword: 2 VALU per dword pair instead of 3
+template <int K>
+FHE_DEV void xpose_swz(cplx& X, cplx& Y) {
+    constexpr int SH = 1 << K;
+    constexpr int PAT = 0x1F | (SH << 10);  // bit mode: and 0x1f, or 0, xor SH
+    const bool hi = ((threadIdx.x & 63) >> K) & 1;
+    uint32_t x[4], y[4];
+    u64_split(X.x, x[0], x[1]);
+    u64_split(X.y, x[2], x[3]);
+    u64_split(Y.x, y[0], y[1]);
+    u64_split(Y.y, y[2], y[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t tx = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x[d], PAT);
+        const uint32_t ty = (uint32_t)__builtin_amdgcn_ds_swizzle((int)y[d], PAT);
+        x[d] = hi ? ty : x[d];
+        y[d] = hi ? y[d] : tx;
+    }
+    X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
+    Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
+}
 FHE_DEV void xpose_dpp32(cplx (&x)[4]) {  // register bits (1, 0) <-> lane bits (3, 2)
+#if WIDE_SWZ
+    xpose_swz<3>(x[0], x[2]);
+    xpose_swz<3>(x[1], x[3]);
+    xpose_swz<2>(x[0], x[1]);
+    xpose_swz<2>(x[2], x[3]);
+#else
     xpose_dpp_banked<3>(x[0], x[2]);
     xpose_dpp_banked<3>(x[1], x[3]);
     xpose_dpp_banked<2>(x[0], x[1]);
     xpose_dpp_banked<2>(x[2], x[3]);
+#endif
 }
 
 // register bits (1, 0) <-> lane bits (KH, KL): pairs (x0,x2),(x1,x3) for bit 1; (x0,x1),(x2,x3) for bit 0
