@@ -305,3 +305,38 @@ def test_biguint_compat_chain_shapes_and_boundaries(keys):
         finally:
             del os.environ["FHE_COMPAT_WAVES"]
         assert got == want and waves == want, (la, lb)
+
+
+def test_random_op_chains(keys):
+    """Seeded random chains of radix ops on the GPU (ciphertext outputs feeding later ops, widths 8 to
+    128 bits, encrypted and clear operands), every intermediate decrypted against exact tfhe
+    semantics: wrapping + - *, & (encrypted and clear), encrypted >> <<, min / max / <, / and % by clear
+    and encrypted divisors (x / 0 = all ones, x % 0 = x)."""
+    from fhe_sign import FheUint
+    ck, _ = keys
+    rng = random.Random(0xC4A1)
+    for bits in (8, 16, 32, 64, 128):
+        M = (1 << bits) - 1
+        vals = [rng.getrandbits(bits) for _ in range(3)] + [0, M]
+        enc = [FheUint.try_encrypt(v, ck, bits=bits) for v in vals]
+        for step in range(10):
+            i, j = rng.randrange(len(vals)), rng.randrange(len(vals))
+            x, y, X, Y = vals[i], vals[j], enc[i], enc[j]
+            op = rng.choice(["add", "sub", "mul", "and", "andc", "shr", "shl", "min", "max", "lt", "divc", "remc",
+                             "div", "rem"] if bits <= 64 else ["add", "sub", "and", "shr", "min", "lt", "divc"])
+            c = rng.getrandbits(max(2, bits // 2)) | 1
+            s = y % bits
+            want, got = {
+                "add": (lambda: ((x + y) & M, X + Y)), "sub": (lambda: ((x - y) & M, X - Y)),
+                "mul": (lambda: ((x * y) & M, X * Y)), "and": (lambda: (x & y, X & Y)),
+                "andc": (lambda: (x & c, X & c)),
+                "shr": (lambda: (x >> s, X >> Y)), "shl": (lambda: ((x << s) & M, X << Y)),
+                "min": (lambda: (min(x, y), X.min(Y))), "max": (lambda: (max(x, y), X.max(Y))),
+                "lt": (lambda: (int(x < y), X.lt(Y))), "divc": (lambda: (x // c, X / c)),
+                "remc": (lambda: (x % c, X % c)),
+                "div": (lambda: (x // y if y else M, X // Y)), "rem": (lambda: (x % y if y else x, X % Y)),
+            }[op]()
+            assert got.decrypt(ck) == want, (bits, step, op, hex(x), hex(y))
+            if op not in ("lt",):  # feed the result into later steps
+                vals.append(want)
+                enc.append(got)
