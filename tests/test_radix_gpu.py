@@ -319,7 +319,7 @@ def test_random_op_chains(keys):
         M = (1 << bits) - 1
         vals = [rng.getrandbits(bits) for _ in range(3)] + [0, M]
         enc = [FheUint.try_encrypt(v, ck, bits=bits) for v in vals]
-        for step in range(10):
+        for step in range(25):
             i, j = rng.randrange(len(vals)), rng.randrange(len(vals))
             x, y, X, Y = vals[i], vals[j], enc[i], enc[j]
             op = rng.choice(["add", "sub", "mul", "and", "andc", "shr", "shl", "min", "max", "lt", "divc", "remc",
