@@ -35,5 +35,8 @@ std::vector<Blocks> biguint_mul_add_columns(Engine& e, const BigUint& a, const B
 // kCompat limbs by the carry-count chain (compat_chain.cpp), for 2 <= min(la, lb) <= 8
 bool compat_chain_applies(size_t la, size_t lb);
 BigUint compat_chain_mul(Engine& e, const BigUint& a, const BigUint& b);
+// the chain's g = 15 - [K mod 2^32 >= 2^32 - 16] * (K mod 16) of each prefix column set (16 columns:
+// column 0 one block, columns 1..15 two blocks, each <= 3), K = sum_m (sum of column m) 4^m
+Blocks compat_chain_g(Engine& e, const std::vector<const std::vector<Blocks>*>& prefixes);
 
 }  // namespace fhe

@@ -869,6 +869,34 @@ int fhe_host_sim_biguint_mul_add_columns(const uint32_t* a, size_t la, const uin
     });
 }
 
+int fhe_host_sim_chain_g(const uint8_t* vals, size_t nprefix, uint32_t* g, uint64_t* pbs, uint64_t* levels) {
+    if ((nprefix && (!vals || !g))) return FHE_ERR_INVALID;
+    return guarded([&] {
+        fhe_ctx c;
+        Engine e(&c, Engine::kSim);
+        std::vector<std::vector<Blocks>> P(nprefix, std::vector<Blocks>(kLimbBlocks));
+        for (size_t k = 0; k < nprefix; ++k) {
+            const uint8_t* v = vals + 31 * k;
+            for (int q = 0; q < 31; ++q) engine_check(v[q] <= 3, "sim chain g: a block value above 3");
+            P[k][0].push_back(e.sim_block(v[0], 3));
+            for (uint32_t m = 1; m < kLimbBlocks; ++m)
+                for (int q = 0; q < 2; ++q) P[k][m].push_back(e.sim_block(v[1 + 2 * (m - 1) + q], 3));
+        }
+        std::vector<const std::vector<Blocks>*> ptrs;
+        for (auto& x : P) ptrs.push_back(&x);
+        const Blocks out = compat_chain_g(e, ptrs);
+        e.flush();
+        for (size_t k = 0; k < nprefix; ++k) {
+            const int64_t h2 = e.sim_half2(out[k]);
+            engine_check(h2 % 2 == 0 && h2 >= 0 && h2 < 32, "sim chain g: g off its range");
+            g[k] = (uint32_t)(h2 / 2);
+        }
+        if (pbs) *pbs = e.pbs_count;
+        if (levels) *levels = e.levels;
+        return FHE_OK;
+    });
+}
+
 // One radix op (FHE_HOST_OP_*) on simulated operands a, b of `bits` (words LSB first, ceil(bits / 64)
 // each); out gets the result (MUL_FULL: 2 bits wide; LT / the comparison: 0 or 1 in out[0]); out2 the
 // remainder of DIVREM.

@@ -72,6 +72,75 @@ PbsItem sign_item(const std::vector<Term>& terms, int32_t half_cst) {
     return it;
 }
 
+}  // namespace
+
+// g = 15 - near * (K mod 16) of each prefix, from its 16 columns (column 0 one block <= 3, columns
+// 1..15 two blocks <= 3 each: v_m <= 6).  near = [K mod 2^32 >= 2^32 - 16] = [the resolved blocks
+// r_2..r_15 all equal 3], r_m = (v_m + c_m) mod 4, c_{m+1} = [v_m + c_m >= 4], c_1 = 0 (v_0 <= 3).
+// r_m = 3 means v_m + c_m in {3, 7}; a carry cannot start at a block that resolves to 3 (v_m = 7 is
+// out of range), so while every block below m resolves to 3, c_m = [v_{m-1} >= 4] (for m = 2 that
+// is the exact carry [v_1 >= 4]; above, v_{m-1} + c_{m-1} = 7 needs v_{m-1} = 6).  The local
+// indicators e_m = [(v_m + [v_{m-1} >= 4]) mod 4 == 3] therefore agree with [r_m == 3] at every block
+// up to the first one that is not 3, and near = AND of e_2..e_15 is exact.  (A bare [v_m == 3] for
+// m >= 3 is not: v_2 = 6 with c_2 = 1 resolves to 3 and carries into block 3.)  Five levels:
+// [v_m >= 4] and v_1 mod 4; the e_m; near; the two ANDs with K mod 16; g.
+Blocks compat_chain_g(Engine& e, const std::vector<const std::vector<Blocks>*>& P) {
+    static const auto GE4 = table([](uint32_t v) { return v >= 4 ? 1u : 0u; });
+    static const auto MOD4 = table([](uint32_t v) { return v & 3u; });
+    static const auto MOD4_EQ3 = table([](uint32_t v) { return (v & 3u) == 3 ? 1u : 0u; });
+    static const auto ID = table([](uint32_t v) { return v; });
+    static const auto AND_ = [] {
+        std::vector<uint32_t> t(16);
+        for (uint32_t v = 0; v < 16; ++v) t[v] = (v >> 2) ? (v & 3u) : 0u;
+        return t;
+    }();
+    auto terms = [](const Blocks& col) {
+        std::vector<Term> t;
+        for (const Block& b : col) t.push_back({b, 1});
+        return t;
+    };
+    const size_t np = P.size();
+    constexpr uint32_t kGe = kLimbBlocks - 2;  // [v_m >= 4], m = 1..14
+    std::vector<PbsItem> items;
+    for (const auto* cols : P) {
+        engine_check(cols->size() == kLimbBlocks && (*cols)[0].size() == 1, "compat chain: prefix column shape");
+        for (uint32_t m = 1; m + 1 < kLimbBlocks; ++m) items.push_back(item(terms((*cols)[m]), GE4));
+        items.push_back(item(terms((*cols)[1]), MOD4));
+    }
+    Blocks l1 = e.run(items);
+    items.clear();
+    for (size_t k = 0; k < np; ++k) {
+        const auto& cols = *P[k];
+        for (uint32_t m = 2; m < kLimbBlocks; ++m) {
+            std::vector<Term> t = terms(cols[m]);
+            t.push_back({l1[k * (kGe + 1) + (m - 2)], 1});  // [v_{m-1} >= 4]
+            items.push_back(item(t, MOD4_EQ3));
+        }
+    }
+    Blocks ind = e.run(items);
+    // near = all 14 indicators (raw: a 14-term input)
+    items.clear();
+    for (size_t k = 0; k < np; ++k) {
+        std::vector<Term> t;
+        for (uint32_t m = 2; m < kLimbBlocks; ++m) t.push_back({ind[k * (kLimbBlocks - 2) + (m - 2)], 1});
+        items.push_back(raw_item(t, 0, [](uint32_t v) { return v == kLimbBlocks - 2 ? 1u : 0u; }, 1));
+    }
+    Blocks near = e.run(items);
+    // g = 15 - near * (4 b1 + b0), b1 = v_1 mod 4, b0 = column 0's single block
+    items.clear();
+    for (size_t k = 0; k < np; ++k) {
+        const Block& b1 = l1[k * (kGe + 1) + kGe];
+        items.push_back(item({{near[k], 4}, {b1, 1}}, AND_));
+        items.push_back(item({{near[k], 4}, {(*P[k])[0][0], 1}}, AND_));
+    }
+    Blocks outs = e.run(items);
+    items.clear();
+    for (size_t k = 0; k < np; ++k) items.push_back(item({{outs[2 * k], -4}, {outs[2 * k + 1], -1}}, ID, 15));
+    return e.run(items);
+}
+
+namespace {
+
 enum Role { kBot, kMid, kTop };
 
 struct Touch {
@@ -266,82 +335,10 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
         Blocks c1 = radix_carry_outs(e, probs);
         for (size_t k = 0; k < c1.size(); ++k) PF[where[k].first][where[k].second].c1 = c1[k];
         phase("carry outs c1");
-        // near = [K mod 2^32 >= 2^32 - 16] = [resolved blocks 2..15 all 3]: blocks 3..15 are v_m (no
-        // carry reaches them without passing an all-3 block 2... so their indicator is [v_m == 3] given
-        // the carry into 3 is 0 -- which holds whenever block 2 resolves to 3 with no carry out: below)
-        static const auto EQ3 = table([](uint32_t v) { return v == 3 ? 1u : 0u; });
-        static const auto GE4 = table([](uint32_t v) { return v >= 4 ? 1u : 0u; });
-        static const auto MOD4 = table([](uint32_t v) { return v & 3u; });
-        static const auto MOD4_EQ3 = table([](uint32_t v) { return (v & 3u) == 3 ? 1u : 0u; });
-        struct Ev {
-            Blocks e;   // indicators, blocks 3..15, then block 2
-            Block c2, b1;
-        };
-        std::vector<std::vector<Ev>> ev(L);
-        std::vector<PbsItem> items;
-        std::vector<std::pair<size_t, size_t>> at;
-        for (size_t l = 0; l < L; ++l) {
-            ev[l].resize(PF[l].size());
-            for (size_t p = 0; p < PF[l].size(); ++p) {
-                const auto& cols = PF[l][p].cols;
-                for (uint32_t m = 3; m < kLimbBlocks; ++m) {
-                    std::vector<Term> t;
-                    for (const Block& b : cols[m]) t.push_back({b, 1});
-                    items.push_back(item(t, EQ3));
-                }
-                std::vector<Term> t1;
-                for (const Block& b : cols[1]) t1.push_back({b, 1});
-                items.push_back(item(t1, GE4));
-                items.push_back(item(t1, MOD4));
-                at.push_back({l, p});
-            }
-        }
-        Blocks outs = e.run(items);
-        size_t o = 0;
-        for (auto& w : at) {
-            Ev& x = ev[w.first][w.second];
-            x.e.assign(outs.begin() + o, outs.begin() + o + 13);
-            o += 13;
-            x.c2 = outs[o++];
-            x.b1 = outs[o++];
-        }
-        // block 2 resolved == 3: (v_2 + c_2) mod 4 == 3 (the carry into block 2 is [v_1 >= 4]: v_0 <= 3)
-        items.clear();
-        for (auto& w : at) {
-            std::vector<Term> t;
-            for (const Block& b : PF[w.first][w.second].cols[2]) t.push_back({b, 1});
-            t.push_back({ev[w.first][w.second].c2, 1});
-            items.push_back(item(t, MOD4_EQ3));
-        }
-        outs = e.run(items);
-        for (size_t k = 0; k < at.size(); ++k) ev[at[k].first][at[k].second].e.push_back(outs[k]);
-        // near = all 14 indicators (raw: a 14-term input)
-        items.clear();
-        for (auto& w : at) {
-            std::vector<Term> t;
-            for (const Block& b : ev[w.first][w.second].e) t.push_back({b, 1});
-            items.push_back(raw_item(t, 0, [](uint32_t v) { return v == 14 ? 1u : 0u; }, 1));
-        }
-        Blocks near = e.run(items);
-        // g = 15 - near * (4 b1 + b0), b0 = column 0's single block
-        static const auto AND_ = [] {
-            std::vector<uint32_t> t(16);
-            for (uint32_t v = 0; v < 16; ++v) t[v] = (v >> 2) ? (v & 3u) : 0u;
-            return t;
-        }();
-        items.clear();
-        for (size_t k = 0; k < at.size(); ++k) {
-            const Ev& x = ev[at[k].first][at[k].second];
-            const Block& b0 = PF[at[k].first][at[k].second].cols[0][0];
-            items.push_back(item({{near[k], 4}, {x.b1, 1}}, AND_));
-            items.push_back(item({{near[k], 4}, {b0, 1}}, AND_));
-        }
-        outs = e.run(items);
-        items.clear();
-        static const auto ID = table([](uint32_t v) { return v; });
-        for (size_t k = 0; k < at.size(); ++k) items.push_back(item({{outs[2 * k], -4}, {outs[2 * k + 1], -1}}, ID, 15));
-        Blocks g = e.run(items);
-        for (size_t k = 0; k < at.size(); ++k) PF[at[k].first][at[k].second].g = g[k];
+        std::vector<const std::vector<Blocks>*> cols;
+        for (auto& w : where) cols.push_back(&PF[w.first][w.second].cols);
+        Blocks g = compat_chain_g(e, cols);
+        for (size_t k = 0; k < where.size(); ++k) PF[where[k].first][where[k].second].g = g[k];
     }
 
     phase("g");

@@ -147,6 +147,7 @@ _SIGNATURES = [
     ("fhe_host_sim_biguint_mul_add_columns", C.c_int, [u32p, C.c_size_t, u32p, C.c_size_t, u32p, C.c_size_t, C.c_int,
                                                        C.POINTER(C.c_uint64), C.c_size_t, u32p, C.POINTER(C.c_uint64),
                                                        C.POINTER(C.c_uint64)]),
+    ("fhe_host_sim_chain_g", C.c_int, [u8p, C.c_size_t, u32p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("fhe_biguint_mul_add_columns", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                               C.POINTER(C.c_void_p)]),
     ("fhe_radix_scalar_mul_add_columns", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t,

@@ -354,6 +354,10 @@ int fhe_host_sim_radix(int op, uint32_t bits, const uint64_t* a, const uint64_t*
 int fhe_host_sim_biguint_mul_add_columns(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k,
                                          size_t lk, int mode, uint64_t* words, size_t nwords, uint32_t* bits,
                                          uint64_t* pbs, uint64_t* levels);
+/* The compat chain's g = 15 - [K mod 2^32 >= 2^32 - 16] (K mod 16) (csrc/compat_chain.cpp) on simulated
+ * prefix columns: vals holds nprefix records of 31 block values (each <= 3): column 0's block, then
+ * the two blocks of each column 1..15; K = sum_m (column m's sum) 4^m.  g: nprefix outputs. */
+int fhe_host_sim_chain_g(const uint8_t* vals, size_t nprefix, uint32_t* g, uint64_t* pbs, uint64_t* levels);
 
 /* ------------------------------------------------------------------- BigUintFHE */
 /* struct BigUintFHE { digits: Vec<FheUint32> } (src/biguint.rs:8-13), device-resident. */

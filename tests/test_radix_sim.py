@@ -284,3 +284,77 @@ def test_environment_switches_simulated(switch):
     r = subprocess.run([_sys.executable, os.path.join(root, "tests", "switch_check.py"), "quick"], env=env,
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+
+
+# ---- the compat chain's g (csrc/compat_chain.cpp compat_chain_g) on hand-built prefix columns
+def _chain_g_expect(v):
+    k = sum(x << (2 * m) for m, x in enumerate(v)) % M32
+    near = k >= M32 - 16
+    return 15 - (k % 16 if near else 0)
+
+
+def _chain_g_record(v):
+    """31 block values of a prefix whose column sums are v (v[0] <= 3, v[m] <= 6)"""
+    rec = [v[0]]
+    for x in v[1:]:
+        a = min(x, 3)
+        rec += [a, x - a]
+    return rec
+
+
+def _unresolve(v, rng, moves):
+    """move value between columns without changing K: +4 at column m, -1 at m + 1 (and back)"""
+    v = list(v)
+    for _ in range(moves):
+        m = rng.randrange(1, 15)
+        if rng.random() < 0.5:
+            if v[m] + 4 <= 6 and v[m + 1] >= 1:
+                v[m] += 4
+                v[m + 1] -= 1
+        elif v[m] >= 4 and v[m + 1] + 1 <= 6:
+            v[m] -= 4
+            v[m + 1] += 1
+    return v
+
+
+def test_chain_g_carry_aware_near():
+    """near = [K mod 2^32 >= 2^32 - 16] with carries moving through blocks that resolve to 3 (ADVICE r5:
+    v_1 >= 4, v_2 = 6, v_3.. = 3 resolves to blocks 3..15 = 0; v_3.. = 2 and runs of 6 resolve to 3)"""
+    rng = random.Random(0xC4A1)
+    cases = [
+        [3, 4, 6] + [3] * 13,            # carry through block 2 into 3: blocks 3..15 resolve to 0 -> near 0
+        [3, 4, 6] + [2] * 13,            # ... resolve to 3 -> near 1
+        [1, 4, 6, 6, 6, 2] + [3] * 10,   # a run of 6s carrying, ended by a 2
+        [2, 4, 6, 6, 6, 6] + [2] * 10,
+        [0, 0, 3] + [3] * 13,            # plain all-3
+        [3, 3, 3] + [3] * 13,
+        [3, 4, 2] + [3] * 13,            # carry absorbed at block 2
+        [3, 5, 6] + [6] * 13,            # carries out of the top: K mod 2^32 small
+        [3, 6, 6] + [6] * 12 + [2],
+    ]
+    # random representations of values at the boundary (K mod 2^32 in [2^32 - 40, 2^32 + 24), and the
+    # same above 2^32)
+    for base in (0, M32):
+        for t in range(-40, 24):
+            kk = (base + M32 + t) % (2 * M32)
+            canon = [(kk >> (2 * m)) & 3 for m in range(16)]
+            if kk >= M32:  # 2^32 sits above column 15: put it there as 4 extra units of column 15
+                canon[15] += 4
+            for _ in range(4):
+                v = _unresolve(canon, rng, rng.randrange(0, 40))
+                if sum(x << (2 * m) for m, x in enumerate(v)) == kk and max(v[1:]) <= 6 and v[0] <= 3:
+                    cases.append(v)
+    for _ in range(200):
+        cases.append([rng.randrange(4)] + [rng.choice([2, 3, 3, 3, 6, rng.randrange(7)]) for _ in range(15)])
+    vals = bytes(b for v in cases for b in _chain_g_record(v))
+    g = (C.c_uint32 * len(cases))()
+    pbs, lev = C.c_uint64(), C.c_uint64()
+    lib = _lib.load()
+    rc = lib.fhe_host_sim_chain_g((C.c_uint8 * len(vals)).from_buffer_copy(vals), len(cases), g, C.byref(pbs),
+                                  C.byref(lev))
+    assert rc == 0, lib.fhe_last_error()
+    assert lev.value == 5
+    assert pbs.value == 33 * len(cases)
+    bad = [(v, g[i], _chain_g_expect(v)) for i, v in enumerate(cases) if g[i] != _chain_g_expect(v)]
+    assert not bad, bad[:4]
+    assert sum(_chain_g_expect(v) != 15 for v in cases) >= 40  # the boundary cases do reach near = 1

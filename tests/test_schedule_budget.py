@@ -48,9 +48,10 @@ def test_radix_op_schedule_budget(key):
 
 def test_biguint_mul_schedule_budget():
     """256-bit BigUintFHE mul: compat (the reference's limbs, carry-count chain, Karatsuba limb products)
-    and fast (true product, Karatsuba twice): r5 57,564 PBS / 44 levels and 29,816 / 29."""
+    and fast (true product, Karatsuba twice): r5 57,564 PBS / 44 levels and 29,816 / 29; r6 59,020 / 44 for
+    compat (the chain's carry-aware near indicators, compat_chain_g: +13 bootstraps per prefix)."""
     pbs, levels = mul_stats(8, 8, 0, COMPAT)
-    assert levels <= 44 and pbs <= 58_500, (pbs, levels)
+    assert levels <= 44 and pbs <= 59_100, (pbs, levels)
     pbs, levels = mul_stats(8, 8, 0, FAST)
     assert levels <= 29 and pbs <= 30_300, (pbs, levels)
 
