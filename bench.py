@@ -39,6 +39,9 @@ FLOPS_PER_CMUX = 4 * 51200 + 4 * 6144 + 32768   # 4 FFT-1024 (5 N log N), 4 twis
 # per Fourier point 3 monomials minus 1 (3) and 3 patterns x 4 polynomials of complex multiply-add (96)
 FLOPS_PER_GROUP_MB = FLOPS_PER_CMUX + 1024 * (3 + 96)
 L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 ~34.5 TB/s aggregate
+CUS = 256                      # MI355X compute units
+DETAIL_DEFAULT = os.path.join(ROOT, "profiles", "r6", "bench_detail_latest.json")
+LINE_MAX_BYTES = 6144          # the driver keeps the last 8 KB of stdout; the line stays well inside it
 
 
 def parse(argv=None):
@@ -52,6 +55,8 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=32768, help="PBS per step per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--detail", default=DETAIL_DEFAULT,
+                    help="side file for the per-run arrays, the multi-bit op legs and the CPU per-op replay")
     ap.add_argument("--seed", type=int, default=0xF11E51)
     ap.add_argument("--no-ops", action="store_true", help="skip the 256-bit mul / sign wall-clock legs")
     ap.add_argument("--no-multibit", action="store_true", help="skip the multi-bit (grouping 2) measurement")
@@ -374,6 +379,11 @@ def ops_legs(ck, ctx, seed):
     s = Schnorr()
     ref = s.sign_with_k0(msg, k0, d)
     leg("sign_fhe_with_k0_v0_compat", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT), lambda r: r == ref)
+    # the reference's unchanged call site (src/schnorr.rs:271-276), operator by operator through the C
+    # ABI as INTEGRATION.md 2's impl Add / impl Mul binding dispatches it: BigUintFHE::new(e), ::new(k),
+    # k_fhe + (e_fhe * privkey_fhe) (normalized limbs), to_biguint, % n
+    leg("sign_fhe_with_k0_v0_callsite", lambda: s.sign_fhe_with_k0_callsite(msg, k0, d, dF, ck, COMPAT),
+        lambda r: r == ref)
     leg("sign_fhe_with_k0_v0_fast", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, FAST), lambda r: r == ref)
     leg("sign_fhe_with_k0_v0_public", lambda: s.sign_fhe_with_k0(msg, k0, d, dF, ck, PUBLIC), lambda r: r == ref)
     # Schnorr::sign_fhe (src/schnorr.rs:154-211): the full signer, encrypting the private key itself --
@@ -546,6 +556,9 @@ def pbs_leg(a, kind, dist, rank, world, device):
     ctx.enable_timing(False)
     ctx.sync()
 
+    # shader clock over the timed steps: every workgroup of the blind rotate adds its lifetime in
+    # s_memtime cycles and s_memrealtime 100 MHz ticks (fhe_ctx_enable_clock; two stamps per workgroup)
+    ctx.enable_clock(True)
     barrier(dist)
     ctx.sync()
     t0 = time.perf_counter()
@@ -555,6 +568,8 @@ def pbs_leg(a, kind, dist, rank, world, device):
     dt = time.perf_counter() - t0
     barrier(dist)
     dt = allmax(dist, dt)
+    cycles, ticks, wgs = ctx.read_clock()
+    ctx.enable_clock(False)
 
     # host-buffer boundary (fhe_pbs_batch: H2D + KS/BR + D2H), reported beside `value`, never as it
     t0 = time.perf_counter()
@@ -612,7 +627,130 @@ def pbs_leg(a, kind, dist, rank, world, device):
         "pcie_inclusive_pbs_per_s": pcie_rate * world,  # per-rank host-buffer rate x ranks
         "latency_level_ms": lat,
     }
+    if ticks and wgs:
+        ghz = cycles / ticks * 0.1  # s_memrealtime counts at 100 MHz
+        res["clock"] = {
+            "shader_ghz": ghz,
+            # clock-normalised cost (drift between boxes is clock): CU-cycles per bootstrap of the timed
+            # step (KS + BR + SE) and of the blind rotate alone (HIP-event kernel time)
+            "cu_cycles_per_pbs": res["ms_per_step"] * 1e-3 * ghz * 1e9 * CUS / B,
+            "br_cu_cycles_per_pbs": br_ms * 1e-3 * ghz * 1e9 * CUS / B,
+            "wg_cycles": cycles / wgs,  # one workgroup's (= one ciphertext's) lifetime, shader cycles
+            "workgroups": wgs,
+            "source": "s_memtime / s_memrealtime of every blind-rotate workgroup over the timed steps",
+        }
     return ck, ctx, res
+
+
+def _sig(x, digits=5):
+    """floats to `digits` significant digits, recursively (the line stays short)"""
+    if isinstance(x, float):
+        return float(f"{x:.{digits}g}")
+    if isinstance(x, dict):
+        return {k: _sig(v, digits) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_sig(v, digits) for v in x]
+    return x
+
+
+# published reference CPU numbers for the same operations (BASELINE.md 1, README.md:104-114; c5.24xlarge,
+# likely a debug build) -- context only, in the detail file
+README_S = {"fheuint32_add": 25.965747001, "fheuint32_mul": 76.051254698, "fheuint32_div5": 1121.134781795,
+            "fheuint32_shr_encrypted": 45.566019345, "fheuint32_cast_u8": 135.023e-6, "fheuint8_min": 25.71097148,
+            "fheuint8_and1": 6.418014644, "sign_fhe_v0_compat": 4269.0}
+# the classic (default-parameter) headline keys, emitted LAST so that the driver's stdout tail keeps them
+HEADLINE_KEYS = ("biguint256_mul_seconds", "biguint256_mul_fast_seconds", "sign_fhe_with_k0_seconds",
+                 "sign_fhe_with_k0_callsite_seconds", "div256_seconds", "div256_by_encrypted_seconds",
+                 "latency_level_ms")
+# multi-bit summary keys -> its op legs
+MB_KEYS = (("biguint256_mul_seconds", "biguint256_mul_compat"), ("biguint256_mul_fast_seconds", "biguint256_mul_fast"),
+           ("sign_fhe_with_k0_seconds", "sign_fhe_with_k0_v0_compat"),
+           ("sign_fhe_with_k0_callsite_seconds", "sign_fhe_with_k0_v0_callsite"),
+           ("div256_by_encrypted_seconds", "div256_by_encrypted"))
+
+
+def compose_line(a, world, cl, ops, mb, fan, cpu):
+    """(the one JSON line, the detail dict).  The line: the contract keys, compact roofline / clock /
+    multi-bit / fan-out / CPU-baseline summaries, every classic op's median seconds, then HEADLINE_KEYS
+    last (< LINE_MAX_BYTES; tests/test_bench_line.py).  The detail (side file, a.detail): the per-run
+    arrays, the reference-equivalent op/s, the README comparison, the multi-bit op legs and the CPU
+    per-op replay."""
+    B = a.batch
+    traffic, traffic_src = pmc_traffic(B)
+    r = cl["roofline"]
+    roof = {k: r[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "peak_measured", "frac_measured",
+                              "flops_per_pbs", "kernel_ms", "keyswitch_ms")}
+    roof["traffic"] = traffic
+    roof["traffic_source"] = traffic_src
+    roof["hbm"] = {k: r["hbm"][k] for k in ("achieved", "peak", "unit", "frac")}
+    roof["l2_to_cu"] = {k: r["l2"][k] for k in ("achieved", "peak", "unit", "frac")}
+    res = {
+        "metric": METRIC,
+        "value": cl["value"],
+        "unit": "PBS/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": cl["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"batched PBS (KS+MS+BR+SE) of {B} 2_2 radix blocks per GPU (configs[1]: 32768 = the "
+                        "block products of the 256-bit BigUintFHE mul, 128x128 pairs x lo/hi)",
+            "batch_pbs_per_gpu": B,
+            "params": cl["params"],
+            "parallelism": f"replicas x{world}",
+        },
+        "roofline": roof,
+    }
+    if "clock" in cl:
+        res["clock"] = {k: v for k, v in cl["clock"].items() if k != "source"}
+    res["pcie_inclusive_pbs_per_s"] = cl["pcie_inclusive_pbs_per_s"]
+    detail = {"metric": METRIC, "roofline": r, "clock": cl.get("clock"), "latency_level_ms": cl["latency_level_ms"]}
+    if mb is not None:
+        t_mb, _ = pmc_traffic(B, ("k_blind_rotate_qy<2>",))
+        m = {"value": mb["value"], "ms_per_step": mb["ms_per_step"], "kernel": mb["roofline"]["kernel"],
+             "frac": mb["roofline"]["frac"], "kernel_ms": mb["roofline"]["kernel_ms"], "traffic": t_mb}
+        if "clock" in mb:
+            m["shader_ghz"] = mb["clock"]["shader_ghz"]
+            m["cu_cycles_per_pbs"] = mb["clock"]["cu_cycles_per_pbs"]
+        m["latency_level_ms"] = mb["latency_level_ms"]
+        if "ops" in mb:
+            for key, leg in MB_KEYS:
+                if leg in mb["ops"]:
+                    m[key] = mb["ops"][leg]["seconds"]
+            detail["multibit_ops"] = mb["ops"]
+        res["multibit"] = m
+        detail["multibit"] = {k: v for k, v in mb.items() if k != "ops"}
+    if fan is not None:
+        res["fanout"] = fan
+    if cpu is not None:
+        c = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "simd", "nproc", "cgroup_cpu_quota") if k in cpu}
+        c["sample"] = (cpu["sample"].split(" (")[0] + " with the C restatement oracle/tfhe_oracle.c (not tfhe-rs), "
+                       f"{cpu['cores']} OpenMP threads")
+        if "ops" in cpu:
+            c["ops_s"] = {k: v["seconds"] for k, v in cpu["ops"].items()}
+        res["cpu_baseline"] = c
+        detail["cpu_baseline"] = cpu
+    res["detail"] = os.path.relpath(os.path.abspath(a.detail), ROOT) if a.detail else None
+    if ops is not None:
+        res["ops_s"] = {k: v["seconds"] for k, v in ops.items()}
+        detail["ops"] = ops
+        # SURVEY.md 8d: reference-equivalent op/s (the reference's operations per second on one GPU)
+        detail["reference_equivalent_ops_per_s"] = {k: 1.0 / v["seconds"] for k, v in ops.items() if v["seconds"] > 0}
+        detail["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
+                                             "speedup": v / ops[k]["seconds"]} for k, v in README_S.items() if k in ops}
+        res["ops_pbs_levels"] = {k: [ops[k]["pbs"], ops[k]["levels"]] for _, k in MB_KEYS if k in ops}
+        for key, leg in MB_KEYS[:4]:
+            res[key] = ops[leg]["seconds"]
+        res["div256_seconds"] = ops["div256_by_u32"]["seconds"]
+        res["div256_by_encrypted_seconds"] = ops["div256_by_encrypted"]["seconds"]
+    # blind rotate of one latency level, B = 1 / 256, before and after the timed throughput steps
+    res["latency_level_ms"] = cl["latency_level_ms"]
+    return _sig(res), detail
 
 
 def main():
@@ -669,64 +807,17 @@ def main():
             mb["sign_fhe_with_k0_seconds"] = mb_ops["sign_fhe_with_k0_v0_compat"]["seconds"]
         ctx_mb.close()
 
-    traffic, traffic_src = pmc_traffic(B)
-    roof = dict(cl["roofline"])
-    roof["traffic"] = traffic
-    roof["traffic_source"] = traffic_src
-    res = {
-        "metric": METRIC,
-        "value": cl["value"],
-        "unit": "PBS/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": cl["ms_per_step"],
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic",
-        "config": {
-            "workload": f"batched programmable bootstrap (KS+MS+BR+SE) of {B} 2_2 radix blocks per GPU "
-                        "(configs[1]: 32768 = the schoolbook block products of the 256-bit BigUintFHE mul, "
-                        "128 x 128 pairs x low/high; r5's Karatsuba split bootstraps 26.8k (compat) / 13.8k "
-                        "(fast) products, in levels of <= 16384)",
-            "batch_pbs_per_gpu": B,
-            "params": cl["params"],
-            "parallelism": f"replicas x{world}",
-        },
-        "roofline": roof,
-    }
-    if ops is not None:
-        res["ops"] = ops
-        res["biguint256_mul_seconds"] = ops["biguint256_mul_compat"]["seconds"]
-        res["sign_fhe_with_k0_seconds"] = ops["sign_fhe_with_k0_v0_compat"]["seconds"]
-        res["div256_seconds"] = ops["div256_by_u32"]["seconds"]
-        # reference-equivalent op/s (the reference's operations per second on one GPU,
-        # independent of how many bootstraps this build spends on them)
-        res["reference_equivalent_ops_per_s"] = {k: 1.0 / v["seconds"] for k, v in ops.items() if v["seconds"] > 0}
-        # published reference CPU numbers for the same operations (README.md:104-114;
-        # c5.24xlarge, likely a debug build) -- context only, not the headline metric
-        readme = {"fheuint32_add": 25.965747001, "fheuint32_mul": 76.051254698, "fheuint32_div5": 1121.134781795,
-                  "fheuint32_shr_encrypted": 45.566019345, "fheuint32_cast_u8": 135.023e-6,
-                  "fheuint8_min": 25.71097148, "fheuint8_and1": 6.418014644, "sign_fhe_v0_compat": 4269.0}
-        res["vs_reference_readme"] = {k: {"reference_s": v, "this_s": ops[k]["seconds"],
-                                          "speedup": v / ops[k]["seconds"]} for k, v in readme.items() if k in ops}
-    res["pcie_inclusive_pbs_per_s"] = cl["pcie_inclusive_pbs_per_s"]
-    # blind rotate of one latency level, B = 1 / 256, before and after the timed throughput steps
-    res["latency_level_ms"] = cl["latency_level_ms"]
-    if mb is not None:
-        # tfhe-rs' MultiBitPBS shape (grouping factor 2) on the same client key: same decrypted results
-        t_mb, src_mb = pmc_traffic(B, ("k_blind_rotate_qy<2>",))
-        mb["roofline"]["traffic"] = t_mb
-        mb["roofline"]["traffic_source"] = src_mb
-        res["multibit"] = mb
-    if fan is not None:
-        res["fanout"] = fan
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_seconds, op_levels)
+    cpu = cpu_baseline(a.seed, a.cpu_seconds, op_levels) if rank == 0 and world == 1 and not a.no_cpu_baseline else None
+    res, detail = compose_line(a, world, cl, ops, mb, fan, cpu)
+    if rank == 0 and a.detail:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(a.detail)), exist_ok=True)
+            with open(a.detail, "w") as f:
+                json.dump(detail, f, indent=1)
+        except OSError as e:
+            sys.stderr.write(f"bench: detail file not written: {e}\n")
     if rank == 0:
-        print(json.dumps(res), file=out, flush=True)
+        print(json.dumps(res, separators=(",", ":")), file=out, flush=True)
     if fan_hung:  # a collective of the abandoned legs may still hold the stream: no orderly teardown
         abandon("fan-out legs hung")
     ctx.close()

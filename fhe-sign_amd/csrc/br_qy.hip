@@ -125,7 +125,16 @@ __global__ __launch_bounds__(256, G == 1 ? QY_WG_PER_CU : 2) void k_blind_rotate
                                                             const cplx* __restrict__ bsk, const cplx* __restrict__ W,
                                                             const cplx* __restrict__ ps, const cplx* __restrict__ Z,
                                                             const cplx* __restrict__ mono, uint64_t* __restrict__ out,
-                                                            int n) {
+                                                            int n, unsigned long long* __restrict__ clk) {
+    // clock probe (clk != null, fhe_ctx_enable_clock): thread 0 of every workgroup adds its lifetime in
+    // shader cycles (s_memtime) and in 100 MHz ticks (s_memrealtime) to clk[0], clk[1] and counts
+    // itself in clk[2] -- the shader clock over the launch is their ratio x 100 MHz.  A buffer of its
+    // own, read by nothing in the kernel.
+    unsigned long long clk_t0 = 0, clk_r0 = 0;  // wave-uniform (scalar registers)
+    if (clk) {
+        clk_t0 = __builtin_amdgcn_s_memtime();
+        clk_r0 = __builtin_amdgcn_s_memrealtime();
+    }
     constexpr int XL_W = 2 * XR_SZ, XL_Z = XL_W + XTW_SZ, XL_T = XL_Z + XZ_SZ;
     __shared__ __attribute__((aligned(16))) cplx s_lds[XL_T + XT_SZ];
     cplx* s_w = s_lds + XL_W;
@@ -541,6 +550,14 @@ __global__ __launch_bounds__(256, G == 1 ? QY_WG_PER_CU : 2) void k_blind_rotate
     } else if (u == 0) {
         o[2048] = f64_to_torus(acc[0] * 0x1p41);
     }
+    if (clk) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            atomicAdd(&clk[0], t1 - clk_t0);
+            atomicAdd(&clk[1], r1 - clk_r0);
+            atomicAdd(&clk[2], 1ull);
+        }
+    }
 }
 
 // Fourier BSK: blind-rotate layout (R = 4v + q, lane L' <-> idx = 4 (L' + 64 v) + q) -> E layout
@@ -564,14 +581,14 @@ hipError_t launch_bsk_to_e(const cplx* bsk, int npoly, cplx* out, hipStream_t s)
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                   const uint64_t* luts, const cplx* bsk_e, const cplx* tw, const cplx* ps,
                                   const cplx* zfull, const cplx* mono, int grouping, uint64_t* out, int count, int n,
-                                  hipStream_t s) {
+                                  unsigned long long* clk, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     if (grouping == 2)
         hipLaunchKernelGGL(k_blind_rotate_qy<2>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
-                           bsk_e, tw, ps, zfull, mono, out, n);
+                           bsk_e, tw, ps, zfull, mono, out, n, clk);
     else
         hipLaunchKernelGGL(k_blind_rotate_qy<1>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
-                           bsk_e, tw, ps, zfull, mono, out, n);
+                           bsk_e, tw, ps, zfull, mono, out, n, clk);
     return hipGetLastError();
 }
 

@@ -281,7 +281,8 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
         return launch_blind_rotate_wide(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk, d_tw_wide, d_psi_wide,
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
     return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_e, d_tw_quad, d_psi_quad, d_zeta_full,
-                                  d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
+                                  d_mono, (int)p.grouping, out, (int)count, (int)p.n,
+                                  clock_probe ? d_clock : nullptr, stream);
 }
 
 // =========================================================================== C ABI (core)
@@ -560,7 +561,7 @@ void fhe_ctx_destroy(fhe_ctx* c) {
     c->engine = nullptr;
     c->release_comm();
     void* ptrs[] = {c->d_ksk, c->d_ksk_planes, c->d_ks_digits, c->d_ks_body, c->d_bsk, c->d_W, c->d_psi, c->d_tw_wide, c->d_psi_wide, c->d_tw_quad,
-                    c->d_psi_quad, c->d_zeta_wide, c->d_mono, c->d_bsk_e, c->d_zeta_full, c->d_flags, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather};
+                    c->d_psi_quad, c->d_zeta_wide, c->d_mono, c->d_bsk_e, c->d_zeta_full, c->d_flags, c->d_luts, c->d_ms, c->d_stage_in, c->d_stage_out, c->d_stage_lut, c->d_gather, c->d_clock};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto ev : c->ev)
@@ -762,6 +763,30 @@ int fhe_ctx_set_wide_threshold(fhe_ctx* c, int threshold) {
 int fhe_ctx_enable_timing(fhe_ctx* c, int enable) {
     if (!c) return FHE_ERR_INVALID;
     c->timing = enable != 0;
+    return FHE_OK;
+}
+
+int fhe_ctx_enable_clock(fhe_ctx* c, int enable) {
+    if (!c) return FHE_ERR_INVALID;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    if (enable && !c->d_clock) FHE_HIP_CHECK(hipMalloc(&c->d_clock, 4 * sizeof(unsigned long long)));
+    if (enable) FHE_HIP_CHECK(hipMemsetAsync(c->d_clock, 0, 4 * sizeof(unsigned long long), c->stream));
+    c->clock_probe = enable != 0;
+    return FHE_OK;
+}
+
+int fhe_ctx_read_clock(fhe_ctx* c, uint64_t* cycles, uint64_t* ticks, uint64_t* workgroups) {
+    if (!c) return FHE_ERR_INVALID;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    if (c->d_clock) {
+        FHE_HIP_CHECK(hipSetDevice(c->device));
+        FHE_HIP_CHECK(hipMemcpyAsync(h, c->d_clock, sizeof h, hipMemcpyDeviceToHost, c->stream));
+        const int rc = c->wait_stream("clock probe read");
+        if (rc) return rc;
+    }
+    if (cycles) *cycles = h[0];
+    if (ticks) *ticks = h[1];
+    if (workgroups) *workgroups = h[2];
     return FHE_OK;
 }
 

@@ -84,6 +84,9 @@ struct fhe_ctx {
     bool timing = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     float last_ks_ms = 0.f, last_br_ms = 0.f;
+    // clock probe of the throughput blind rotate (fhe_ctx_enable_clock / fhe_ctx_read_clock)
+    unsigned long long* d_clock = nullptr;  // {sum of workgroup shader cycles, of 100 MHz ticks, workgroups}
+    bool clock_probe = false;
     // radix-layer executor (created with the server key)
     fhe::Engine* engine = nullptr;
     // Multi-GPU fan-out (comm.cpp): every rank runs the same radix program on identical inputs;

@@ -432,6 +432,18 @@ int fhe_schnorr_sign_with_k0(const uint8_t* msg, size_t len, const uint8_t k0[32
     return FHE_OK;
 }
 
+// the plaintext steps 1-5 of sign_fhe_with_k0 (src/schnorr.rs:239-267): R = k0 G, k (k0 or n - k0 by
+// R's y parity), e = H(R || P || m); what the reference's call site then feeds to BigUintFHE::new
+int fhe_schnorr_sign_prologue(const uint8_t* msg, size_t len, const uint8_t k0[32], const uint8_t privkey[32],
+                              uint8_t k_out[32], uint8_t e_out[32], uint8_t rx_out[32]) {
+    if ((len && !msg) || !k0 || !privkey || !k_out || !e_out || !rx_out) return FHE_ERR_INVALID;
+    const SignCore c = core(msg, len, U256::from_be(k0), U256::from_be(privkey));
+    c.k.to_be(k_out);
+    c.e.to_be(e_out);
+    c.r.x.to_be(rx_out);
+    return FHE_OK;
+}
+
 int fhe_schnorr_sign(const uint8_t* msg, size_t len, const uint8_t aux[32], const uint8_t privkey[32], uint8_t sig[64]) {
     uint8_t k0[32];
     int rc = fhe_schnorr_compute_nonce(privkey, msg, len, aux, k0);

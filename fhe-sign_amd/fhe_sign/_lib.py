@@ -66,6 +66,8 @@ _SIGNATURES = [
     ("fhe_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     ("fhe_ctx_last_pbs_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("fhe_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("fhe_ctx_enable_clock", C.c_int, [C.c_void_p, C.c_int]),
+    ("fhe_ctx_read_clock", C.c_int, [C.c_void_p, u64p, u64p, u64p]),
     ("fhe_ctx_set_wide_threshold", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_ctx_set_br_kernel", C.c_int, [C.c_void_p, C.c_int]),
     ("fhe_ctx_set_ks_kernel", C.c_int, [C.c_void_p, C.c_int]),
@@ -170,6 +172,7 @@ _SIGNATURES = [
     ("fhe_schnorr_compute_nonce", C.c_int, [u8p, u8p, C.c_size_t, u8p, u8p]),
     ("fhe_schnorr_sign_with_k0", C.c_int, [u8p, C.c_size_t, u8p, u8p, u8p]),
     ("fhe_schnorr_sign", C.c_int, [u8p, C.c_size_t, u8p, u8p, u8p]),
+    ("fhe_schnorr_sign_prologue", C.c_int, [u8p, C.c_size_t, u8p, u8p, u8p, u8p, u8p]),
     ("fhe_schnorr_sign_fhe_with_k0", C.c_int, [C.c_void_p, C.c_void_p, u8p, C.c_size_t, u8p, u8p, C.c_void_p, C.c_int, u8p]),
     ("fhe_schnorr_sign_fhe_with_k0_batch", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p),
                                                     C.POINTER(C.c_size_t), C.c_char_p, C.c_char_p,

@@ -263,3 +263,13 @@ class Context:
         ks, br = C.c_float(), C.c_float()
         check(load().fhe_ctx_last_pbs_timing(self._h, C.byref(ks), C.byref(br)))
         return float(ks.value), float(br.value)
+
+    def enable_clock(self, on: bool = True) -> None:
+        """clock probe of the throughput blind rotate (fhe_ctx_enable_clock); enabling resets its sums"""
+        check(load().fhe_ctx_enable_clock(self._h, 1 if on else 0))
+
+    def read_clock(self):
+        """(shader cycles, 100 MHz ticks, workgroups) summed over the probed launches' workgroups"""
+        cy, tk, wg = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(load().fhe_ctx_read_clock(self._h, C.byref(cy), C.byref(tk), C.byref(wg)))
+        return int(cy.value), int(tk.value), int(wg.value)

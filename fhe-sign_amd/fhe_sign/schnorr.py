@@ -11,6 +11,9 @@ from ._lib import check, load
 from .integer import COMPAT, _ctx
 
 
+CURVE_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141  # secp256k1 n
+
+
 def _b32(x: int) -> bytes:
     return int(x).to_bytes(32, "big")
 
@@ -41,6 +44,27 @@ class Schnorr:
         sig = (C.c_uint8 * 64)()
         check(load().fhe_schnorr_sign_with_k0(_buf(message), len(message), _buf(_b32(k0)), _buf(_b32(privkey)), sig))
         return bytes(sig)
+
+    def sign_prologue(self, message: bytes, k0: int, privkey: int):
+        """(k, e, r_x) of sign_fhe_with_k0's plaintext steps 1-5 (src/schnorr.rs:239-267)"""
+        k, e, rx = (C.c_uint8 * 32)(), (C.c_uint8 * 32)(), (C.c_uint8 * 32)()
+        check(load().fhe_schnorr_sign_prologue(_buf(message), len(message), _buf(_b32(k0)), _buf(_b32(privkey)), k, e,
+                                               rx))
+        return int.from_bytes(bytes(k), "big"), int.from_bytes(bytes(e), "big"), bytes(rx)
+
+    def sign_fhe_with_k0_callsite(self, message: bytes, k0: int, privkey: int, privkey_fhe, client_key,
+                                  mode: int = COMPAT) -> bytes:
+        """sign_fhe_with_k0 exactly as the reference's call site runs it (src/schnorr.rs:271-276), each
+        operator through its own C entry point -- what INTEGRATION.md 2's impl Add / impl Mul binding
+        dispatches: e_fhe = BigUintFHE::new(e), k_fhe = BigUintFHE::new(k), k_fhe + (e_fhe * privkey_fhe),
+        to_biguint, % n.  Signature identical to sign_fhe_with_k0 (which fuses the block into one
+        column-form schedule)."""
+        from .integer import BigUintFHE
+        k, e, rx = self.sign_prologue(message, k0, privkey)
+        e_fhe = BigUintFHE.new(e, client_key)
+        k_fhe = BigUintFHE.new(k, client_key)
+        s_without_mod = k_fhe.add(e_fhe.mul(privkey_fhe, mode), mode).to_biguint(client_key)
+        return rx + _b32(s_without_mod % CURVE_ORDER)
 
     def sign_fhe_with_k0(self, message: bytes, k0: int, privkey: int, privkey_fhe, client_key, mode: int = COMPAT) -> bytes:
         sig = (C.c_uint8 * 64)()

@@ -148,6 +148,11 @@ int fhe_memcpy_d2h(fhe_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* Profiling: time of the last fhe_pbs_batch_device split by stage (ms, HIP events). */
 int fhe_ctx_last_pbs_timing(fhe_ctx* ctx, float* ks_ms, float* br_ms);
 int fhe_ctx_enable_timing(fhe_ctx* ctx, int enable);
+/* Clock probe of the throughput blind rotate: while enabled, thread 0 of every workgroup adds its
+ * lifetime in shader cycles (s_memtime) and in 100 MHz ticks (s_memrealtime); enabling resets the
+ * sums.  read_clock waits for the stream: shader clock = cycles / ticks x 100 MHz. */
+int fhe_ctx_enable_clock(fhe_ctx* ctx, int enable);
+int fhe_ctx_read_clock(fhe_ctx* ctx, uint64_t* cycles, uint64_t* ticks, uint64_t* workgroups);
 /* Batches of at most `threshold` bootstraps use the latency-optimised blind rotate (one
  * ciphertext per 512-thread workgroup); larger ones the throughput kernel.  Default 256. */
 int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
@@ -415,6 +420,11 @@ int fhe_schnorr_sign_with_k0(const uint8_t* msg, size_t msg_len, const uint8_t k
                              const uint8_t privkey[32], uint8_t sig[64]);
 int fhe_schnorr_sign(const uint8_t* msg, size_t msg_len, const uint8_t aux_rand[32],
                      const uint8_t privkey[32], uint8_t sig[64]);
+/* The plaintext steps 1-5 of sign_fhe_with_k0 (src/schnorr.rs:239-267): k (k0, or n - k0 when R = k0 G
+ * has odd y), the challenge e = H(R || P || m) and R's x -- so a caller can run the reference's own FHE
+ * block (src/schnorr.rs:271-276) through fhe_biguint_encrypt / _mul / _add / _decrypt unchanged. */
+int fhe_schnorr_sign_prologue(const uint8_t* msg, size_t msg_len, const uint8_t k0[32], const uint8_t privkey[32],
+                              uint8_t k_out[32], uint8_t e_out[32], uint8_t rx_out[32]);
 /* Schnorr::sign_fhe_with_k0 (src/schnorr.rs:235-290): privkey_fhe = BigUintFHE::new(privkey).
  * mode FHE_BIGUINT_COMPAT / FHE_BIGUINT_FAST run the reference's block (e and k encrypted, BigUintFHE
  * mul + add); FHE_SIGN_PUBLIC_OPERANDS keeps e and k in the clear (they are public values the

@@ -42,3 +42,18 @@ def test_vector0_expected_signature():
     assert sig.hex().upper() == ("E907831F80848D1069A5371B402410364BDF1C5F8307B0084C55F1CE2DCA8215"
                                  "25F66A4A85EA8B71E482A74F382D2CE5EBEEE8FDB2172F477DF4900D310536C0")
     assert Schnorr.verify(bytes(32), public_key_x(3), sig)
+
+
+@pytest.mark.parametrize("row", [r for r in ROWS if r["secret key"]], ids=lambda r: r["index"])
+def test_sign_prologue(row):
+    """fhe_schnorr_sign_prologue = sign_fhe_with_k0's plaintext steps 1-5 (src/schnorr.rs:239-267): the k,
+    e and r_x that the reference's call site feeds to BigUintFHE::new, vs the restatement"""
+    d = int(row["secret key"], 16) % R.N
+    msg, aux = bytes.fromhex(row["message"]), bytes.fromhex(row["aux_rand"])
+    k0 = compute_nonce(d, msg, aux)
+    k, e, rx = Schnorr().sign_prologue(msg, k0, d)
+    flow = R.sign_fhe_limb_flow(msg, k0, d)
+    assert (R.to_u32_digits(k), R.to_u32_digits(e)) == (flow["k"], flow["e"])
+    assert rx == R.b32(flow["r_x"]) == Schnorr().sign_with_k0(msg, k0, d)[:32]
+    # the call site's arithmetic on these values gives the signature
+    assert rx + R.b32((k + e * d) % R.N) == Schnorr().sign_with_k0(msg, k0, d)

@@ -93,3 +93,19 @@ def test_sign_fhe_with_k0_batch(env, mode):
     assert got == want
     for idx, sig in zip(("0", "1", "2", "15"), got):
         assert sig.hex().upper() == ROWS[idx]["signature"].upper()
+
+
+@pytest.mark.parametrize("idx", ["0", "1"])
+def test_sign_fhe_with_k0_reference_call_site(env, idx):
+    """the reference's unchanged call site (src/schnorr.rs:271-276: BigUintFHE::new(e), ::new(k),
+    k_fhe + (e_fhe * privkey_fhe), to_biguint, % n) bound operator by operator to the C ABI
+     == the fused signer == the CSV"""
+    row = ROWS[idx]
+    d = int(row["secret key"], 16)
+    msg, aux = bytes.fromhex(row["message"]), bytes.fromhex(row["aux_rand"])
+    k0 = compute_nonce(d, msg, aux)
+    s = Schnorr()
+    d_fhe = BigUintFHE.new(d, env)
+    sig = s.sign_fhe_with_k0_callsite(msg, k0, d, d_fhe, env, COMPAT)
+    assert sig.hex().upper() == row["signature"].upper()
+    assert sig == s.sign_fhe_with_k0(msg, k0, d, d_fhe, env, COMPAT)
