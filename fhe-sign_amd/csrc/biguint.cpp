@@ -1,8 +1,6 @@
 // biguint.cpp -- BigUintFHE add / mul over the GPU radix layer (src/biguint.rs:120-265).
 #include "biguint.h"
 
-#include <cstdlib>
-
 namespace fhe {
 
 static Radix concat(const std::vector<const Radix*>& limbs) {
@@ -119,10 +117,8 @@ static BigUint mul_impl(Engine& e, const BigUint& A, const BigUint& B, int mode,
     BigUint out;
     if (la == 0 || lb == 0) return out;
     // compat with 2..8 limbs on the shorter side: the carry-count chain (compat_chain.cpp), one
-    // lookup level per limb; FHE_COMPAT_WAVES=1 keeps the dependency-wave window adds below
-    const char* wv = getenv("FHE_COMPAT_WAVES");  // read per call: same-process A/Bs (tools/compat_ab.py)
-    const bool use_waves = wv && atoi(wv) != 0;
-    if (mode == kCompat && !use_waves && compat_chain_applies(la, lb)) return compat_chain_mul(e, A, B);
+    // lookup level per limb; above 8 the dependency-wave window adds below
+    if (mode == kCompat && compat_chain_applies(la, lb)) return compat_chain_mul(e, A, B);
     const size_t len = la + lb;
     if (mode == kFast || la == 1 || lb == 1) {
         std::vector<const Radix*> pa, pb;

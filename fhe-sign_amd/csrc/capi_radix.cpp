@@ -644,10 +644,31 @@ int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t
     });
 }
 
+// Test hooks of the radix size rules (radix.h Tuning): process-wide, *previous gets the old value
+int fhe_host_set_tuning(int key, int64_t value, int64_t* previous) {
+    Tuning& t = tuning();
+    int64_t old;
+    switch (key) {
+    case FHE_TUNE_KARA_MIN: old = t.kara_min; t.kara_min = (uint32_t)std::max<int64_t>(0, value); break;
+    case FHE_TUNE_KARA_COMPAT_MIN: old = t.kara_compat_min; t.kara_compat_min = (uint32_t)std::max<int64_t>(0, value); break;
+    case FHE_TUNE_KARA_FORCE: old = t.kara_force; t.kara_force = value != 0; break;
+    case FHE_TUNE_DIV_R16_LEAD: old = t.div_r16_lead; t.div_r16_lead = (uint32_t)std::max<int64_t>(0, value); break;
+    case FHE_TUNE_SCALAR_DIV_RESIDUE:
+        old = t.scalar_div_residue;
+        t.scalar_div_residue = value < 0 ? -1 : value != 0;
+        break;
+    default: return FHE_ERR_INVALID;
+    }
+    if (previous) *previous = old;
+    return FHE_OK;
+}
+
 // Dry run (no GPU): the same op on la x lb "encrypted" limbs (placeholder blocks) recorded and scheduled
 // by the engine without launching anything -- its bootstrap count, launch levels and level sizes.
 int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64_t* pbs, uint64_t* levels,
                                uint32_t* level_sizes, size_t cap) {
+    const bool columns = (mode & FHE_HOST_STATS_COLUMNS) != 0;  // the signer's column form instead
+    mode &= ~FHE_HOST_STATS_COLUMNS;
     if (!pbs || !levels || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
     return guarded([&] {
         fhe_ctx c;
@@ -662,12 +683,10 @@ int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64
             return r;
         };
         const BigUint A = make(la), B = make(lb);
-        // FHE_STATS_COLUMNS=1: the signer's column form (biguint_mul_add_columns) instead
-        const char* cv = getenv("FHE_STATS_COLUMNS");
         BigUint R;
         std::vector<Blocks> cols;
         uint32_t nb = 0;
-        if (cv && atoi(cv) != 0)
+        if (columns)
             cols = biguint_mul_add_columns(e, A, B, make(lk), mode, &nb);
         else
             R = lk ? biguint_mul_add(e, A, B, make(lk), mode) : biguint_mul(e, A, B, mode);
@@ -704,11 +723,7 @@ int fhe_host_radix_stats(int op, uint32_t bits, uint64_t* pbs, uint64_t* levels,
         case FHE_HOST_OP_SUB: keep = {radix_sub(e, A, B)}; break;
         case FHE_HOST_OP_SHR: keep = {radix_shr(e, A, B)}; break;
         case FHE_HOST_OP_LT: keep = {Radix{{radix_lt(e, A, B)}}}; break;
-        case FHE_HOST_OP_DIV_SCALAR: {  // FHE_STATS_DIVISOR (hex, <= 64 bits): another divisor's schedule
-            const char* dv = getenv("FHE_STATS_DIVISOR");
-            keep = {radix_scalar_div(e, A, BigConst{dv ? strtoull(dv, nullptr, 16) : 0xC0FFEE01u})};
-            break;
-        }
+        case FHE_HOST_OP_DIV_SCALAR: keep = {radix_scalar_div(e, A, BigConst{0xC0FFEE01u})}; break;
         default: engine_check(false, "unknown host op");
         }
         e.flush();

@@ -162,13 +162,14 @@ bool compat_chain_applies(size_t la, size_t lb) { return std::min(la, lb) >= 2 &
 
 BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
     const size_t la = A.digits.size(), lb = B.digits.size(), L = la + lb;
-    // FHE_CHAIN_PHASES=1 (diagnostic, dry runs): flush and print the bootstrap count after each phase
-    static const bool phases = getenv("FHE_CHAIN_PHASES") && atoi(getenv("FHE_CHAIN_PHASES"));
+    // FHE_DEBUG=chain (diagnostic, dry runs): flush and print the bootstrap count after each phase;
+    // chain-host: host time only, no flush
+    const bool phases = debug().chain || debug().chain_host;
     const auto t0 = std::chrono::steady_clock::now();
     auto phase = [&](const char* what) {
         if (!phases) return;
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        if (getenv("FHE_CHAIN_NOFLUSH")) {  // host time only
+        if (debug().chain_host) {  // host time only
             fprintf(stderr, "[compat chain] %-28s host %7.1f ms\n", what, ms);
             return;
         }
@@ -192,9 +193,8 @@ BigUint compat_chain_mul(Engine& e, const BigUint& A, const BigUint& B) {
     // into the limb's overflow O below)
     std::vector<int64_t> excess;
     // the high half (hi(P) columns) is read only by the prefix sums, whose inputs take a previous prefix
-    // column (<= 6) plus the product column: <= 9 there suffices (FHE_CHAIN_HI_LIM, read per call)
-    const char* hv = getenv("FHE_CHAIN_HI_LIM");
-    const uint32_t hi_lim = hv ? (uint32_t)std::max(6, std::min(9, atoi(hv))) : 9u;
+    // column (<= 6) plus the product column: <= 9 there suffices
+    constexpr uint32_t hi_lim = 9;
     std::vector<std::vector<Blocks>> PC = radix_mul_many_columns(e, ops, 2 * kLimbBlocks, &excess, kLimbBlocks, hi_lim);
     phase("product columns");
     {

@@ -28,6 +28,27 @@
 
 namespace fhe {
 
+Tuning& tuning() {
+    static Tuning t;
+    return t;
+}
+
+const Debug& debug() {
+    static const Debug d = [] {
+        Debug x;
+        const char* v = getenv("FHE_DEBUG");
+        const std::string s = v ? std::string(",") + v + "," : std::string();
+        auto has = [&](const char* k) { return s.find(std::string(",") + k + ",") != std::string::npos; };
+        x.levels = has("levels");
+        x.graph = has("graph");
+        x.chain = has("chain");
+        x.chain_host = has("chain-host");
+        x.residue = has("residue");
+        return x;
+    }();
+    return d;
+}
+
 void engine_check(bool ok, const char* what) {
     if (!ok) throw std::runtime_error(what);
 }
@@ -47,7 +68,7 @@ Slot::~Slot() {
 }
 
 BlockPool::~BlockPool() {
-    if (dry_) return;
+    if (dry_ || chunks_.empty()) return;  // a host-only engine never touches the HIP runtime
     (void)hipSetDevice(device_);
     for (void* c : chunks_) (void)hipFree(c);
 }
@@ -83,19 +104,11 @@ std::shared_ptr<Slot> BlockPool::alloc() {
 
 // ============================================================================ engine
 Engine::Engine(fhe_ctx* ctx, int host_mode) : ctx_(ctx), host_mode_(host_mode) {
-    pool_ = std::make_shared<BlockPool>(ctx->device, host_mode_ == kDry || host_mode_ == kSim);
+    pool_ = std::make_shared<BlockPool>(ctx->device, host_mode_ != kDevice);  // host modes allocate no device slots
     if (host_mode_ == kDevice)
         for (auto& ev : desc_ev_) hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
-    // FHE_TRACE_LEVELS=1: synchronize after every level and print its size and wall time (stderr);
-    // a diagnostic for schedule work, never set by the bench or the tests.
-    if (const char* t = getenv("FHE_TRACE_LEVELS")) trace_ = atoi(t) != 0;
-    if (const char* t = getenv("FHE_GRAPH_STATS")) gstats_ = atoi(t) != 0;
-    // FHE_SCHED=1: forward (deadline-driven) list scheduling instead of the default backward one
-    if (const char* t = getenv("FHE_SCHED")) sched_ = atoi(t);
-    // FHE_ROUND: level fill granule in bootstraps per GPU (schedule experiments; default 256)
-    if (const char* t = getenv("FHE_ROUND")) round_ = std::max(1, atoi(t));
-    // FHE_NO_EAGER=1: no eager launch of a first large independent batch (schedule experiments)
-    if (const char* t = getenv("FHE_NO_EAGER")) no_eager_ = atoi(t) != 0;
+    trace_ = debug().levels;
+    gstats_ = debug().graph;
 }
 
 int32_t Engine::depth_of(const Block& b) const {
@@ -389,7 +402,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     // products) is one throughput level under any schedule: launch it now, so the GPU works while
     // the host builds the rest of the graph (once per explicit flush: later independent batches,
     // e.g. the compressions that follow, stay in the graph to be spread over idle capacity)
-    if (eager_ok_ && !no_eager_ && pending_.size() >= kEagerBatch && pending_dependent_ == 0) {
+    if (eager_ok_ && pending_.size() >= kEagerBatch && pending_dependent_ == 0) {
         flush();
         eager_ok_ = false;
     }
@@ -564,8 +577,8 @@ void Engine::flush() {
     for (size_t k = 0; k < N; ++k) deps[k] = pending_[k].deps;
     if (gstats_) graph_stats(deps);
     // a fanned-out level's round is one latency-kernel round on every rank
-    const size_t round = (size_t)round_ * (size_t)std::max(1, ctx_->fanout_world());
-    std::vector<std::vector<int32_t>> lv = schedule_levels(deps, sched_, round);
+    const size_t round = (size_t)kRound * (size_t)std::max(1, ctx_->fanout_world());
+    std::vector<std::vector<int32_t>> lv = schedule_levels(deps, 0, round);
     if (host_mode_ == kDry || host_mode_ == kSim) {  // the schedule's statistics, nothing launched
         for (auto& l : lv) {
             pbs_count += l.size();
@@ -1015,10 +1028,6 @@ static bool col_live(const Blocks& c) {
 // satisfy that bound -- so a column that is fine on its own but gains a carry part is split in the
 // same round (lo <= 3 + incoming hi <= 3), instead of rippling one column per round afterwards.
 static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
-    static const bool pass_tail = [] {
-        const char* v = getenv("FHE_COMPRESS_PASS");
-        return !v || atoi(v) != 0;
-    }();
     for (;;) {
         std::vector<PbsItem> items;
         struct Dest {
@@ -1081,7 +1090,7 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
                     // round instead of paying a lo/hi pair now, when the column also forms a full group
                     // this round (so it still shrinks): 16 % fewer bootstraps on a 128 x 16-block product
                     // (the signer's e * d'), 2 % on 16 x 16 (tools/compress_sim.py), same round count
-                    if (pass_tail && made > 0 && g.size() <= 2 && deg <= 6 && noi <= (uint32_t)g.size()) {
+                    if (made > 0 && g.size() <= 2 && deg <= 6 && noi <= (uint32_t)g.size()) {
                         for (auto& t : g) next[pi][k].push_back(t.b);
                         continue;
                     }
@@ -1246,14 +1255,12 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
             base.push_back({k, k == 0, 0, {}, {}});
             latest.push_back((int)k);
         }
-        // generic plan over all positions (FHE_PREFIX=ks: the greedy Kogge-Stone form)
+        // generic plan over all positions
         std::vector<PNode> gen = base;
         std::vector<int> glat = latest;
         int glev = 0;
         // the first s levels Sklansky, the rest greedy: the fewest levels, then the fewest nodes, over
-        // every s (host planning only; FHE_PREFIX=ks: s = 0)
-        const char* pv = getenv("FHE_PREFIX");
-        const bool ks_only = pv && strcmp(pv, "ks") == 0;
+        // every s (host planning only)
         for (int s_sk = 0;; ++s_sk) {
             std::vector<PNode> nd = base;
             std::vector<int> lat = latest;
@@ -1272,7 +1279,7 @@ static std::vector<Blocks> carry_prefix(Engine& e, std::vector<Blocks> in, const
                 glat = std::move(lat);
                 glev = lev;
             }
-            if (ks_only || sk_done) break;
+            if (sk_done) break;
         }
         // top propagate/kill run [G, m)
         uint32_t G = m;
@@ -1660,11 +1667,6 @@ static std::vector<ColProblem> mul_problems(Engine& e, const std::vector<std::pa
 // a 257-bit multiplier (radix_scalar_div) compresses with ~12.6k bootstraps in 5 rounds instead of
 // ~24.2k in 6 (tools/compress_sim.py).  The public constant (the -3's and the products of a's
 // trivial blocks) is reduced mod 4^nblocks and added as trivial column entries.
-static bool recode_public() {  // FHE_SCALAR_RECODE=0: the plain digits (read per call: same-process A/Bs)
-    const char* v = getenv("FHE_SCALAR_RECODE");
-    return !v || atoi(v) != 0;
-}
-
 static void scalar_products(const Radix& a, const Radix& b, uint32_t nblocks,
                             std::vector<std::pair<uint32_t, Block>>& direct) {
     // recoded digits of b, one more than b has (the last carry)
@@ -1714,8 +1716,8 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
     return propagate_many(e, probs);
 }
 
-// Karatsuba split of a full product of two encrypted n-block operands (n >= FHE_KARA_MIN blocks,
-// default 24; FHE_KARATSUBA=0 turns it off; both read per call for same-process A/Bs):
+// Karatsuba split of a full product of two encrypted n-block operands (n >= tuning().kara_min blocks,
+// default 24):
 //   a b = z0 + X^2 z2 + X (m - z0 - z2),  X = 4^h, h = ceil(n / 2),
 //   z0 = a0 b0, z2 = a1 b1, m = (a0 + a1)(b0 + b1)  (the sums propagated to h + 1 clean blocks),
 // 3 products of ~h^2 block pairs instead of 4.  z0 and z2 (split again while large enough) are
@@ -1733,32 +1735,24 @@ std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const R
 // (shifted) in its own public constant.  Only for full products (N >= 2n and room for m at X:
 // nothing truncated) whose blocks are all encrypted, and not for the compat chain's limb products
 // (radix_mul_many_columns), whose consumer needs the columns to sum to the product itself.
-static bool karatsuba_on() {
-    const char* v = getenv("FHE_KARATSUBA");
-    return !v || atoi(v) != 0;
-}
-static uint32_t kara_min() {
-    const char* v = getenv("FHE_KARA_MIN");
-    return v && atoi(v) >= 6 ? (uint32_t)atoi(v) : 24u;
-}
+// (thresholds: tuning().kara_min / kara_compat_min; below 6 blocks a split never pays)
+static uint32_t kara_min() { return tuning().kara_min ? std::max<uint32_t>(6, tuning().kara_min) : UINT32_MAX; }
 // blocks below the top run of trivial zeros
 static uint32_t live_len(const Radix& r) {
     uint32_t n = r.nblocks();
     while (n > 0 && r.blocks[n - 1].trivial() && r.blocks[n - 1].value == 0) --n;
     return n;
 }
-// the compat chain's 16-block limb products (FHE_KARA_COMPAT_MIN, default 16; above 16: unsplit)
+// the compat chain's 16-block limb products (default 16; above 16: unsplit)
 static uint32_t kara_compat_min() {
-    const char* v = getenv("FHE_KARA_COMPAT_MIN");
-    return v && atoi(v) >= 6 ? (uint32_t)atoi(v) : 16u;
+    return tuning().kara_compat_min ? std::max<uint32_t>(6, tuning().kara_compat_min) : UINT32_MAX;
 }
 static bool kara_eligible(const Radix& a, const Radix& b, uint32_t nblocks, uint32_t min_n) {
     const uint32_t n = live_len(a), h = (n + 1) / 2;
-    if (!karatsuba_on() || n != live_len(b) || n < min_n || nblocks < 2 * n || nblocks < 3 * h + 3) return false;
-    // FHE_KARA_FORCE=1 (CPU tests): split publicly known operands too, so that the host-folding
+    if (n != live_len(b) || n < min_n || nblocks < 2 * n || nblocks < 3 * h + 3) return false;
+    // tuning().kara_force (CPU tests): split publicly known operands too, so that the host-folding
     // engine checks the split's algebra (offsets, complements, constants) on known values
-    const char* fv = getenv("FHE_KARA_FORCE");
-    const bool force = fv && atoi(fv) != 0;
+    const bool force = tuning().kara_force;
     for (const Radix* r : {&a, &b})
         for (uint32_t k = 0; k < n; ++k) {
             const Block& x = r->blocks[k];
@@ -1858,10 +1852,10 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
         }
         std::vector<ColProblem> mp = mul_problems_ops(e, mops, {}, true, &mq, min_n);
         std::vector<ColProblem*> ptrs;
-        // z0, z2 compressed to column sums <= 8 of <= 4 blocks (FHE_KARA_ZLIM, read once; 6 = the
-        // propagation's own target): the combination re-compresses them anyway, and the looser target
-        // saves a round's lo/hi pairs (dry: fast 256-bit mul 30.1k -> 29.8k, compat 58.3k -> 57.6k)
-        static const uint32_t zlim = getenv("FHE_KARA_ZLIM") ? (uint32_t)std::max(6, std::min(12, atoi(getenv("FHE_KARA_ZLIM")))) : 8u;
+        // z0, z2 compressed to column sums <= 8 of <= 4 blocks (6 = the propagation's own target): the
+        // combination re-compresses them anyway, and the looser target saves a round's lo/hi pairs
+        // (dry: fast 256-bit mul 30.1k -> 29.8k, compat 58.3k -> 57.6k)
+        constexpr uint32_t zlim = 8;
         for (auto& p : zp) {  // m enters uncompressed (once, no copy)
             p.lim = p.lim0 = zlim;
             p.max_cnt = zlim > 6 ? 4 : 3;
@@ -1925,7 +1919,7 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
     // compat 256-bit mul's 32768 block products); the rest follows as the engine's eager batch.
     size_t est = 0;
     for (size_t i : plain) est += (size_t)ops[i].a->nblocks() * ops[i].b->nblocks();
-    bool head = e.eager_head_ok() && !e.no_eager() && est >= 4 * Engine::kEagerHead;
+    bool head = e.eager_head_ok() && est >= 4 * Engine::kEagerHead;
     Blocks outs;
     std::vector<size_t> first(ops.size(), 0), last(ops.size(), 0);
     for (size_t i : plain) {
@@ -1939,7 +1933,7 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
             return true;
         };
         if (all_trivial(*pa) && !all_trivial(*pb)) std::swap(pa, pb);
-        if (all_trivial(*pb) && !all_trivial(*pa) && recode_public()) {
+        if (all_trivial(*pb) && !all_trivial(*pa)) {
             scalar_products(*pa, *pb, nblocks, direct[i]);
             last[i] = first[i];
             continue;
@@ -2014,9 +2008,8 @@ Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {
 std::vector<Blocks> radix_mul_add_columns(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks) {
     std::vector<ColProblem> probs = mul_problems(e, {{&a, &b}}, nblocks, {&c}, true);
     // compressed until each column fits one block (value <= 15): the columns are then the blocks of a
-    // radix ciphertext with carries, each the (lazy) sum of its column (FHE_COLUMNS_LIM: the bound)
-    const char* lv = getenv("FHE_COLUMNS_LIM");
-    const uint32_t lim = lv ? (uint32_t)std::max(6, std::min(15, atoi(lv))) : 15u;
+    // radix ciphertext with carries, each the (lazy) sum of its column
+    constexpr uint32_t lim = 15;
     probs[0].lim0 = probs[0].lim = lim;
     probs[0].max_cnt = 6;
     std::vector<ColProblem*> ptrs{&probs[0]};
@@ -2200,12 +2193,11 @@ static void choose_multiplier(const BigConst& d, uint32_t N, BigConst* m, uint32
 // / u32: 14.5k -> 8.3k bootstraps, 13 -> 17 levels (dry schedule); same-process A/B 114 -> 78 ms
 // (DESIGN.md 6).  The remainder needs S only (S propagated, divided by the multiplier method,
 // r = S - d floor(S / d)).
-// FHE_SCALAR_DIV_RESIDUE (read per call): 0 off, 1 wherever valid, unset = the size rule (dividends of
-// >= 64 blocks: the dry model and the A/B favour the split there for every divisor width it admits).
+// the size rule: dividends of >= 64 blocks (the dry model and the A/B favour the split there for every
+// divisor width it admits); tuning().scalar_div_residue 0 / 1: never / wherever valid (tests)
 static bool residue_split(uint32_t n, uint32_t dl) {
     if (dl + 12 > n) return false;  // S would not be narrow (the size rule implies it)
-    const char* v = getenv("FHE_SCALAR_DIV_RESIDUE");
-    if (v) return atoi(v) != 0;
+    if (tuning().scalar_div_residue >= 0) return tuning().scalar_div_residue != 0;
     return n >= 64;
 }
 
@@ -2343,8 +2335,8 @@ static Radix scalar_div_residue(Engine& e, const Radix& a, const BigConst& d, Ra
     PS.cols.assign(we, {});
     BigConst E;
     const_products(a, R, we, PS.cols, true, &E);
-    // FHE_RESIDUE_PHASES: bootstraps per phase (each phase flushed on its own: diagnostics only)
-    static const bool dbg = getenv("FHE_RESIDUE_PHASES") != nullptr;
+    // FHE_DEBUG=residue: bootstraps per phase (each phase flushed on its own: diagnostics only)
+    const bool dbg = debug().residue;
     uint64_t p0 = 0;
     auto phase = [&](const char* what) {
         if (!dbg) return;
@@ -2684,15 +2676,12 @@ static Radix barrel4(Engine& e, const Radix& a, const Radix& amount, bool right)
     return radix_clean(e, Radix{cur});
 }
 
-static bool barrel_4way() {  // FHE_BARREL4=0: the 2-way shifter (same-process A/Bs)
-    const char* v = getenv("FHE_BARREL4");
-    return !v || atoi(v) != 0;
-}
+// 4-way stages from two blocks up; a one-block (2-bit) operand has a one-bit amount: the 2-way stage
 Radix radix_shr(Engine& e, const Radix& a, const Radix& amount) {
-    return barrel_4way() && a.nblocks() >= 2 ? barrel4(e, a, amount, true) : barrel(e, a, amount, true);
+    return a.nblocks() >= 2 ? barrel4(e, a, amount, true) : barrel(e, a, amount, true);
 }
 Radix radix_shl(Engine& e, const Radix& a, const Radix& amount) {
-    return barrel_4way() && a.nblocks() >= 2 ? barrel4(e, a, amount, false) : barrel(e, a, amount, false);
+    return a.nblocks() >= 2 ? barrel4(e, a, amount, false) : barrel(e, a, amount, false);
 }
 
 Radix radix_bitand(Engine& e, const Radix& a, const Radix& b) {
@@ -2779,14 +2768,7 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
         span *= kMaxTerms;
         scaled = last;
     }
-    std::vector<std::vector<uint32_t>> sel(4);
-    for (uint32_t c = 0; c < 4; ++c) sel[c] = lut1([c](uint32_t v) { return (v >> 2) == c ? v & 3 : 0u; });
     static const auto sel_hi = lut1([](uint32_t v) { return v >= 8 ? (v - 8) & 3 : 0u; });
-    // FHE_DIV_MERGED (same-process A/Bs): 2 (default) selectors from the prefix's scaled top carries,
-    // 1 selectors in a level of their own, 0 the subtractions' separate final level
-    const char* mv = getenv("FHE_DIV_MERGED");
-    const int mode = mv ? atoi(mv) : 2;
-    const bool merged2 = mode >= 2, merged = mode == 1;
     Blocks r;  // remainder, w - 1 blocks before step i
     Radix q;
     q.blocks.resize(n);
@@ -2797,13 +2779,11 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
     // costs the 2 + P levels of ONE radix-4 step for two quotient blocks.  Its multiples need only
     // d mod 4^L (L = lead: exact products c (d mod 4^L) on L + 2 blocks, public-scalar: one propagation) and
     // the flags [c d < 4^w] = [d's blocks >= L zero] and [blocks w..L+1 of c (d mod 4^L) zero]: a setup
-    // that fills the early steps' idle rounds.  FHE_DIV_R16 = the number of leading dividend blocks so
-    // handled (read per call; rounded down to even, capped at the width; default 32, 0: radix-4
-    // throughout; same-process A/B in DESIGN.md 6).
-    const char* hv = getenv("FHE_DIV_R16");
-    uint32_t lead = std::min<uint32_t>(hv ? (uint32_t)std::max(0, atoi(hv)) : 32u, 256u);
+    // that fills the early steps' idle rounds.  tuning().div_r16_lead = the number of leading dividend
+    // blocks so handled (rounded down to even, capped at the width; default 32; same-process A/B in
+    // DESIGN.md 6).
+    uint32_t lead = std::min<uint32_t>(tuning().div_r16_lead, 256u);
     lead = std::min(lead, n) & ~1u;
-    if (mode == 0) lead = 0;  // the leading steps hand over a lazy remainder only the merged steps absorb
     if (lead > 0) {
         const uint32_t L = lead;
         // exact low multiples m_c = c (d mod 4^L) on L + 2 blocks (< 15 4^L): their low L blocks are
@@ -2936,10 +2916,10 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
             probs[c].cols[0].push_back(Block::make_trivial(1));
             probs[c].cols[w] = {P[c][w]};
         }
-        Blocks G;  // 8 ge_c (merged2)
-        std::vector<Blocks> cur = propagate_carries(e, probs, nullptr, nullptr, merged2 ? &G : nullptr);
+        Blocks G;  // 8 ge_c
+        std::vector<Blocks> cur = propagate_carries(e, probs, nullptr, nullptr, &G);
         Blocks h;
-        if (merged2) {
+        {
             // selectors without a level of their own: the prefix's top nodes also give G_c = 8 ge_c, and
             // as ge_1 >= ge_2 >= ge_3, 8 [q == c] = G_c - G_(c+1) (G_0 = 8, G_4 = 0) -- a difference the
             // degree bookkeeping cannot bound, so the selects are raw items (actual input in [0, 15],
@@ -2976,59 +2956,6 @@ std::pair<Radix, Radix> radix_divrem(Engine& e, const Radix& a, const Radix& d) 
             h = e.run(hs);
             q.blocks[i] = h.back();
             h.pop_back();
-        } else if (merged) {
-            // the quotient digit and the selectors S_c = 8 [q == c] (a PBS output of degree 8 and
-            // fresh noise), then r_k = sum_c f(S_c + x_ck) with x_0k = r4_k and x_ck the UNREDUCED
-            // column sum + carry in of subtraction c (<= 7): f(v) = (v - 8) mod 4 for v >= 8, else 0 --
-            // the subtractions' final level folded into the select (input <= 15, noise <= 7)
-            std::vector<PbsItem> items;
-            PbsItem qi;
-            qi.terms = {{cur[0][w], 1}, {cur[1][w], 1}, {cur[2][w], 1}};
-            qi.table = LUT_ID;
-            items.push_back(qi);
-            for (uint32_t c = 0; c < 4; ++c) {
-                qi.table = lut1([c](uint32_t v) { return v == c ? 8u : 0u; });
-                items.push_back(qi);
-            }
-            Blocks o = e.run(items);
-            q.blocks[i] = o[0];
-            std::vector<PbsItem> hs;
-            for (uint32_t k = 0; k < w; ++k)
-                for (uint32_t c = 0; c < 4; ++c) {
-                    PbsItem it;
-                    it.terms = {{o[1 + c], 1}};
-                    if (c == 0) {
-                        it.terms.push_back({r4[k], 1});
-                    } else {
-                        for (auto& b : probs[c - 1].cols[k]) it.terms.push_back({b, 1});
-                        if (k > 0) it.terms.push_back({cur[c - 1][k - 1], 1});
-                    }
-                    it.table = sel_hi;
-                    hs.push_back(it);
-                }
-            h = e.run(hs);
-        } else {
-            std::vector<PbsItem> items;
-            for (int c = 0; c < 3; ++c) final_items(probs[c], cur[c], w, items);
-            {
-                PbsItem qi;
-                qi.terms = {{cur[0][w], 1}, {cur[1][w], 1}, {cur[2][w], 1}};
-                qi.table = LUT_ID;
-                items.push_back(qi);
-            }
-            Blocks o = e.run(items);
-            const Block qb = o[3 * w];
-            q.blocks[i] = qb;
-            // r_k = sum over c of [q == c] cand_c[k], exactly one term nonzero
-            std::vector<PbsItem> hs;
-            for (uint32_t k = 0; k < w; ++k)
-                for (uint32_t c = 0; c < 4; ++c) {
-                    PbsItem it;
-                    it.terms = {{qb, 4}, {c == 0 ? r4[k] : o[(c - 1) * w + k], 1}};
-                    it.table = sel[c];
-                    hs.push_back(it);
-                }
-            h = e.run(hs);
         }
         // r_k = sum of the four half-selects (exactly one nonzero): kept lazy (noise 4), it enters
         // the next step's columns and half-selects directly -- no cleaning level per step

@@ -29,6 +29,26 @@ constexpr uint32_t kMsgBits = 2;
 constexpr uint32_t kMsgMod = 4;
 constexpr uint32_t kMaxNoise = 25;  // variance units (sigma <= 5 fresh sigmas, tfhe-rs 2_2 max noise level 5)
 
+// Size rules of the radix algorithms that tests move (fhe_host_set_tuning; process-wide, set before
+// an op runs).  The defaults are the product; a test lowers a threshold so that a small CPU or GPU
+// case takes the code path the product takes at 256 bits.  No environment variable is read on an op
+// path (engine diagnostics: FHE_DEBUG, read once per process, below).
+struct Tuning {
+    uint32_t kara_min = 24;         // Karatsuba for full products of >= this many live blocks (0: never)
+    uint32_t kara_compat_min = 16;  // ... for the compat chain's 16-block limb products (0: never)
+    bool kara_force = false;        // split publicly known operands too (the host-folding algebra checks)
+    uint32_t div_r16_lead = 32;     // encrypted division: leading dividend blocks taken in radix-16 steps
+    int scalar_div_residue = -1;    // public divisors: -1 size rule (dividends >= 64 blocks), 0 never, 1 where valid
+};
+Tuning& tuning();
+// Engine diagnostics on stderr, read once per process from FHE_DEBUG (comma-separated): levels (sync and
+// time every level), graph (graph statistics), chain (compat chain phases, flushed), chain-host (the
+// same, host time only), residue (the residue split's phases)
+struct Debug {
+    bool levels = false, graph = false, chain = false, chain_host = false, residue = false;
+};
+const Debug& debug();
+
 class BlockPool;
 
 struct Slot {
@@ -161,7 +181,6 @@ public:
     static constexpr size_t kEagerHead = 3072;  // 4 rounds of the throughput kernel (3 x 256 CUs)
     // nothing pending and no eager batch since the last flush (radix_mul_many's early head launch)
     bool eager_head_ok() const { return eager_ok_ && pending_.empty(); }
-    bool no_eager() const { return no_eager_; }
     // statistics
     uint64_t pbs_count = 0, levels = 0, fanout_levels = 0;
     uint64_t dead_nodes = 0;  // recorded bootstraps dropped at flush: nothing could read their outputs
@@ -185,9 +204,7 @@ private:
     bool gstats_ = false;
     std::vector<uint8_t> in_deg_;              // gstats_: max input value of each pending node
     std::vector<std::string> in_key_;          // gstats_: the node's input (terms + constant)
-    int sched_ = 0;
-    bool no_eager_ = false;
-    int round_ = 256;  // level fill granule (bootstraps per GPU)
+    static constexpr int kRound = 256;  // level fill granule: one latency round (a ciphertext per CU)
     double run_ns_ = 0.0;  // host time inside run() (trace)
     size_t run_calls_ = 0;
     static constexpr size_t kEagerBatch = 4096;

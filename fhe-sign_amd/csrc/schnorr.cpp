@@ -460,15 +460,12 @@ namespace {
 // levels hold every signature's bootstraps.
 struct SignJob {
     SignCore c;
-    fhe_biguint *e_fhe = nullptr, *k_fhe = nullptr, *s_fhe = nullptr;
-    fhe_radix* s_rad = nullptr;
-    fhe_columns* s_cols = nullptr;  // s_without_mod in column form (the default)
+    fhe_biguint *e_fhe = nullptr, *k_fhe = nullptr;
+    fhe_columns* s_cols = nullptr;  // s_without_mod in column form
     uint32_t bits = 0;
     ~SignJob() {
         fhe_biguint_destroy(e_fhe);
         fhe_biguint_destroy(k_fhe);
-        fhe_biguint_destroy(s_fhe);
-        fhe_radix_destroy(s_rad);
         fhe_columns_destroy(s_cols);
     }
 };
@@ -489,11 +486,8 @@ int sign_prepare(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t le
 // s_without_mod is only ever decrypted (to_biguint, then % n on the host: src/schnorr.rs:275-276), so
 // it stays in column form: the FHE block's work without its final carry propagation, the carries
 // resolved by the decryption as tfhe-rs's decrypt_radix does for blocks with carries (same value, same
-// signature; FHE_SIGN_COLUMNS=0: the normalized BigUintFHE / radix result, decrypted limb-wise)
-static bool sign_columns() {
-    const char* v = getenv("FHE_SIGN_COLUMNS");
-    return !v || atoi(v) != 0;
-}
+// signature).  The reference's operator-by-operator call site (normalized limbs: fhe_biguint_mul,
+// fhe_biguint_add, fhe_biguint_decrypt) is fhe_sign.Schnorr.sign_fhe_with_k0_callsite.
 
 int sign_begin(fhe_ctx* ctx, const fhe_biguint* privkey_fhe, int mode, SignJob* j) {
     const SignCore& c = j->c;
@@ -512,37 +506,24 @@ int sign_begin(fhe_ctx* ctx, const fhe_biguint* privkey_fhe, int mode, SignJob* 
             kw[i] = c.k.w[i];
         }
         rc = fhe_biguint_to_radix(privkey_fhe, j->bits, &d);
-        if (!rc)
-            rc = sign_columns() ? fhe_radix_scalar_mul_add_columns(ctx, d, ew, 4, kw, 4, &j->s_cols)
-                                : fhe_radix_scalar_mul_add_words(ctx, d, ew, 4, kw, 4, &j->s_rad);
+        if (!rc) rc = fhe_radix_scalar_mul_add_columns(ctx, d, ew, 4, kw, 4, &j->s_cols);
         fhe_radix_destroy(d);
         return rc;
     }
     // FHE block (src/schnorr.rs:272-276): k_fhe + e_fhe * privkey_fhe as one schedule (limbs
     // identical to the reference's mul, then add)
-    if (sign_columns()) return fhe_biguint_mul_add_columns(ctx, j->e_fhe, privkey_fhe, j->k_fhe, mode, &j->s_cols);
-    return fhe_biguint_mul_add(ctx, j->e_fhe, privkey_fhe, j->k_fhe, mode, &j->s_fhe);
+    return fhe_biguint_mul_add_columns(ctx, j->e_fhe, privkey_fhe, j->k_fhe, mode, &j->s_cols);
 }
 
 int sign_end(fhe_ctx* ctx, fhe_client_key* ck, SignJob* j, uint8_t sig[64]) {
     std::vector<uint32_t> limbs;
     int rc = FHE_OK;
-    if (j->s_cols) {
+    {
         uint32_t bits = 0;
         fhe_columns_bits(j->s_cols, &bits);
         std::vector<uint64_t> w((bits + 63) / 64);
         rc = fhe_columns_decrypt(ctx, ck, j->s_cols, w.data(), w.size());
         for (uint32_t i = 0; i < bits / 32 && !rc; ++i) limbs.push_back((uint32_t)(w[i / 2] >> (32 * (i % 2))));
-    } else if (j->s_rad) {
-        std::vector<uint64_t> w((j->bits + 63) / 64);
-        rc = fhe_radix_decrypt(ctx, ck, j->s_rad, w.data(), w.size());
-        for (uint32_t i = 0; i < j->bits / 32 + 1 && !rc; ++i) limbs.push_back((uint32_t)(w[i / 2] >> (32 * (i % 2))));
-    } else {
-        size_t n = 0;
-        fhe_biguint_len(j->s_fhe, &n);
-        limbs.resize(n + 1);
-        rc = fhe_biguint_decrypt(ctx, ck, j->s_fhe, limbs.data(), limbs.size(), &n);
-        limbs.resize(n);
     }
     if (rc) return rc;
     // s = s_without_mod % n (to_biguint then %, src/schnorr.rs:275-276)

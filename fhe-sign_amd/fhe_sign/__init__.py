@@ -9,7 +9,7 @@ All ciphertext arithmetic runs on the GPU through lib/libfhe_rocm.so; this packa
 """
 from ._lib import FheError, FheParams, load  # noqa: F401
 from .core import (ClientKey, Context, ServerKey, comm_unique_id, default_params, generate_keys,  # noqa: F401
-                   multi_bit_params)
+                   multi_bit_params, tuning)
 from .integer import (  # noqa: F401,E402
     COMPAT, FAST, PUBLIC, BigUintFHE, FheBool, FheUint, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, set_server_key,
     LEVEL_SPLIT, level_log, rank_pbs, stats, to_u32_digits)

@@ -1,6 +1,7 @@
 """Keys, device context and the raw PBS boundary (thin wrappers over the C ABI)."""
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 
 import numpy as np
@@ -273,3 +274,22 @@ class Context:
         cy, tk, wg = C.c_uint64(), C.c_uint64(), C.c_uint64()
         check(load().fhe_ctx_read_clock(self._h, C.byref(cy), C.byref(tk), C.byref(wg)))
         return int(cy.value), int(tk.value), int(wg.value)
+
+
+TUNE_KEYS = {"kara_min": 1, "kara_compat_min": 2, "kara_force": 3, "div_r16_lead": 4, "scalar_div_residue": 5}
+
+
+@contextlib.contextmanager
+def tuning(**values):
+    """Test hook (fhe_host_set_tuning): move the radix algorithms' size rules for the duration of a
+    with-block -- e.g. tuning(kara_min=6) -- and restore them after.  Process-wide."""
+    old = {}
+    try:
+        for k, v in values.items():
+            prev = C.c_int64()
+            check(load().fhe_host_set_tuning(TUNE_KEYS[k], int(v), C.byref(prev)))
+            old[k] = prev.value
+        yield
+    finally:
+        for k, v in old.items():
+            check(load().fhe_host_set_tuning(TUNE_KEYS[k], v, None))

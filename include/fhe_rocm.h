@@ -327,7 +327,18 @@ int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t
                          int mode, uint32_t* out, size_t cap, size_t* n);
 /* Dry run (no GPU): the bootstraps and launch levels the engine schedules for the la x lb BigUintFHE mul
  * (or k + a * b with lk > 0 limbs of k) on encrypted limbs -- recorded and scheduled, nothing launched.
+ * mode | FHE_HOST_STATS_COLUMNS: k + a * b in the signer's column form (fhe_biguint_mul_add_columns).
  * level_sizes (optional, up to cap entries): bootstraps per launched level. */
+#define FHE_HOST_STATS_COLUMNS 0x100
+/* Test hooks: the radix algorithms' size rules, process-wide (defaults = the product; a test moves a
+ * threshold so that a small case takes the path the product takes at 256 bits).  *previous (optional)
+ * gets the old value.  Not for production use; no environment variable changes them. */
+#define FHE_TUNE_KARA_MIN 1            /* Karatsuba from this many blocks (default 24; 0 never) */
+#define FHE_TUNE_KARA_COMPAT_MIN 2     /* ... for the compat chain's limb products (default 16; 0 never) */
+#define FHE_TUNE_KARA_FORCE 3          /* 1: split publicly known operands too (host-fold checks) */
+#define FHE_TUNE_DIV_R16_LEAD 4        /* encrypted division: leading radix-16 dividend blocks (default 32) */
+#define FHE_TUNE_SCALAR_DIV_RESIDUE 5  /* public divisors: -1 size rule (default), 0 never, 1 where valid */
+int fhe_host_set_tuning(int key, int64_t value, int64_t* previous);
 int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64_t* pbs, uint64_t* levels,
                                uint32_t* level_sizes, size_t cap);
 /* Dry run of one radix op on two encrypted `bits`-wide operands: bootstraps, launch levels and level

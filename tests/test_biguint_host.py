@@ -9,7 +9,7 @@ import random
 import pytest
 
 import ref_semantics as R
-from fhe_sign import _lib
+from fhe_sign import _lib, tuning
 
 M = 1 << 32
 COMPAT, FAST = 0, 1
@@ -83,13 +83,16 @@ def test_fast_and_mul_add():
         assert host_mul(a, b, COMPAT, k) == R.biguint_add(k, R.biguint_mul(a, b))
 
 
-@pytest.mark.parametrize("kmin", [4, 7, 16])
-def test_karatsuba_split_algebra(monkeypatch, kmin):
+@pytest.mark.parametrize("kmin", [6, 7, 16])
+def test_karatsuba_split_algebra(kmin):
     """The Karatsuba split of full products (csrc/radix.cpp mul_problems_ops) forced onto publicly known
-    operands (FHE_KARA_FORCE): its offsets, complements and public constants, recursion down to kmin
-    blocks, odd halves and trimmed zero tops, against the reference limb loop in both modes."""
-    monkeypatch.setenv("FHE_KARA_FORCE", "1")
-    monkeypatch.setenv("FHE_KARA_MIN", str(kmin))
+    operands (tuning kara_force): its offsets, complements and public constants, recursion down to kmin
+    blocks (at least 6), odd halves and trimmed zero tops, against the reference limb loop in both modes."""
+    with tuning(kara_force=1, kara_min=kmin):
+        _karatsuba_cases(kmin)
+
+
+def _karatsuba_cases(kmin):
     for a, b in _cases(77 + kmin, 12):
         assert R.from_limbs(host_mul(a, b, FAST)) == R.from_limbs(a) * R.from_limbs(b)
         assert host_mul(a, b, COMPAT) == R.biguint_mul(a, b)

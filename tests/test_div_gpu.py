@@ -12,7 +12,7 @@ import random
 import pytest
 
 from fhe_sign import (Context, FheUint8, FheUint32, FheUint64, FheUint128, FheUint256, generate_keys, multi_bit_params,
-                      set_server_key)
+                      set_server_key, tuning)
 
 pytestmark = pytest.mark.gpu
 M256 = (1 << 256) - 1
@@ -115,8 +115,7 @@ def test_public_scalar_recoding(keys):
     """Products with a public operand recode its base-4 digits to {-1, 0, 1, 2} (csrc/radix.cpp
     scalar_products: -x as 3 - x with a public -3): multipliers made of 3-digits (2^k - 1), mixed
     ones, wrap-around widths, multiply-add and the Granlund-Montgomery divisions that use them --
-    equal to exact integer arithmetic and to the plain-digit form (FHE_SCALAR_RECODE=0)."""
-    import os
+    equal to exact integer arithmetic."""
     ck, _ = keys
     rng = random.Random(0x5CA1)
     m = (1 << 128) - 1
@@ -126,25 +125,24 @@ def test_public_scalar_recoding(keys):
              rng.getrandbits(128)]
     for s in cases:
         got = [(A * s).decrypt(ck), A.scalar_mul_add(s, 0x3FFF).decrypt(ck)]
-        os.environ["FHE_SCALAR_RECODE"] = "0"
-        try:
-            plain = [(A * s).decrypt(ck), A.scalar_mul_add(s, 0x3FFF).decrypt(ck)]
-        finally:
-            del os.environ["FHE_SCALAR_RECODE"]
         want = [(a * s) & m, (a * s + 0x3FFF) & m]
-        assert got == want and plain == want, hex(s)
+        assert got == want, hex(s)
     for d in (3, 5, 0xFFFFFFFF, (1 << 64) - 59, (1 << 127) + 1):
         assert (A / d).decrypt(ck) == a // d, hex(d)
         assert (A % d).decrypt(ck) == a % d, hex(d)
 
 
 @pytest.mark.parametrize("method", ["residue", "multiplier"])
-def test_div256_residue_split(keys, method, monkeypatch):
+def test_div256_residue_split(keys, method):
+    with tuning(scalar_div_residue=1 if method == "residue" else 0):
+        _div256_cases(keys)
+
+
+def _div256_cases(keys):
     """Division by a public divisor, 256-bit dividends: the residue split a = d T + S (default for >= 64
-    blocks; csrc/radix.cpp scalar_div_residue) and the multiplier method (FHE_SCALAR_DIV_RESIDUE=0), on
+    blocks; csrc/radix.cpp scalar_div_residue) and the multiplier method (tuning scalar_div_residue 0), on
     divisors across the split's range (3 up to 116 bits, even ones, 2^k +- 1) and dividends at the
     edges: quotient and remainder equal floor division."""
-    monkeypatch.setenv("FHE_SCALAR_DIV_RESIDUE", "1" if method == "residue" else "0")
     ck, _ = keys
     rng = random.Random(0x5E51)
     for a, d in [(M256, 3), (rng.getrandbits(256), 10), (rng.getrandbits(256), (1 << 32) - 5),

@@ -282,10 +282,8 @@ def test_biguint_compat_uneven_limbs(keys):
 def test_biguint_compat_chain_shapes_and_boundaries(keys):
     """The compat carry-count chain (csrc/compat_chain.cpp) on the GPU: shapes 2x8, 8x2 and 8x12 (the
     shorter side decides), limbs at the 2^32 boundaries the chain's near / g logic keys on (2^32 - 1,
-    - 2, - 16, - 17, 15, 16), and the same products through the dependency-wave form
-    (FHE_COMPAT_WAVES=1, r4) -- equal decrypted limbs, equal to the reference's loop; 9x9 (outside the
-    chain's range) goes through the waves."""
-    import os
+    - 2, - 16, - 17, 15, 16) -- decrypted limbs equal to the reference's loop; 9x9 (outside the chain's
+    range) goes through the dependency-wave form."""
     ck, _ = keys
     M = 1 << 32
     special = [M - 1, M - 2, M - 16, M - 17, 15, 16, 0]
@@ -299,12 +297,7 @@ def test_biguint_compat_chain_shapes_and_boundaries(keys):
         want = R.biguint_mul(al, bl)
         a, b = _big(ck, al), _big(ck, bl)
         got = a.mul(b, COMPAT).decrypt_limbs(ck)
-        os.environ["FHE_COMPAT_WAVES"] = "1"
-        try:
-            waves = a.mul(b, COMPAT).decrypt_limbs(ck)
-        finally:
-            del os.environ["FHE_COMPAT_WAVES"]
-        assert got == want and waves == want, (la, lb)
+        assert got == want, (la, lb)
 
 
 def test_random_op_chains(keys):

@@ -12,7 +12,7 @@ import random
 import pytest
 
 import ref_semantics as R
-from fhe_sign import _lib
+from fhe_sign import _lib, tuning
 
 COMPAT, FAST = 0, 1
 DIVREM, MUL, ADD, SUB, SHR, LT, DIV_SCALAR, SHL, MUL_FULL, AND, MIN = range(11)
@@ -84,13 +84,11 @@ def test_radix_ops_simulated(bits, op):
         assert got == expect(op, bits, a, b), (op, bits, hex(a), hex(b))
 
 
-@pytest.mark.parametrize("bits", [2, 8, 16, 32, 64, 256])
+@pytest.mark.parametrize("bits", [2, 4, 8, 16, 32, 64, 256])
 @pytest.mark.parametrize("op", [SHR, SHL])
-@pytest.mark.parametrize("four_way", ["1", "0"])
-def test_encrypted_shifts_simulated(monkeypatch, bits, op, four_way):
-    """Both barrel shifters (4-way stages by amount blocks, default; FHE_BARREL4=0 the 2-way one):
-    every amount below the width at small widths, the amount's high bits ignored (mod the width)."""
-    monkeypatch.setenv("FHE_BARREL4", four_way)
+def test_encrypted_shifts_simulated(bits, op):
+    """The barrel shifters (4-way stages by amount blocks; one-block operands: the 2-way stage): every
+    amount below the width at small widths, the amount's high bits ignored (mod the width)."""
     rng = random.Random(bits + 7 * op)
     M = 1 << bits
     amounts = range(bits) if bits <= 16 else [0, 1, 2, 3, 4, 7, 8, 31, bits // 2 + 1, bits - 1]
@@ -123,16 +121,16 @@ def _limbs(rng, n):
     return [rng.choice(special) if rng.random() < 0.4 else rng.getrandbits(32) for _ in range(n)]
 
 
-@pytest.mark.parametrize("kara", [None, "6", "off"])
-def test_biguint_mul_simulated(monkeypatch, kara):
+@pytest.mark.parametrize("kara", [None, 6, 0])
+def test_biguint_mul_simulated(kara):
     """BigUintFHE mul / mul-add on simulated limbs: compat (the reference's limbs, lost carries included)
     and fast (the true product) across limb shapes, with the Karatsuba split at its default threshold,
-    recursing down to 6 blocks, and off."""
-    if kara == "off":
-        monkeypatch.setenv("FHE_KARATSUBA", "0")
-    elif kara:
-        monkeypatch.setenv("FHE_KARA_MIN", kara)
-    rng = random.Random(5 if kara is None else 6)
+    recursing down to 6 blocks, and off (tuning kara_min / kara_compat_min)."""
+    with tuning(**({} if kara is None else {"kara_min": kara, "kara_compat_min": kara})):
+        _biguint_mul_cases(random.Random(5 if kara is None else 6 + kara))
+
+
+def _biguint_mul_cases(rng):
     # 2 <= min <= 8: the carry-count chain; 1 or > 8 limbs (9 x 9, 12 x 4): the wave form; 0: zero
     shapes = [(1, 1), (2, 2), (1, 8), (8, 1), (3, 5), (8, 8), (9, 9), (12, 4), (0, 3), (3, 0)]
     for la, lb in shapes:
@@ -189,14 +187,18 @@ def test_scalar_mac_columns_simulated(bits):
         assert got == (a * m + m) % M, (bits, hex(a), hex(m))
 
 
-@pytest.mark.parametrize("lead", ["0", "2", "6", "16", "256"])
+@pytest.mark.parametrize("lead", [0, 2, 6, 16, 256])
 @pytest.mark.parametrize("bits", [16, 32, 64])
-def test_encrypted_divrem_radix16_lead_simulated(monkeypatch, lead, bits):
-    """The leading radix-16 steps (FHE_DIV_R16 = dividend blocks taken two at a time before the radix-4
+def test_encrypted_divrem_radix16_lead_simulated(lead, bits):
+    with tuning(div_r16_lead=lead):
+        _radix16_lead_cases(lead, bits)
+
+
+def _radix16_lead_cases(lead, bits):
+    """The leading radix-16 steps (tuning div_r16_lead = dividend blocks taken two at a time before the radix-4
     steps; 256 = every step) on divisors whose multiples c*d (c = 1..15) sit at the window boundaries
     4^w of the early steps, where the [c*d < 4^w] flags (d's high blocks zero and the exact low multiple
     c*(d mod 4^L) below 4^w) decide the candidate set."""
-    monkeypatch.setenv("FHE_DIV_R16", lead)
     rng = random.Random(bits * 31 + int(lead))
     M = 1 << bits
     divisors = {1, 2, 3, 5, 15, 16, 17, M - 1, M // 2, M // 2 + 1}
@@ -217,17 +219,18 @@ def test_encrypted_divrem_radix16_lead_simulated(monkeypatch, lead, bits):
 DIVREM_CLEAR, DIVREM_CLEAR_MIXED = 12, 13
 
 
-@pytest.mark.parametrize("residue", ["0", "1", None])
+@pytest.mark.parametrize("residue", [0, 1, -1])
 @pytest.mark.parametrize("bits", [32, 128, 256])
-def test_scalar_divrem_simulated(monkeypatch, residue, bits):
-    """a / d and a % d for PUBLIC divisors (radix_scalar_div / _rem): the multiplier method
-    (FHE_SCALAR_DIV_RESIDUE=0), the residue split a = d T + S wherever it is valid (1) and the size rule
-    (unset), on divisors from 3 up to beyond the residue split's range, odd and even, 2^k +- 1."""
-    if residue is None:
-        monkeypatch.delenv("FHE_SCALAR_DIV_RESIDUE", raising=False)
-    else:
-        monkeypatch.setenv("FHE_SCALAR_DIV_RESIDUE", residue)
-    rng = random.Random(bits * 7 + (int(residue) if residue else 5))
+def test_scalar_divrem_simulated(residue, bits):
+    """a / d and a % d for PUBLIC divisors (radix_scalar_div / _rem): the multiplier method (tuning
+    scalar_div_residue 0), the residue split a = d T + S wherever it is valid (1) and the size rule (-1,
+    the default), on divisors from 3 up to beyond the residue split's range, odd and even, 2^k +- 1."""
+    with tuning(scalar_div_residue=residue):
+        _scalar_divrem_cases(residue, bits)
+
+
+def _scalar_divrem_cases(residue, bits):
+    rng = random.Random(bits * 7 + (residue if residue >= 0 else 5))
     M = 1 << bits
     divisors = [3, 5, 6, 7, 10, 12, 255, 257, 1000003, 0xC0FFEE01, (1 << 31) - 1, (1 << 32) - 5,
                 rng.getrandbits(20) | 1, rng.getrandbits(40) | 3, rng.getrandbits(bits // 2) | 1]
@@ -256,34 +259,6 @@ def test_radix_ops_max_width_simulated(bits):
                 b = rng.randrange(bits)
             got, _ = sim_radix(op, bits, a, b)
             assert got == expect(op, bits, a, b), (op, bits)
-
-
-@pytest.mark.parametrize("mode", ["0", "1", "2"])
-def test_encrypted_divrem_step_forms_simulated(monkeypatch, mode):
-    """The encrypted division's step forms (FHE_DIV_MERGED, same-process A/B switch): 2 (default)
-    selectors from scaled prefix tops, 1 selectors in their own level, 0 the subtractions' separate final
-    level (no leading radix-16 steps in that form) -- every form exact, the zero divisor included."""
-    monkeypatch.setenv("FHE_DIV_MERGED", mode)
-    rng = random.Random(40 + int(mode))
-    for bits in (8, 32, 64):
-        for a, b in [(rng.getrandbits(bits), rng.getrandbits(bits // 2) | 1), ((1 << bits) - 1, 3), (7, 0)]:
-            assert sim_radix(DIVREM, bits, a, b) == expect(DIVREM, bits, a, b), (mode, bits, a, b)
-
-
-@pytest.mark.parametrize("switch", ["FHE_KARA_ZLIM=6", "FHE_KARA_ZLIM=12", "FHE_CHAIN_HI_LIM=6", "FHE_COMPAT_WAVES=1",
-                                    "FHE_SCALAR_RECODE=0", "FHE_PREFIX=ks", "FHE_COMPRESS_PASS=0",
-                                    "FHE_COLUMNS_LIM=6", "FHE_SCHED=1", "FHE_ROUND=128", "FHE_NO_EAGER=1"])
-def test_environment_switches_simulated(switch):
-    """each A/B switch (several are read once per process, hence a subprocess) leaves
-    the results exact (tests/switch_check.py, quick form)."""
-    import subprocess
-    import sys as _sys
-    k, v = switch.split("=")
-    env = dict(os.environ, **{k: v})
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([_sys.executable, os.path.join(root, "tests", "switch_check.py"), "quick"], env=env,
-                       capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
 
 
 # ---- the compat chain's g (csrc/compat_chain.cpp compat_chain_g) on hand-built prefix columns

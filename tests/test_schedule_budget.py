@@ -11,6 +11,7 @@ from fhe_sign import _lib
 
 DIVREM, MUL, ADD, SUB, SHR, LT, DIV_SCALAR = range(7)
 COMPAT, FAST = 0, 1
+STATS_COLUMNS = 0x100  # FHE_HOST_STATS_COLUMNS
 
 
 def radix_stats(op, bits):
@@ -56,12 +57,11 @@ def test_biguint_mul_schedule_budget():
     assert levels <= 29 and pbs <= 30_300, (pbs, levels)
 
 
-def test_signer_column_form_schedule_budget(monkeypatch):
+def test_signer_column_form_schedule_budget():
     """sign_fhe_with_k0's FHE block k + e*d' on vector 0's shape (8 x 1 limbs + 8): the column form the
-    signer uses (FHE_STATS_COLUMNS: biguint_mul_add_columns) against the normalized mul-add."""
-    monkeypatch.setenv("FHE_STATS_COLUMNS", "1")
-    pbs, levels = mul_stats(8, 1, 8, COMPAT)
+    signer uses (FHE_HOST_STATS_COLUMNS: biguint_mul_add_columns) against the normalized mul-add of the
+    reference's call site."""
+    pbs, levels = mul_stats(8, 1, 8, COMPAT | STATS_COLUMNS)
     assert levels <= 4 and pbs <= 6_500, (pbs, levels)
-    monkeypatch.setenv("FHE_STATS_COLUMNS", "0")
     pbs_n, levels_n = mul_stats(8, 1, 8, COMPAT)
     assert levels_n > levels and pbs_n > pbs

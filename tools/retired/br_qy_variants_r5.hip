@@ -75,12 +75,28 @@ constexpr int XZ_SZ = 140;
 // [20 + 34 c + 17 h + k] = W[16 m5] (c = 0), W[8 m5] (c = 1), m5 = (b4 .. b0) = 2 k + h (phase B)
 constexpr int XT_SZ = 20 + 68;
 
-// Key slices (G = 1): points 0, 1 of each (row, column) issued at the top of the step, in flight across
-// the whole forward transform; points 2, 3 after the B' -> E barrier (same-box A/Bs of the other
-// placements -- after the B' stores, before the B' stages, late slices before the barrier, the untwist
-// loads after the second barrier, two workgroups per CU -- in DESIGN.md 5 and 9; their sources:
-// tools/retired/br_qy_variants_r5.hip)
-constexpr int kKeyEarly = 2;
+// key-slice points issued before the B' -> E barrier (the rest after it); variant builds only
+#ifndef QY_KSPLIT
+#define QY_KSPLIT 2
+#endif
+// where those are issued: 1 (default) at the top of the step, in flight across the whole forward
+// transform (same-box A/B 213.6-214.1 vs 216.3-217.1 ms per 32768, profiles/r4/sched_ab_r4r.txt);
+// 0 after the B' stores, 2 before the B' stages (the scheduler's own choice for 0 under max-memory-clause)
+#ifndef QY_KEARLY
+#define QY_KEARLY 1
+#endif
+// untwist-factor loads: 0 (default) after the B' -> B round trip; 1 right after the second barrier,
+// 2 after the MAC (spills).  1 with the post-RA scheduler off won one same-box A/B (-0.8 %,
+// profiles/r4/sched_ab_r4s.txt) and lost another by 3 % with the L2 hit rate falling 0.976 -> 0.758
+// (10x the L2 fills, profiles/r4/l2ab_r4u/): workgroups drift apart in the key stream; not adopted
+#ifndef QY_PEARLY
+#define QY_PEARLY 0
+#endif
+// the late key slices ((q & 3) >= QY_KSPLIT): 0 (default) issued after the B' -> E barrier; 1 right
+// after the B' stores, before it (x is dead there, so the slices take its registers: same peak)
+#ifndef QY_KLATE_PRE
+#define QY_KLATE_PRE 0
+#endif
 
 template <int K, class F>
 FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
@@ -97,9 +113,12 @@ FHE_DEV void dit_pairs(cplx (&x)[8], F&& tw) {
 // phase E, the key bundle K_rc = sum_B (e_B - 1) G_B,rc (B = 1..3, patterns in order, from +0) -- it
 // depends on the key and the group's monomials only, so it is built during the forward transform, one
 // pattern's 16 key slices at a time -- then the MAC with no (e - 1) factor after it; the last forward
-// stage as t = zeta c, (a + t, a - t).  Three workgroups per CU classic (164-166 VGPRs), two multi-bit.
+// stage as t = zeta c, (a + t, a - t).  Two workgroups per CU.
 template <int G>
-__global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const uint64_t* __restrict__ ms, int ms_stride,
+#ifndef QY_WG_PER_CU
+#define QY_WG_PER_CU 3  // classic: three 4-wave workgroups per CU (164 VGPRs); variant builds only
+#endif
+__global__ __launch_bounds__(256, G == 1 ? QY_WG_PER_CU : 2) void k_blind_rotate_qy(const uint64_t* __restrict__ ms, int ms_stride,
                                                             const PbsDesc* __restrict__ desc,
                                                             const uint32_t* __restrict__ lut_idx,
                                                             const uint64_t* __restrict__ luts,
@@ -223,11 +242,13 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
         const bptr kb{bsk_rs, 16u * (uint32_t)L, (uint32_t)(i * 4096 + w * 256) * 16u};
 
         cplx Kb[16];  // G = 1: key slices [4 (row, column) + point k]; G = 2: the key bundle, same order
+#if QY_KEARLY == 1
         if constexpr (G == 1) {
 #pragma unroll
             for (int q = 0; q < 16; ++q)
-                if ((q & 3) < kKeyEarly) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+                if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
         }
+#endif
         // digits of acc itself (factored CMUX), with the previous update's deferred reduction
         cplx x[8];
         if (red_in) {
@@ -327,6 +348,13 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
         wave_sync();
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bBp + xq(idx_Bp(0, 0, r))];
+#if QY_KEARLY == 2
+        if constexpr (G == 1) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        }
+#endif
         if constexpr (G == 2) {
             __builtin_amdgcn_sched_barrier(0);
             fold(2, Ga);
@@ -349,12 +377,27 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
         }
 #pragma unroll
         for (int r = 0; r < 8; ++r) reg[bBp + xq(idx_Bp(0, 0, r))] = x[r];
+#if QY_KEARLY == 0
+        // key slices of this step in the E layout (row, column, point k): in flight across the barrier
+        if constexpr (G == 1) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if ((q & 3) < QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        }
+#endif
         if constexpr (G == 2) {
             __builtin_amdgcn_sched_barrier(0);
             fold(3, Gb);
             issue(4, Ga);
             __builtin_amdgcn_sched_barrier(0);
         }
+#if QY_KLATE_PRE
+        if constexpr (G == 1) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if ((q & 3) >= QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        }
+#endif
         cplx e0 = make_double2(1.0, 0.0);
         if constexpr (G == 1) {
             e0 = cmul(Ebn, Fn);  // exact when kk = 0 (Fn = E[0] = 1)
@@ -369,11 +412,13 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
         // ---- phase E: both polynomials at this wave's points, stages 8 (b1), 9 (b0)
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
+#if !QY_KLATE_PRE
         if constexpr (G == 1) {
 #pragma unroll
             for (int q = 0; q < 16; ++q)
-                if ((q & 3) >= kKeyEarly) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+                if ((q & 3) >= QY_KSPLIT) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
         }
+#endif
 #pragma unroll
         for (int r = 0; r < 8; ++r)
             if (!(r & 2)) dit_bfly(x[r], x[r + 2], z8);
@@ -405,6 +450,11 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
                 x[4 + k] = o1;
             }
         }
+#if QY_PEARLY == 2
+        cplx pst[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
+#endif
         // ---- inverse: b0 (twiddle 1), b1 (twiddles 1, -i) in E
 #pragma unroll
         for (int r = 0; r < 8; r += 2) {
@@ -421,6 +471,11 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
 #pragma unroll
         for (int r = 0; r < 8; ++r) s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))] = x[r];
         __syncthreads();
+#if QY_PEARLY == 1
+        cplx pst[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
+#endif
         // ---- B' (inverse): b2 (register bit 0), b3 (bit 1), b4 (bit 2)
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bBp + xq(idx_Bp(0, 0, r))];
@@ -442,9 +497,11 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
         wave_sync();
 #pragma unroll
         for (int r = 0; r < 8; ++r) x[r] = reg[bB + xq(idx_B(0, 0, r))];
+#if QY_PEARLY == 0
         cplx pst[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
+#endif
         {
             const cplx w5 = s_t[20 + 17 * h + kB], w6 = s_t[54 + 17 * h + kB];
             dit_pairs<1>(x, [&](int) { return conj_(w5); });

@@ -25,10 +25,38 @@
 #include "device_math.h"
 #include "kernels.h"
 
+// WMB7 (timing-only variant builds, tools/g3_probe.sh): the G = 2 kernel with a grouping-3 step's
+// shape -- n/3 steps, 7 key patterns per step loaded and bundled -- on the grouping-2 key's slices
+// (wrong numbers; for the grouping-3 cost estimate of DESIGN.md 3a only)
+#ifndef WIDE_KPRE
+#define WIDE_KPRE 0
+#endif
+#ifdef WMB7
+constexpr int WMBP = 7, WMBDIV = 3;
+#else
+constexpr int WMBP = 3, WMBDIV = 2;
+#endif
+
 namespace fhe {
 
-// Variant builds of this kernel (phase stamps, ds_swizzle transposes, early key loads, the grouping-3
-// timing shape) live in tools/retired/br_wide_variants_r5.hip; their A/Bs are in DESIGN.md 5.
+// WIDE_STAMPS (diagnostic variant build only, tools/wide_stamps.sh): lane 0 of every wave of the
+// first WS_CT ciphertexts records the shader clock (s_memtime) at the phase boundaries of WS_IT
+// CMUX iterations from WS_I0 on, written with vector stores to g_wide_stamps, read back by
+// fhe_debug_wide_stamps.  The product build compiles none of it.
+#ifdef WIDE_STAMPS
+constexpr int WS_CT = 2, WS_I0 = 200, WS_IT = 32, WS_N = 10;
+__device__ uint64_t g_wide_stamps[WS_CT][8][WS_IT][WS_N];
+#define WSTAMP(k)                                                                                      \
+    do {                                                                                               \
+        if (ct < WS_CT && i >= WS_I0 && i < WS_I0 + WS_IT && L == 0)                                   \
+            g_wide_stamps[ct][w][i - WS_I0][(k) + L] = __builtin_amdgcn_s_memtime();                   \
+    } while (0)
+#else
+#define WSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 namespace {
 // cross-wave regions: an XOR swizzle pos = A idx over GF(2) (bijective, no padding) under which the
 // D-side stores/loads and E-side loads/stores are all conflict-free by the gfx950 lane-group rules
@@ -104,11 +132,43 @@ FHE_DEV void xpose_dpp_banked(cplx& X, cplx& Y) {
     X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
     Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
 }
+#ifndef WIDE_SWZ
+#define WIDE_SWZ 0
+#endif
+// (variant builds, WIDE_SWZ=1) the same exchange through ds_swizzle (lane ^ SH within 32 lanes, on the LDS
+// crossbar, no memory) and one select per output dword: 2 VALU per dword pair instead of 3
+template <int K>
+FHE_DEV void xpose_swz(cplx& X, cplx& Y) {
+    constexpr int SH = 1 << K;
+    constexpr int PAT = 0x1F | (SH << 10);  // bit mode: and 0x1f, or 0, xor SH
+    const bool hi = ((threadIdx.x & 63) >> K) & 1;
+    uint32_t x[4], y[4];
+    u64_split(X.x, x[0], x[1]);
+    u64_split(X.y, x[2], x[3]);
+    u64_split(Y.x, y[0], y[1]);
+    u64_split(Y.y, y[2], y[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t tx = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x[d], PAT);
+        const uint32_t ty = (uint32_t)__builtin_amdgcn_ds_swizzle((int)y[d], PAT);
+        x[d] = hi ? ty : x[d];
+        y[d] = hi ? y[d] : tx;
+    }
+    X = make_double2(u64_join(x[0], x[1]), u64_join(x[2], x[3]));
+    Y = make_double2(u64_join(y[0], y[1]), u64_join(y[2], y[3]));
+}
 FHE_DEV void xpose_dpp32(cplx (&x)[4]) {  // register bits (1, 0) <-> lane bits (3, 2)
+#if WIDE_SWZ
+    xpose_swz<3>(x[0], x[2]);
+    xpose_swz<3>(x[1], x[3]);
+    xpose_swz<2>(x[0], x[1]);
+    xpose_swz<2>(x[2], x[3]);
+#else
     xpose_dpp_banked<3>(x[0], x[2]);
     xpose_dpp_banked<3>(x[1], x[3]);
     xpose_dpp_banked<2>(x[0], x[1]);
     xpose_dpp_banked<2>(x[2], x[3]);
+#endif
 }
 
 // register bits (1, 0) <-> lane bits (KH, KL): pairs (x0,x2),(x1,x3) for bit 1; (x0,x1),(x2,x3) for bit 0
@@ -273,11 +333,27 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#if WIDE_KPRE
+    // (variant build) classic: the key slices of step i + 1 are loaded right after step i's MAC
+    cplx Kown[4], Koth[4];
+    if constexpr (G == 1) {
+        const bptr kb{bsk_rs, kvo, 0u};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            Kown[2 * k] = kb[0 * 1024 + 128 * k];
+            Koth[2 * k] = kb[2 * 1024 + 128 * k];
+            Kown[2 * k + 1] = kb[3 * 1024 + 128 * k];
+            Koth[2 * k + 1] = kb[1 * 1024 + 128 * k];
+        }
+    }
+#endif
     uint32_t upd = 0;  // performed updates: acc + y is reduced mod 2^64 on every second one (oracle)
     bool red_in = false;  // the previous update's reduction, deferred to this step's digits (red_digit_s)
-    for (int i = 0; i < n / G; ++i) {
+    for (int i = 0; i < n / (G == 1 ? 1 : WMBDIV); ++i) {  // n / G in the product build
         cplx x[4];
+#if !WIDE_KPRE
         cplx Kown[4], Koth[4];  // BSK rows p (own digit) and 1 - p of column p (G = 2: the key bundle)
+#endif
         uint32_t mB[3] = {0u, 0u, 0u};
         const bool reduce = (upd++ & 1u) != 0;
         cplx e1;  // G = 1: zeta^((4 j0 + 1) a) of this lane's point r = 0
@@ -297,6 +373,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             }
         };
         if constexpr (G == 1) {
+            WSTAMP(0);
             digits();
         }
         if constexpr (G == 1) {
@@ -314,7 +391,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         // BSK slice for this iteration (issued early; consumed after the forward FFT): for MAC pair
         // k (points 2k, 2k + 1; this lane's point 2k + hL) the rows 0, 1 of column 0 (Kown[2k],
         // Koth[2k]) and of column 1 (Kown[2k + 1], Koth[2k + 1])
-        {
+        if (!WIDE_KPRE) {
             const bptr kb{bsk_rs, kvo, (uint32_t)i * 65536u};
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -325,6 +402,9 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             }
         }
         e1 = cmul(s_mono[(i & 1) * 256 + q * 64 + Lp], s_monf[(i & 1) * 64 + fselp]);
+        WSTAMP(1);
+        WSTAMP(2);
+        WSTAMP(3);
         } else {
         mB[0] = a_next;
         mB[1] = a_next1;
@@ -346,11 +426,20 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             const cplx* tf = s_monf + (i & 1) * 192 + fsel;
 #pragma unroll
             for (int r = 0; r < 4; ++r) Kown[r] = Koth[r] = make_double2(0.0, 0.0);
+#ifdef WMB7
 #pragma unroll
-            for (int B = 0; B < 3; ++B) {
+            for (int BB = 0; BB < WMBP; ++BB) {
+                const int B = BB % 3;
+                const size_t sl = (size_t)(7 * i + BB) % (3 * 417);
+                const gcptr b0 = as_global(bsk) + ((size_t)((sl * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;
+                const gcptr b1 = as_global(bsk) + ((size_t)((sl * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;
+#else
+#pragma unroll
+            for (int B = 0; B < WMBP; ++B) {
                 // (64-bit pointers here: the buffer form pushes one value of this kernel to scratch)
                 const gcptr b0 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + p) * 2 + p) * 16 + 4 * q) * 64 + L;
                 const gcptr b1 = as_global(bsk) + ((size_t)(((3 * i + B) * 2 + (p ^ 1)) * 2 + p) * 16 + 4 * q) * 64 + L;
+#endif
                 const cplx e = cmul(tb[B * 256], tf[B * 64]);  // zeta^((4 j0 + 1) m_B)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -380,7 +469,9 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         ct2(x, ZT[6], ZT[7]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) cross[xD ^ fx(4 * r)] = x[r];
+        if constexpr (G == 1) WSTAMP(4);
         __syncthreads();
+        if constexpr (G == 1) WSTAMP(5);
         // phase E reads both polynomials' regions, so the MAC needs no digit-swap exchange (one barrier
         // less per CMUX).  Classic: each point of each polynomial is transformed by one lane (below);
         // multi-bit: every wave transforms both polynomials at its points (the other polynomial's
@@ -411,6 +502,18 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
                 x[2 * k] = o0;
                 x[2 * k + 1] = o1;
             }
+#if WIDE_KPRE
+            if (i + 1 < n) {  // the next step's key slices, in flight across the inverse and the forward
+                const bptr kb{bsk_rs, kvo, (uint32_t)(i + 1) * 65536u};
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    Kown[2 * k] = kb[0 * 1024 + 128 * k];
+                    Koth[2 * k] = kb[2 * 1024 + 128 * k];
+                    Kown[2 * k + 1] = kb[3 * 1024 + 128 * k];
+                    Koth[2 * k + 1] = kb[1 * 1024 + 128 * k];
+                }
+            }
+#endif
         } else {
             cplx y[4];
             const cplx* cross_other = s_cross[p ^ 1];
@@ -425,6 +528,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
 #pragma unroll
             for (int r = 0; r < 4; ++r) x[r] = mac2(x[r], Kown[r], y[r], Koth[r]);
         }
+        if constexpr (G == 1) WSTAMP(6);
 
         // ---- inverse FFT: E -> D (cross-wave) -> C -> B -> A (wave-private)
         {
@@ -445,6 +549,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             for (int r = 0; r < 4; ++r) inv[xE ^ fx(r)] = x[r];
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the monomial DMA
+        if constexpr (G == 1) WSTAMP(7);
         __syncthreads();
         // Classic: the p = 1 wave of each SIMD is the critical one (it reaches barrier X ~1.6k ticks
         // after its p = 0 partner, which issues first by age and then waits: profiles/r5/wide_stamps_r5.txt),
@@ -453,6 +558,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
         // B = 1: 2.08 -> 2.00 ms, B = 256: 2.33 -> 2.26 ms (profiles/r5/wide_prio_ab*_r5.txt); the same
         // window in the multi-bit kernel (key bundle before the digits) costs 40 %, so it is classic only.
         if (G == 1 && p == 1) __builtin_amdgcn_s_setprio(2);
+        if constexpr (G == 1) WSTAMP(8);
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[r] = inv[xD ^ fx(4 * r)];
         dit2(x, T[9], T[10], T[11]);
@@ -476,6 +582,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
             acc[r + 4] = y.y;
         }
         if constexpr (G == 1) {
+            WSTAMP(9);
             red_in = reduce;  // applied at the next step's digits
         } else {
             // branch-free (a branch here made the compiler drain the next key-bundle loads: 1.63 ->
@@ -505,6 +612,16 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_wide(const uint64_t* __
     }
 }
 
+#ifdef WIDE_STAMPS
+}  // namespace fhe
+extern "C" int fhe_debug_wide_stamps(uint64_t* out, size_t n) {
+    const size_t words = sizeof(fhe::g_wide_stamps) / 8;
+    if (n < words) return (int)words;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fhe::g_wide_stamps), words * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+namespace fhe {
+#endif
 
 hipError_t launch_blind_rotate_wide(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                     const uint64_t* luts, const double2* bsk, const double2* tw, const double2* psiw,

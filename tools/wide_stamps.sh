@@ -3,4 +3,4 @@
 # CPU; run tools/wide_stamps.py on the GPU box.
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-EXTRA_FLAGS="-DWIDE_STAMPS ${EXTRA_FLAGS:-}" $ROOT/tools/build_variant.sh ${1:-wide_stamps} ${2:-$ROOT/fhe-sign_amd/csrc/br_wide.hip} "" br_wide
+EXTRA_FLAGS="-DWIDE_STAMPS ${EXTRA_FLAGS:-}" $ROOT/tools/build_variant.sh ${1:-wide_stamps} ${2:-$ROOT/tools/retired/br_wide_variants_r5.hip} "" br_wide
