@@ -464,12 +464,12 @@ int fhe_ctx_stats(fhe_ctx* c, uint64_t* pbs, uint64_t* levels) {
 
 // ----------------------------------------------------------------- operand distribution (comm.cpp)
 int fhe_ctx_broadcast_radix(fhe_ctx* c, fhe_radix** x, int root) {
-    const bool sends = c && (!c->comm || c->rank == root);
+    const bool sends = c && (!c->attached() || c->rank == root);
     if (!c || !x || (sends && !*x)) return FHE_ERR_INVALID;
     std::vector<Radix> g;
     if (sends) g.push_back((*x)->r);
     const int rc = bcast_radix_groups(c, root, &g);
-    if (rc || (c->comm && c->rank == root)) return rc;  // the root keeps its handle
+    if (rc || (c->attached() && c->rank == root)) return rc;  // the root keeps its handle
     if (g.size() != 1) {
         set_error("broadcast_radix: the root sent a BigUintFHE, not one radix integer");
         return FHE_ERR_INVALID;
@@ -480,12 +480,12 @@ int fhe_ctx_broadcast_radix(fhe_ctx* c, fhe_radix** x, int root) {
 }
 
 int fhe_ctx_broadcast_biguint(fhe_ctx* c, fhe_biguint** x, int root) {
-    const bool sends = c && (!c->comm || c->rank == root);
+    const bool sends = c && (!c->attached() || c->rank == root);
     if (!c || !x || (sends && !*x)) return FHE_ERR_INVALID;
     std::vector<Radix> g;
     if (sends) g = (*x)->v.digits;
     const int rc = bcast_radix_groups(c, root, &g);
-    if (rc || (c->comm && c->rank == root)) return rc;
+    if (rc || (c->attached() && c->rank == root)) return rc;
     for (const Radix& d : g)
         if (d.nblocks() != kLimbBlocks) {
             set_error("broadcast_biguint: the root sent digits that are not FheUint32");

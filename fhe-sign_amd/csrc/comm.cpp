@@ -85,8 +85,26 @@ int comm_wait_impl(fhe_ctx* c, const char* what) {
     }
 }
 
+// ---- the test transport (fhe_ctx_attach_test_transport): host-staged, synchronous
+int tx_check(int r, const char* what) {
+    if (r == 0) return FHE_OK;
+    set_error(std::string("test transport ") + what + " failed");
+    return FHE_ERR_HIP;
+}
+// a device buffer from root to every rank: stream sync, host copy, callback, copy back
+int tx_bcast_device(fhe_ctx* c, void* dev, size_t bytes, int root) {
+    if (bytes == 0) return FHE_OK;
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    std::vector<uint8_t> h(bytes);
+    FHE_HIP_CHECK(hipMemcpy(h.data(), dev, bytes, hipMemcpyDeviceToHost));
+    int rc = tx_check(c->tx.bcast(c->tx.user, h.data(), bytes, root), "broadcast");
+    if (!rc && c->rank != root) FHE_HIP_CHECK(hipMemcpy(dev, h.data(), bytes, hipMemcpyHostToDevice));
+    return rc;
+}
+
 // broadcast `bytes` of host memory from root (in place on every rank), through a device bounce buffer
 int bcast_host(fhe_ctx* c, void* host, size_t bytes, int root) {
+    if (c->has_tx) return tx_check(c->tx.bcast(c->tx.user, host, bytes, root), "broadcast");
     void* d = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d, bytes));
     ncclComm_t cm = (ncclComm_t)c->comm;
@@ -103,6 +121,12 @@ int bcast_host(fhe_ctx* c, void* host, size_t bytes, int root) {
 
 // every rank contributes ok (0/1); *all = min over the ranks (one-word all-reduce)
 int agree(fhe_ctx* c, int ok, int* all) {
+    if (c->has_tx) {
+        uint8_t b = ok ? 1 : 0;
+        const int rc = tx_check(c->tx.allreduce_min_u8(c->tx.user, &b, 1), "agreement");
+        *all = b;
+        return rc;
+    }
     int32_t v = ok ? 1 : 0;
     int32_t* d = nullptr;
     FHE_HIP_CHECK(hipMalloc(&d, sizeof v));
@@ -126,7 +150,7 @@ int fhe_ctx::wait_stream(const char* what) {
 }
 
 namespace {
-int comm_wait(fhe_ctx* c, const char* what) { return comm_wait_impl(c, what); }
+int comm_wait(fhe_ctx* c, const char* what) { return c->wait_stream(what); }
 }  // namespace
 
 int fhe_ctx::ensure_gather(size_t n) {
@@ -140,6 +164,15 @@ int fhe_ctx::ensure_gather(size_t n) {
 }
 
 int fhe_ctx::allgather(uint64_t* buf, size_t words) {
+    if (has_tx) {  // test transport: this rank's segment through the host, the others from the callback
+        FHE_HIP_CHECK(hipStreamSynchronize(stream));
+        std::vector<uint64_t> h((size_t)nranks * words);
+        FHE_HIP_CHECK(hipMemcpy(h.data() + (size_t)rank * words, buf + (size_t)rank * words, words * 8,
+                                hipMemcpyDeviceToHost));
+        const int rc = tx_check(tx.allgather(tx.user, h.data(), words * 8), "all-gather");
+        if (!rc) FHE_HIP_CHECK(hipMemcpy(buf, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+        return rc;
+    }
     if (!comm) return FHE_OK;  // emulated ranks already wrote every segment
     ncclComm_t cm = (ncclComm_t)comm;
     return nccl_settle(cm, ncclAllGather(buf + (size_t)rank * words, buf, words, ncclUint64, cm, stream),
@@ -211,7 +244,12 @@ extern "C" int fhe_progress_marks_probe(uint32_t levels, uint32_t* max_gap) {
 }
 
 int fhe_ctx::allreduce_min_u8(uint8_t* flags, size_t n) {
-    if (!comm || n == 0) return FHE_OK;
+    if (n == 0) return FHE_OK;
+    if (has_tx) {
+        FHE_HIP_CHECK(hipStreamSynchronize(stream));
+        return tx_check(tx.allreduce_min_u8(tx.user, flags, n), "all-reduce (dead nodes)");
+    }
+    if (!comm) return FHE_OK;
     if (n > flags_cap) {  // grown rarely (a hipFree synchronises the device)
         if (d_flags) FHE_HIP_CHECK(hipFree(d_flags));
         flags_cap = std::max<size_t>(n, 1 << 16);
@@ -235,6 +273,8 @@ void fhe_ctx::release_comm() {
         (void)ncclCommDestroy((ncclComm_t)comm);
         comm = nullptr;
     }
+    has_tx = false;
+    tx = fhe_test_transport{};
     prog_q.clear();
     prog_seq = 0;
     nranks = 1;
@@ -342,7 +382,7 @@ int bcast_radix_groups(fhe_ctx* c, int root, std::vector<Radix>* groups) {
         return FHE_ERR_NO_KEY;  // local misuse, caught before any collective (all ranks must pass it)
     }
     FHE_HIP_CHECK(hipSetDevice(c->device));
-    const bool loopback = !c->comm;  // emulated ranks (test hook): the root's data through the receiver path
+    const bool loopback = !c->attached();  // emulated ranks (test hook): the root's data through the receiver path
     const bool is_root = loopback || c->rank == root;
     BcastHdr h{};
     std::vector<uint32_t> meta;
@@ -412,12 +452,17 @@ int bcast_radix_groups(fhe_ctx* c, int root, std::vector<Radix>* groups) {
         release();
         return rc;
     }
-    ncclComm_t comm = (ncclComm_t)c->comm;
-    rc = nccl_settle(comm, ncclBroadcast(d_meta, d_meta, meta_words, ncclUint32, root, comm, c->stream),
-                     "ncclBroadcast", c->comm_timeout_ms, false);
-    if (!rc && data_words)
-        rc = nccl_settle(comm, ncclBroadcast(d_data, d_data, data_words, ncclUint64, root, comm, c->stream),
+    if (c->has_tx) {
+        rc = tx_bcast_device(c, d_meta, meta_words * 4, root);
+        if (!rc) rc = tx_bcast_device(c, d_data, data_words * 8, root);
+    } else {
+        ncclComm_t comm = (ncclComm_t)c->comm;
+        rc = nccl_settle(comm, ncclBroadcast(d_meta, d_meta, meta_words, ncclUint32, root, comm, c->stream),
                          "ncclBroadcast", c->comm_timeout_ms, false);
+        if (!rc && data_words)
+            rc = nccl_settle(comm, ncclBroadcast(d_data, d_data, data_words, ncclUint64, root, comm, c->stream),
+                             "ncclBroadcast", c->comm_timeout_ms, false);
+    }
     if (!rc && !is_root) {
         meta.resize(meta_words);
         rc = hipMemcpyAsync(meta.data(), d_meta, meta_words * 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess
@@ -475,6 +520,19 @@ int fhe_ctx_attach_comm(fhe_ctx* c, const uint8_t id[FHE_COMM_ID_BYTES], int nra
     return fhe_ctx_attach_comm_timeout(c, id, nranks, rank, FHE_COMM_DEFAULT_TIMEOUT_MS);
 }
 
+int fhe_ctx_attach_test_transport(fhe_ctx* c, const fhe_test_transport* tx, int nranks, int rank) {
+    if (!c || !tx || !tx->bcast || !tx->allgather || !tx->allreduce_min_u8 || nranks < 1 || rank < 0 ||
+        rank >= nranks)
+        return FHE_ERR_INVALID;
+    FHE_HIP_CHECK(hipSetDevice(c->device));
+    c->release_comm();
+    c->tx = *tx;
+    c->has_tx = true;
+    c->nranks = nranks;
+    c->rank = rank;
+    return FHE_OK;
+}
+
 int fhe_ctx_set_comm_timeout(fhe_ctx* c, uint32_t timeout_ms) {
     if (!c || timeout_ms == 0) return FHE_ERR_INVALID;
     if (!c->comm) {
@@ -503,7 +561,7 @@ int fhe_ctx_detach_comm(fhe_ctx* c) {
 // the receivers' buffer allocations are agreed with a one-word all-reduce (min) before any data
 // moves; the final wait is bounded (comm_wait: deadline, then ncclCommAbort).
 int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
-    if (!c || !c->comm || root < 0 || root >= c->nranks) {
+    if (!c || !c->attached() || root < 0 || root >= c->nranks) {
         set_error("broadcast_server_key needs an attached communicator and a valid root");
         return FHE_ERR_INVALID;
     }
@@ -579,15 +637,20 @@ int fhe_ctx_broadcast_server_key(fhe_ctx* c, int root) {
         set_error(local_ok ? std::string("broadcast_server_key: another rank could not take the key") : local_why);
         return local_ok ? FHE_ERR_INVALID : FHE_ERR_ALLOC;
     }
-    ncclComm_t comm = (ncclComm_t)c->comm;
-    const uint32_t tmo = c->comm_timeout_ms;
     uint64_t* ksk_buf = is_root ? c->d_ksk : n_ksk;
     double2* bsk_buf = is_root ? c->d_bsk : n_bsk;
-    rc = nccl_settle(comm, ncclBroadcast(ksk_buf, ksk_buf, ksk_words, ncclUint64, root, comm, c->stream),
-                     "ncclBroadcast", tmo, false);
-    if (!rc)
-        rc = nccl_settle(comm, ncclBroadcast(bsk_buf, bsk_buf, bsk_doubles, ncclFloat64, root, comm, c->stream),
+    if (c->has_tx) {
+        rc = tx_bcast_device(c, ksk_buf, ksk_words * 8, root);
+        if (!rc) rc = tx_bcast_device(c, bsk_buf, bsk_doubles * 8, root);
+    } else {
+        ncclComm_t comm = (ncclComm_t)c->comm;
+        const uint32_t tmo = c->comm_timeout_ms;
+        rc = nccl_settle(comm, ncclBroadcast(ksk_buf, ksk_buf, ksk_words, ncclUint64, root, comm, c->stream),
                          "ncclBroadcast", tmo, false);
+        if (!rc)
+            rc = nccl_settle(comm, ncclBroadcast(bsk_buf, bsk_buf, bsk_doubles, ncclFloat64, root, comm, c->stream),
+                             "ncclBroadcast", tmo, false);
+    }
     if (!rc) rc = comm_wait(c, "broadcast_server_key");
     if (rc || is_root) {
         if (rc) drop_new();

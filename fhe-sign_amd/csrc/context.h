@@ -100,7 +100,11 @@ struct fhe_ctx {
     size_t fanout_min = 257;  // above one ciphertext per CU (256 CUs) a level costs 2x the floor
     uint64_t* d_gather = nullptr;        // [nranks * chunk][2049]
     size_t gather_cap = 0;               // ciphertexts
-    int fanout_world() const { return comm ? nranks : (fanout_emulate > 1 ? fanout_emulate : 1); }
+    // test hook (fhe_ctx_attach_test_transport): the collectives through host buffers and callbacks
+    fhe_test_transport tx{};
+    bool has_tx = false;
+    bool attached() const { return comm != nullptr || has_tx; }  // a real multi-rank transport
+    int fanout_world() const { return attached() ? nranks : (fanout_emulate > 1 ? fanout_emulate : 1); }
     int ensure_gather(size_t ciphertexts);
     // in-place all-gather of nranks segments of `words` u64 each (segment `rank` is local)
     int allgather(uint64_t* buf, size_t words);

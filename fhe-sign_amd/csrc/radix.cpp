@@ -531,7 +531,7 @@ void Engine::flush() {
         }
         // Only a real multi-rank communicator needs the agreement (the collective is rank-uniform: every
         // rank takes this branch or none does); at world size 1 it would only drain the stream.
-        if (ctx_->comm && ctx_->nranks > 1) {
+        if (ctx_->attached() && ctx_->nranks > 1) {
             const int rc = ctx_->allreduce_min_u8(dead.data(), N0);
             if (rc != FHE_OK) throw EngineError(rc, std::string("dead-node agreement: ") + last_error());
         }
@@ -662,7 +662,7 @@ void Engine::flush() {
         } else {
             // own slice (every slice when ranks are emulated on one GPU)
             for (int r = 0; r < W; ++r)
-                if (!ctx_->comm || r == ctx_->rank) pbs(r * chunk, std::min(G, (r + 1) * chunk));
+                if (!ctx_->attached() || r == ctx_->rank) pbs(r * chunk, std::min(G, (r + 1) * chunk));
             if (const int rc = ctx_->allgather(ctx_->d_gather, chunk * kBigCt); rc != FHE_OK)
                 throw EngineError(rc, std::string("all-gather: ") + last_error());
             hip_check(launch_scatter_blocks(ctx_->d_gather, reinterpret_cast<uint64_t* const*>(ld + G), (int)G,
@@ -674,7 +674,7 @@ void Engine::flush() {
         pbs_count += G;
         levels += 1;
         // this rank's bootstraps: its slice of a fanned-out level (rank 0's when ranks are emulated), else all
-        const size_t r0 = ctx_->comm ? (size_t)ctx_->rank : 0;
+        const size_t r0 = ctx_->attached() ? (size_t)ctx_->rank : 0;
         rank_pbs += split ? std::min(G, (r0 + 1) * chunk) - std::min(G, r0 * chunk) : G;
         if (level_log.size() < kLevelLogCap) level_log.push_back((uint32_t)G | (split ? kLevelSplit : 0u));
         if (trace_) {

@@ -32,6 +32,16 @@ class FheParams(C.Structure):
         return self.lwe_dimension if g == 1 else self.lwe_dimension // g * ((1 << g) - 1)
 
 
+# fhe_test_transport (include/fhe_rocm.h): the host-staged test hook in place of RCCL
+TX_BCAST = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int)
+TX_ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
+TX_MIN_U8 = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
+
+
+class TestTransport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("bcast", TX_BCAST), ("allgather", TX_ALLGATHER), ("allreduce_min_u8", TX_MIN_U8)]
+
+
 # (name, restype, argtypes) -- every symbol include/fhe_rocm.h declares
 _SIGNATURES = [
     ("fhe_last_error", C.c_char_p, []),
@@ -80,6 +90,7 @@ _SIGNATURES = [
     ("fhe_ctx_broadcast_biguint", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int]),
     ("fhe_ctx_params", C.c_int, [C.c_void_p, C.POINTER(FheParams)]),
     ("fhe_ctx_detach_comm", C.c_int, [C.c_void_p]),
+    ("fhe_ctx_attach_test_transport", C.c_int, [C.c_void_p, C.POINTER(TestTransport), C.c_int, C.c_int]),
     ("fhe_ctx_set_fanout", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
     ("fhe_ctx_fanout_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint64)]),
     ("fhe_radix_encrypt", C.c_int, [C.c_void_p, C.c_void_p, u64p, C.c_uint32, C.POINTER(C.c_void_p)]),

@@ -221,6 +221,23 @@ int fhe_ctx_broadcast_biguint(fhe_ctx* ctx, fhe_biguint** x, int root);
 /* parameters of the server key installed in a context */
 int fhe_ctx_params(const fhe_ctx* ctx, fhe_params* out);
 int fhe_ctx_detach_comm(fhe_ctx* ctx);
+/* TEST HOOK -- several ranks on one GPU (RCCL refuses two ranks per device).  Attaches a host-staged
+ * transport in place of RCCL: the engine's collectives (the fan-out all-gather, the dead-node min
+ * all-reduce, the key / operand broadcasts and their agreements) become stream syncs, host copies and
+ * calls of these callbacks (the tests implement them over a gloo process group), so every rank-
+ * dependent branch of the production fan-out runs with real rank slices.  Each callback returns 0 on
+ * success; bytes/n are the same on every rank.  Detach with fhe_ctx_detach_comm.  RCCL stays the only
+ * production transport: nothing else selects this one. */
+typedef struct fhe_test_transport {
+    void* user;
+    /* host[0..bytes) of rank `root` to every rank, in place */
+    int (*bcast)(void* user, void* host, size_t bytes, int root);
+    /* host holds nranks segments of seg_bytes, this rank's filled: fill the others */
+    int (*allgather)(void* user, void* host, size_t seg_bytes);
+    /* host[0..n) = element-wise min over the ranks, in place */
+    int (*allreduce_min_u8)(void* user, uint8_t* host, size_t n);
+} fhe_test_transport;
+int fhe_ctx_attach_test_transport(fhe_ctx* ctx, const fhe_test_transport* tx, int nranks, int rank);
 /* split threshold (default 257: above one ciphertext per CU) and, for single-GPU tests, the number of emulated ranks (0 = off) */
 int fhe_ctx_set_fanout(fhe_ctx* ctx, uint32_t min_level, int emulate_ranks);
 /* rank, world (emulated ranks counted) and the number of levels split so far */

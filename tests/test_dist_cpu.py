@@ -246,3 +246,48 @@ def test_bare_launch_deadline_kills_every_rank():
                        capture_output=True, text=True, timeout=120, env=_bare_env())
     assert p.returncode == 124, (p.returncode, p.stderr)
     assert "deadline" in p.stderr
+
+
+def _transport_rank(rank, world, port, q):
+    """the test transport's callbacks (tests/gloo_transport.py) called through their C function pointers,
+    as comm.cpp calls them, on host buffers"""
+    import ctypes as C
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.path.insert(0, os.path.join(ROOT, "fhe-sign_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gloo_transport
+    bcast, gather, amin = gloo_transport.callbacks(rank, world)
+    out = {}
+    buf = (C.c_uint8 * 1000)(*([7 if rank == 1 else 0] * 1000))
+    assert bcast(None, C.addressof(buf), 1000, 1) == 0
+    out["bcast"] = set(buf) == {7}
+    seg = 4096
+    g = (C.c_uint8 * (seg * world))()
+    for k in range(seg):
+        g[rank * seg + k] = (rank * 31 + k) % 251
+    assert gather(None, C.addressof(g), seg) == 0
+    out["gather"] = all(g[r * seg + k] == (r * 31 + k) % 251 for r in range(world) for k in range(seg))
+    f = (C.c_uint8 * 64)(*[(k + rank) % 3 for k in range(64)])
+    assert amin(None, C.addressof(f), 64) == 0
+    out["min"] = list(f) == [min((k + r) % 3 for r in range(world)) for k in range(64)]
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_test_transport_callbacks_world2():
+    """The gloo test transport that stands in for RCCL in the one-GPU world-2 fan-out test
+    (test_fanout_gpu.py::test_world2_fanout_gloo_transport): broadcast, all-gather of rank segments and
+    the element-wise min, called through the same C function pointers the engine calls."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transport_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    got = dict(q.get() for _ in range(2))
+    assert got[0] == got[1] == {"bcast": True, "gather": True, "min": True}

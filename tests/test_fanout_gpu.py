@@ -334,3 +334,43 @@ def load_comm_attached(ctx) -> bool:
         return True
     except FheError:
         return False
+
+
+def test_world2_fanout_gloo_transport():
+    """Config 5 readiness on one GPU: TWO processes run the production fan-out with real rank slices
+    through the test transport (tests/fanout_gloo_rank.py, tests/gloo_transport.py; RCCL refuses two
+    ranks per device): rank 1 receives the server key (broadcast_server_key's receive side) and the
+    operands (broadcast_biguint); each rank bootstraps only its own slice of every split level; the
+    dead-node all-reduce runs while rank 1 holds a handle rank 0 dropped.  The compat 256-bit product's
+    ciphertext bytes are equal on both ranks and equal to the unsplit run's; fast mul, the extra node
+    and both signers on BIP-340 vectors 0 and 1 are exact on both ranks."""
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "fanout_gloo_rank.py")],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    res = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=240)
+            assert p.returncode == 0, e[-3000:]
+            res.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    r0, r1 = sorted(res, key=lambda x: x["rank"])
+    for r in (r0, r1):
+        assert r["compat_ok"] and r["fast_ok"] and r["sig0_ok"] and r["sig1_ok"], r
+        assert r["compat_split_levels"] > 0 and r["split_levels"] > r["compat_split_levels"], r
+        assert r["rank_pbs"] < r["pbs"], r  # each rank bootstrapped only its slices of the split levels
+    assert r1["extra_ok"]
+    assert r0["unsplit_ok"] and r0["compat_sha"] == r1["compat_sha"] == r0["unsplit_sha"]

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle
-from fhe_sign import Context, generate_keys, multi_bit_params
+from fhe_sign import Context, default_params, generate_keys, multi_bit_params
 
 pytestmark = pytest.mark.gpu
 SEED = 0xC0FFEE
@@ -241,6 +241,53 @@ def test_keyswitch_kernels_identical(env):
         assert np.array_equal(valu, mfma), count
     ref = ok.pbs_batch(cts[:4], np.stack([ok.make_lut(t) for t in tables]), np.arange(4, dtype=np.uint32) % len(tables))
     assert np.array_equal(mfma[:4], ref)
+
+
+@pytest.mark.parametrize("lwe_bound", [44, 45])
+def test_noise_budget_lwe_bound(lwe_bound):
+    """The decode margin at the radix layer's largest input (22 units, as below) with the small key's
+    TUniform bound at 44 and at 45 (tfhe 0.10's recalled value): keyswitch + modulus
+    switch by the oracle on the same keys, the phase error's sigma in the 4096-domain (half step 64)
+    printed and bounded at 8 sigma, and every input bootstrapped to the right carry by the GPU."""
+    P, OP = default_params(), oracle.default_params()
+    P.lwe_noise_log2 = OP.lwe_noise_log2 = lwe_bound
+    ck, sk = generate_keys(P, seed=SEED)
+    ok = oracle.OracleKeys(SEED, OP)
+    ctx = Context(0)
+    try:
+        ctx.set_server_key(sk)
+        sigma, worst = _radix_limit_margin(ok, ctx, 1024)
+    finally:
+        ctx.close()
+    print(f"\nlwe TUniform 2^{lwe_bound}: 22-unit input after KS + MS: sigma {sigma:.2f}, max |err| {worst} "
+          f"of the half step 64 ({64 / sigma:.1f} sigma)")
+    assert worst < 64 and sigma * 8 < 64
+
+
+def _radix_limit_margin(ok, ctx, N):
+    """(sigma, max |error|) of 4 s0 + 2 s1 + s2 + c built from N x 4 GPU bootstrap outputs, after the
+    oracle's keyswitch and modulus switch, in the 4096-domain; the GPU bootstraps each to its carry"""
+    ident = ctx.lut(list(range(16)))
+    rs = np.random.default_rng(5)
+    s = rs.integers(0, 3, size=(3, N))
+    c = rs.integers(0, 2, size=N)
+    r = ok.rng(77)
+    fresh = np.stack([ok.encrypt(r, int(v)) for v in np.concatenate([s.ravel(), c])])
+    unit = ctx.pbs(fresh, ident).astype(np.uint64)
+    s0, s1, s2, cb = unit[:N], unit[N:2 * N], unit[2 * N:3 * N], unit[3 * N:]
+    with np.errstate(over="ignore"):
+        comb = (np.uint64(4) * s0 + np.uint64(2) * s1 + s2 + cb).astype(np.uint64)
+    m = 4 * s[0] + 2 * s[1] + s[2] + c
+    n = ok.params.n
+    sk = ok.lwe_sk.astype(np.int64)
+    small = ok.keyswitch_batch(comb)
+    ms = (((small[:, : n + 1].astype(object) + (1 << 51)) >> 52) % 4096).astype(np.int64)
+    phase = (ms[:, n] - (ms[:, :n] * sk).sum(axis=1)) % 4096
+    errs = ((phase - 128 * m + 2048) % 4096 - 2048).astype(np.float64)
+    carry = ctx.lut([1 if v >= 8 else 0 for v in range(16)])
+    out = ctx.pbs(comb, carry)
+    assert [ok.decrypt(o) for o in out] == [int(v >= 8) for v in m]
+    return float(errs.std()), int(np.abs(errs).max())
 
 
 def test_noise_budget_at_radix_limit(env):
