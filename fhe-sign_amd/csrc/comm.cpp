@@ -91,14 +91,19 @@ int tx_check(int r, const char* what) {
     set_error(std::string("test transport ") + what + " failed");
     return FHE_ERR_HIP;
 }
-// a device buffer from root to every rank: stream sync, host copy, callback, copy back
+// a device buffer from root to every rank: host copy, callback, copy back -- every copy ordered on the
+// engine stream and waited for (a pageable hipMemcpy on the null stream could still be in flight when
+// the next kernel on the engine stream reads the buffer)
 int tx_bcast_device(fhe_ctx* c, void* dev, size_t bytes, int root) {
     if (bytes == 0) return FHE_OK;
-    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
     std::vector<uint8_t> h(bytes);
-    FHE_HIP_CHECK(hipMemcpy(h.data(), dev, bytes, hipMemcpyDeviceToHost));
+    FHE_HIP_CHECK(hipMemcpyAsync(h.data(), dev, bytes, hipMemcpyDeviceToHost, c->stream));
+    FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
     int rc = tx_check(c->tx.bcast(c->tx.user, h.data(), bytes, root), "broadcast");
-    if (!rc && c->rank != root) FHE_HIP_CHECK(hipMemcpy(dev, h.data(), bytes, hipMemcpyHostToDevice));
+    if (!rc && c->rank != root) {
+        FHE_HIP_CHECK(hipMemcpyAsync(dev, h.data(), bytes, hipMemcpyHostToDevice, c->stream));
+        FHE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    }
     return rc;
 }
 
@@ -165,12 +170,15 @@ int fhe_ctx::ensure_gather(size_t n) {
 
 int fhe_ctx::allgather(uint64_t* buf, size_t words) {
     if (has_tx) {  // test transport: this rank's segment through the host, the others from the callback
-        FHE_HIP_CHECK(hipStreamSynchronize(stream));
         std::vector<uint64_t> h((size_t)nranks * words);
-        FHE_HIP_CHECK(hipMemcpy(h.data() + (size_t)rank * words, buf + (size_t)rank * words, words * 8,
-                                hipMemcpyDeviceToHost));
+        FHE_HIP_CHECK(hipMemcpyAsync(h.data() + (size_t)rank * words, buf + (size_t)rank * words, words * 8,
+                                     hipMemcpyDeviceToHost, stream));
+        FHE_HIP_CHECK(hipStreamSynchronize(stream));
         const int rc = tx_check(tx.allgather(tx.user, h.data(), words * 8), "all-gather");
-        if (!rc) FHE_HIP_CHECK(hipMemcpy(buf, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+        if (!rc) {  // ordered before the scatter on the engine stream, waited for before h goes away
+            FHE_HIP_CHECK(hipMemcpyAsync(buf, h.data(), h.size() * 8, hipMemcpyHostToDevice, stream));
+            FHE_HIP_CHECK(hipStreamSynchronize(stream));
+        }
         return rc;
     }
     if (!comm) return FHE_OK;  // emulated ranks already wrote every segment

@@ -368,8 +368,9 @@ def test_world2_fanout_gloo_transport():
             if p.poll() is None:
                 p.kill()
     r0, r1 = sorted(res, key=lambda x: x["rank"])
+    print(json.dumps(r0), json.dumps(r1), sep="\n")
     for r in (r0, r1):
-        assert r["compat_ok"] and r["fast_ok"] and r["sig0_ok"] and r["sig1_ok"], r
+        assert r["compat_ok"] and r["fast_ok"] and r["sig0_ok"] and r["sig1_ok"], (r0, r1)
         assert r["compat_split_levels"] > 0 and r["split_levels"] > r["compat_split_levels"], r
         assert r["rank_pbs"] < r["pbs"], r  # each rank bootstrapped only its slices of the split levels
     assert r1["extra_ok"]
