@@ -44,6 +44,7 @@ const Debug& debug() {
         x.chain = has("chain");
         x.chain_host = has("chain-host");
         x.residue = has("residue");
+        x.nodes = has("nodes");
         return x;
     }();
     return d;
@@ -681,6 +682,19 @@ void Engine::flush() {
             hip_check(hipStreamSynchronize(ctx_->stream), "trace sync");
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             fprintf(stderr, "[level %llu] %zu PBS %.3f ms\n", (unsigned long long)levels, G, ms);
+        }
+        if (debug().nodes) {  // FHE_DEBUG=nodes: FNV-1a of every output of this level, in level order
+            hip_check(hipStreamSynchronize(ctx_->stream), "nodes sync");
+            std::vector<uint64_t> w(kBigCt);
+            for (size_t g = 0; g < G; ++g) {
+                const PbsDesc& d = h[at[li] + g];
+                const uint64_t* dst = split ? reinterpret_cast<uint64_t* const*>(h + at[li] + G)[g] : d.dst;
+                hip_check(hipMemcpy(w.data(), dst, kBigCt * 8, hipMemcpyDeviceToHost), "nodes copy");
+                uint64_t x = 1469598103934665603ull;
+                for (uint64_t v : w) x = (x ^ v) * 1099511628211ull;
+                fprintf(stderr, "[node] %llu %zu %u %u %llu %016llx\n", (unsigned long long)levels, g, d.lut, d.nterms,
+                        (unsigned long long)d.cst, (unsigned long long)x);
+            }
         }
     }
     for (auto& n : pending_) n.hold[0]->node = -1;

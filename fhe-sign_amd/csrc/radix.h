@@ -43,9 +43,10 @@ struct Tuning {
 Tuning& tuning();
 // Engine diagnostics on stderr, read once per process from FHE_DEBUG (comma-separated): levels (sync and
 // time every level), graph (graph statistics), chain (compat chain phases, flushed), chain-host (the
-// same, host time only), residue (the residue split's phases)
+// same, host time only), residue (the residue split's phases), nodes (a hash of every launched
+// bootstrap's output, per level: cross-run / cross-rank comparisons)
 struct Debug {
-    bool levels = false, graph = false, chain = false, chain_host = false, residue = false;
+    bool levels = false, graph = false, chain = false, chain_host = false, residue = false, nodes = false;
 };
 const Debug& debug();
 
