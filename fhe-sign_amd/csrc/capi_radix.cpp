@@ -644,6 +644,29 @@ int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t
     });
 }
 
+// The recording-order fingerprint (Engine::fingerprint) of a dry la x lb BigUintFHE mul (or k + a * b)
+int fhe_host_biguint_mul_fingerprint(size_t la, size_t lb, size_t lk, int mode, uint64_t* fp) {
+    if (!fp || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
+    return guarded([&] {
+        fhe_ctx c;
+        Engine e(&c, Engine::kDry);
+        auto make = [&](size_t n) {
+            BigUint r;
+            for (size_t i = 0; i < n; ++i) {
+                Radix d;
+                for (uint32_t q = 0; q < kLimbBlocks; ++q) d.blocks.push_back(e.dry_block(3));
+                r.digits.push_back(std::move(d));
+            }
+            return r;
+        };
+        const BigUint A = make(la), B = make(lb);
+        const BigUint R = lk ? biguint_mul_add(e, A, B, make(lk), mode) : biguint_mul(e, A, B, mode);
+        e.flush();
+        *fp = e.fingerprint;
+        return FHE_OK;
+    });
+}
+
 // Test hooks of the radix size rules (radix.h Tuning): process-wide, *previous gets the old value
 int fhe_host_set_tuning(int key, int64_t value, int64_t* previous) {
     Tuning& t = tuning();

@@ -581,6 +581,22 @@ void Engine::flush() {
     const size_t round = (size_t)kRound * (size_t)std::max(1, ctx_->fanout_world());
     std::vector<std::vector<int32_t>> lv = schedule_levels(deps, 0, round);
     if (host_mode_ == kDry || host_mode_ == kSim) {  // the schedule's statistics, nothing launched
+        auto mix = [&](uint64_t v) { fingerprint = (fingerprint ^ v) * 1099511628211ull; };
+        for (auto& l : lv) {
+            mix(l.size());
+            for (int32_t k : l) {
+                const Pending& pn = pending_[k];
+                mix((uint64_t)k);
+                mix(pn.d.lut);
+                mix(pn.d.nterms);
+                mix(pn.d.cst);
+                if (pn.ext.empty())
+                    for (uint32_t u = 0; u < pn.d.nterms && u < (uint32_t)kMaxTerms; ++u) mix((uint64_t)(int64_t)pn.d.coef[u]);
+                else
+                    for (const TermExt& t : pn.ext) mix((uint64_t)(int64_t)t.coef);
+                for (int32_t dp : pn.deps) mix((uint64_t)(int64_t)dp);
+            }
+        }
         for (auto& l : lv) {
             pbs_count += l.size();
             levels += 1;
@@ -1827,10 +1843,15 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
     if (!kara.empty()) {
         // halves and (memoized by operand) normalized half sums
         std::deque<Radix> store;
+        // lookups by operand address; every iteration in first-use order (program order), never in
+        // address order: the fan-out ranks must record the same nodes in the same order (addresses
+        // differ between processes; a pointer-ordered walk permuted the half sums' nodes between ranks)
         std::map<const Radix*, std::array<const Radix*, 3>> parts;  // lo, hi, lo + hi
+        std::vector<const Radix*> first_use;
         auto halves = [&](const Radix* r) {
             auto it = parts.find(r);
             if (it != parts.end()) return;
+            first_use.push_back(r);
             const uint32_t n = live_len(*r), h = (n + 1) / 2;
             Radix lo, hi;
             lo.blocks.assign(r->blocks.begin(), r->blocks.begin() + h);
@@ -1854,10 +1875,11 @@ static std::vector<ColProblem> mul_problems_ops(Engine& e, const std::vector<Mul
         }
         std::vector<int64_t> zq, mq;
         std::vector<ColProblem> zp = mul_problems_ops(e, zops, {}, true, &zq, min_n);
-        for (auto& kv : parts) {
-            const uint32_t h = kv.second[0]->nblocks();
-            store.push_back(radix_sum(e, {kv.second[0], kv.second[1]}, h + 1));
-            kv.second[2] = &store.back();
+        for (const Radix* r : first_use) {
+            auto& pr = parts[r];
+            const uint32_t h = pr[0]->nblocks();
+            store.push_back(radix_sum(e, {pr[0], pr[1]}, h + 1));
+            pr[2] = &store.back();
         }
         std::vector<MulOp> mops;
         for (size_t i : kara) {

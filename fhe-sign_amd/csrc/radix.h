@@ -190,6 +190,11 @@ public:
     std::vector<uint32_t> level_log;
     static constexpr uint32_t kLevelSplit = 1u << 31;
     uint64_t rank_pbs = 0;  // bootstraps this rank ran itself (fanned-out levels: its slice)
+    // kDry / kSim: FNV-1a over every scheduled level's nodes in order (LUT, terms' coefficients, constant,
+    // producers by recording index) -- no addresses.  Equal across processes iff the program records
+    // the same graph in the same order, which the fan-out's split relies on (every rank scatters the
+    // gathered slices by its own node order)
+    uint64_t fingerprint = 1469598103934665603ull;
     static constexpr size_t kLevelLogCap = 1u << 20;
 
 private:

@@ -147,6 +147,8 @@ _SIGNATURES = [
     ("fhe_progress_marks_probe", C.c_int, [C.c_uint32, u32p]),
     ("fhe_host_biguint_mul", C.c_int, [u32p, C.c_size_t, u32p, C.c_size_t, u32p, C.c_size_t, C.c_int, u32p, C.c_size_t,
                                        C.POINTER(C.c_size_t)]),
+    ("fhe_host_biguint_mul_fingerprint", C.c_int, [C.c_size_t, C.c_size_t, C.c_size_t, C.c_int,
+                                                   C.POINTER(C.c_uint64)]),
     ("fhe_host_set_tuning", C.c_int, [C.c_int, C.c_int64, C.POINTER(C.c_int64)]),
     ("fhe_host_biguint_mul_stats", C.c_int, [C.c_size_t, C.c_size_t, C.c_size_t, C.c_int, C.POINTER(C.c_uint64),
                                              C.POINTER(C.c_uint64), u32p, C.c_size_t]),

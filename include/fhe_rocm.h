@@ -347,6 +347,10 @@ int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t
  * mode | FHE_HOST_STATS_COLUMNS: k + a * b in the signer's column form (fhe_biguint_mul_add_columns).
  * level_sizes (optional, up to cap entries): bootstraps per launched level. */
 #define FHE_HOST_STATS_COLUMNS 0x100
+/* The same dry run's recording-order fingerprint: a hash of every scheduled level's nodes in order (LUT,
+ * coefficients, constants, producers by recording index; no addresses).  The multi-GPU fan-out needs it
+ * equal on every rank: ranks scatter the all-gathered slices by their own node order. */
+int fhe_host_biguint_mul_fingerprint(size_t la, size_t lb, size_t lk, int mode, uint64_t* fp);
 /* Test hooks: the radix algorithms' size rules, process-wide (defaults = the product; a test moves a
  * threshold so that a small case takes the path the product takes at 256 bits).  *previous (optional)
  * gets the old value.  Not for production use; no environment variable changes them. */

@@ -4,6 +4,7 @@ node runs after its inputs, the level count is the critical path, levels are fil
 latency-kernel rounds (256) only with work that could run there, and the backward schedule keeps
 the throughput work off the chain levels' critical capacity."""
 import ctypes as C
+import os
 import random
 
 import numpy as np
@@ -148,3 +149,39 @@ def test_progress_marks_stay_spread():
         gap = ctypes.c_uint32()
         assert _lib.load().fhe_progress_marks_probe(levels, ctypes.byref(gap)) == 0
         assert 1 <= gap.value <= bound, (levels, gap.value)
+
+
+_FP_SCRIPT = r"""
+import ctypes, random, sys
+sys.path.insert(0, sys.argv[1])
+from fhe_sign import _lib
+libc = ctypes.CDLL(None)
+libc.malloc.restype = ctypes.c_void_p
+rng = random.Random(int(sys.argv[2]))
+keep = [libc.malloc(rng.randrange(16, 1 << 16)) for _ in range(rng.randrange(0, 4000))]  # shift the C++ heap
+out = []
+for la, lb, lk, mode in ((2, 2, 0, 0), (8, 8, 0, 0), (8, 8, 0, 1), (8, 1, 8, 0), (3, 5, 0, 0)):
+    fp = ctypes.c_uint64()
+    assert _lib.load().fhe_host_biguint_mul_fingerprint(la, lb, lk, mode, ctypes.byref(fp)) == 0
+    out.append(fp.value)
+    keep += [libc.malloc(rng.randrange(16, 1 << 12)) for _ in range(rng.randrange(0, 500))]
+print(out)
+"""
+
+
+def test_recording_order_is_address_independent():
+    """The fan-out splits a level by position and every rank scatters the gathered slices by ITS node
+    order, so every rank must record the same graph in the same order.  Three processes with differently
+    perturbed C++ heaps record the BigUintFHE mul (compat and fast, 2x2 to 8x8, the signer's mul-add) and
+    must produce equal recording-order fingerprints (Engine::fingerprint: no addresses).  Round 6 found
+    the Karatsuba half sums walked in operand-address order (the world-2 GPU test's wrong compat limbs)."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    outs = []
+    for seed in (1, 2, 3):
+        r = subprocess.run([sys.executable, "-c", _FP_SCRIPT, os.path.join(ROOT, "fhe-sign_amd"), str(seed)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout.strip())
+    assert outs[0] == outs[1] == outs[2], outs
