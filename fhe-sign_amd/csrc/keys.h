@@ -22,7 +22,7 @@ struct Params {
     uint32_t pbs_base_log = 23;
     uint32_t ks_base_log = 3;
     uint32_t ks_level = 5;
-    uint32_t lwe_noise_log2 = 44;
+    uint32_t lwe_noise_log2 = 45;  // recalled tfhe 0.10 new_t_uniform(45); 44 until r6
     uint32_t glwe_noise_log2 = 17;
     uint32_t message_modulus = 4;
     uint32_t carry_modulus = 4;

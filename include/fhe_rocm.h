@@ -45,7 +45,7 @@ typedef struct fhe_params {
     uint32_t pbs_level;       /* 1 */
     uint32_t ks_base_log;     /* 3 */
     uint32_t ks_level;        /* 5 */
-    uint32_t lwe_noise_log2;  /* TUniform bound, small key (44) */
+    uint32_t lwe_noise_log2;  /* TUniform bound, small key (45, recalled tfhe 0.10; 44 until r6) */
     uint32_t glwe_noise_log2; /* TUniform bound, big/GLWE key (17) */
     uint32_t message_modulus; /* 4 */
     uint32_t carry_modulus;   /* 4 */

@@ -36,7 +36,7 @@ void fho_default_params(fho_params* p) {
     p->ks_base_log = 3;
     p->ks_level = 5;
     p->pbs_base_log = 23;
-    p->lwe_noise_log2 = 44;
+    p->lwe_noise_log2 = 45; /* recalled new_t_uniform(45); 44 until r6 */
     p->glwe_noise_log2 = 17;
     p->message_modulus = 4;
     p->carry_modulus = 4;

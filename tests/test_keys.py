@@ -57,7 +57,7 @@ def test_ksk_rows_decrypt_to_gadget(keys):
             phase = (int(row[n]) - int(np.dot(row[:n].astype(object), ok.lwe_sk.astype(object)))) % 2**64
             expect = (int(ok.glwe_sk[j]) << (64 - 3 * (lv + 1))) % 2**64
             err = (phase - expect + 2**63) % 2**64 - 2**63
-            assert abs(err) <= 2**44
+            assert abs(err) <= 2**ok.params.lwe_noise_log2
 
 
 def test_batch_encryption_equals_sequential():
