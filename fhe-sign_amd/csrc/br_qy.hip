@@ -503,6 +503,332 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// k_blind_rotate_qy2: the classic (G = 1) kernel above with TWO ciphertexts per workgroup.  Every wave
+// runs its quarter of both ciphertexts at the same points in the same layouts, so each key slice it
+// loads serves two external products (half the key stream per ciphertext), both ciphertexts share the
+// two workgroup barriers of a CMUX, and a wave has two independent dependency chains to interleave
+// (the latency the single-ciphertext kernel leaves exposed at 3 waves per SIMD).  LDS: both
+// ciphertexts' regions (4 x XR_SZ) + the forward-zeta and inverse-twiddle tables; the phase-A inverse
+// twiddles W[4u], W[2u], W[u], W[u + 128] are read from global memory (loop-invariant per lane), so two
+// workgroups fit a CU (2 waves per SIMD).  Same f64 operation sequence per ciphertext as qy: identical
+// bits.  An odd count runs its last ciphertext twice and stores it once.
+__global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __restrict__ ms, int ms_stride,
+                                                          const PbsDesc* __restrict__ desc,
+                                                          const uint32_t* __restrict__ lut_idx,
+                                                          const uint64_t* __restrict__ luts,
+                                                          const cplx* __restrict__ bsk, const cplx* __restrict__ W,
+                                                          const cplx* __restrict__ ps, const cplx* __restrict__ Z,
+                                                          const cplx* __restrict__ mono, uint64_t* __restrict__ out,
+                                                          int n, int count, unsigned long long* __restrict__ clk) {
+    constexpr int NC = 2;
+    unsigned long long clk_t0 = 0, clk_r0 = 0;
+    if (clk) {
+        clk_t0 = __builtin_amdgcn_s_memtime();
+        clk_r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    constexpr int XL_Z = NC * 2 * XR_SZ, XL_T = XL_Z + XZ_SZ;
+    __shared__ __attribute__((aligned(16))) cplx s_lds[XL_T + XT_SZ];
+    cplx* s_z = s_lds + XL_Z;
+    cplx* s_t = s_lds + XL_T;
+    if (threadIdx.x < 16) {
+        const int m = threadIdx.x >> 2, c = threadIdx.x & 3;
+        s_t[5 * m + c] = W[c == 0 ? 128 * m : c == 1 ? 64 * m : 32 * m + (c == 3 ? 128 : 0)];
+    } else if (threadIdx.x < 16 + 64) {
+        const int e = threadIdx.x - 16, c = e >> 5, m5 = e & 31;
+        s_t[20 + 34 * c + 17 * (m5 & 1) + (m5 >> 1)] = W[c == 0 ? 16 * m5 : 8 * m5];
+    }
+    if (threadIdx.x < XZ_SZ) {
+        const int k = threadIdx.x;
+        int zi;
+        if (k < 4) zi = 8 + 2 * k;
+        else if (k < 12) zi = 16 + 2 * (k - 4);
+        else if (k < 44) zi = 32 + (k - 12);
+        else if (k < 76) zi = 64 + 2 * (k - 44);
+        else zi = 128 + 4 * ((k - 76) & 31) + 2 * ((k - 76) >> 5);
+        s_z[k] = Z[zi];
+    }
+    const int ct0 = blockIdx.x * NC;
+    const bool has1 = ct0 + 1 < count;  // wave-uniform
+    const int cts[NC] = {ct0, has1 ? ct0 + 1 : ct0};
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;
+    const int p = w >> 1, h = w & 1;
+    const int u = 2 * L + h;
+    const uint64_t* a_ct[NC] = {ms + (size_t)ct0 * ms_stride, ms + (size_t)(has1 ? ct0 + 1 : ct0) * ms_stride};
+    const int bB = xq(idx_B(h, L, 0));
+    const int bBp = xq(idx_Bp(h, L, 0));
+    const int bE = xq(idx_E(w, L, 0));
+    const int k98 = 2 * bt(L, 5) + bt(L, 4);
+    const int ip = idx_Bp(h, L, 0);
+    const int U = ip >> 5;
+    const int m2 = 2 * bt(ip, 1) + h;
+    const int kB = L & 15;
+    const int ie = idx_E(w, L, 0);
+    const int V = ie >> 2;
+    const cplx z8 = Z[256 + V], z9 = Z[512 + 2 * V];
+    uint32_t jm = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) jm |= (uint32_t)bt(ie, 9 - k) << k;
+    const uint32_t c4 = 4u * jm + 1u;
+    const int wb3 = QW1 == 3 ? bt(w, 1) : bt(w, 0), wb2 = QW1 == 3 ? bt(w, 0) : bt(w, 1);
+    const uint32_t kk = (uint32_t)__builtin_amdgcn_readfirstlane(wb3 + 2 * wb2);
+
+    double acc[NC][16];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t btm = modswitch_2n(a_ct[c][n]);
+        const int rotb = (int)((4096u - btm) & 4095u);
+        const uint64_t* lut = luts + (size_t)(desc ? desc[cts[c]].lut : lut_idx[cts[c]]) * 2048;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            double v = 0.0;
+            if (p == 1) {
+                const uint32_t uu = (uint32_t)(128 * r + u - rotb) & 4095u;
+                v = neg_if((double)(int64_t)lut[uu & 2047u], (uu >> 11) << 31);
+            }
+            acc[c][r] = v * 0x1p-41;
+        }
+    }
+    uint32_t a_next[NC], a_next1[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        a_next[c] = modswitch_2n(a_ct[c][0]);
+        a_next1[c] = modswitch_2n(a_ct[c][1]);
+    }
+    const __amdgpu_buffer_rsrc_t mono_rs = table_rsrc(mono);
+    auto pair_factor = [&](uint32_t a) { return bptr{mono_rs, 0u, 16u * ((256u * kk * a) & 4095u)}[0]; };
+    auto lane_factor = [&](uint32_t a) { return bptr{mono_rs, ((c4 * a) & 4095u) * 16u, 0u}[0]; };
+    cplx Fn[NC], Ebn[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        Fn[c] = pair_factor(a_next[c]);
+        Ebn[c] = lane_factor(a_next[c]);
+    }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t bsk_rs = table_rsrc(bsk), ps_rs = table_rsrc(ps), w_rs = table_rsrc(W);
+    const cplx* Zu = Z;
+    uint32_t upd = 0;
+    bool red_in = false;
+    for (int i = 0; i < n; ++i) {
+        uint32_t a[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            a[c] = a_next[c];
+            a_next[c] = a_next1[c];
+            a_next1[c] = modswitch_2n(a_ct[c][i + 2 <= n ? i + 2 : n]);
+        }
+        const bool reduce = (upd++ & 1u) != 0;
+        const bptr P{ps_rs, 16u * (uint32_t)u, 0u};
+        const bptr kb{bsk_rs, 16u * (uint32_t)L, (uint32_t)(i * 4096 + w * 256) * 16u};
+        cplx Kb[16];  // key slices [4 (row, column) + point k], shared by both ciphertexts
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if ((q & 3) < kKeyEarly) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+        cplx x[NC][8];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (red_in) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) x[c][r].x = red_digit_s(acc[c][r]);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) x[c][r].y = red_digit_s(acc[c][r + 8]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) x[c][r] = make_double2(tor_digit_s(acc[c][r]), tor_digit_s(acc[c][r + 8]));
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            // ---- phase A: stages 0-2 (uniform zetas)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dit_bfly(x[c][r], x[c][r + 4], Zu[1]);
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) dit_bfly(x[c][r], x[c][r + 2], (r >> 2) ? mul_i(Zu[2]) : Zu[2]);
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) {
+                const cplx base = (r >> 2) ? Zu[6] : Zu[4];
+                dit_bfly(x[c][r], x[c][r + 1], ((r >> 1) & 1) ? mul_i(base) : base);
+            }
+            // ---- A -> B
+#pragma unroll
+            for (int r = 0; r < 4; ++r) qx_permlane<5>(x[c][r], x[c][r + 4]);
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) qx_permlane<4>(x[c][r], x[c][r + 2]);
+            // ---- phase B: stages 3, 4
+            {
+                const cplx z3 = s_z[k98], z4a = s_z[4 + 2 * k98], z4b = s_z[5 + 2 * k98];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dit_bfly(x[c][r], x[c][r + 4], (r & 1) ? mul_i(z3) : z3);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    if (r & 2) continue;
+                    const cplx base = (r & 1) ? z4b : z4a;
+                    dit_bfly(x[c][r], x[c][r + 2], (r >> 2) ? mul_i(base) : base);
+                }
+            }
+            cplx* reg = s_lds + (2 * c + p) * XR_SZ;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) reg[bB + xq(idx_B(0, 0, r))] = x[c][r];
+        }
+        // ---- B -> B' (wave-private LDS round trips, both ciphertexts)
+        wave_sync();
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            cplx* reg = s_lds + (2 * c + p) * XR_SZ;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) x[c][r] = reg[bBp + xq(idx_Bp(0, 0, r))];
+            // ---- phase B': stages 5, 6, 7
+            const cplx z5 = s_z[12 + U], z6 = s_z[44 + U], z7a = s_z[76 + U], z7b = s_z[108 + U];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dit_bfly(x[c][r], x[c][r + 4], z5);
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) dit_bfly(x[c][r], x[c][r + 2], (r & 4) ? mul_i(z6) : z6);
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) {
+                const cplx base = (r & 4) ? z7b : z7a;
+                dit_bfly(x[c][r], x[c][r + 1], (r & 2) ? mul_i(base) : base);
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) reg[bBp + xq(idx_Bp(0, 0, r))] = x[c][r];
+        }
+        cplx e0[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            e0[c] = cmul(Ebn[c], Fn[c]);
+            Fn[c] = pair_factor(a_next[c]);
+            Ebn[c] = lane_factor(a_next[c]);
+        }
+        __syncthreads();
+        // ---- phase E: both polynomials of each ciphertext at this wave's points, one ciphertext after the
+        // other (only one ciphertext's E registers live at a time: the MAC is the register peak)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if ((q & 3) >= kKeyEarly) Kb[q] = kb[(q >> 2) * 1024 + (q & 3) * 64];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) x[c][r] = s_lds[(2 * c + (r >> 2)) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) dit_bfly(x[c][r], x[c][r + 2], z8);
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) dit_bfly(x[c][r], x[c][r + 1], (r & 2) ? mul_i(z9) : z9);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const cplx d0 = x[c][k], d1 = x[c][4 + k];
+                const cplx o0 = mac2(d0, Kb[0 * 4 + k], d1, Kb[2 * 4 + k]);
+                const cplx o1 = mac2(d1, Kb[3 * 4 + k], d0, Kb[1 * 4 + k]);
+                const uint32_t tr = (uint32_t)((k >> 1) + 2 * (k & 1)) * a[c];
+                const cplx wv = k == 0 ? make_double2(e0[c].x - 1.0, e0[c].y) : turn_sel_m1(e0[c], tr);
+                x[c][k] = cmul(o0, wv);
+                x[c][4 + k] = cmul(o1, wv);
+            }
+            // ---- inverse: b0, b1 in E
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) {
+                const cplx a0 = x[c][r], c0 = x[c][r + 1];
+                x[c][r] = cadd(a0, c0);
+                x[c][r + 1] = csub(a0, c0);
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                if (r & 2) continue;
+                dit_bfly_unit(x[c][r], x[c][r + 2], (r & 1) ? mul_negi(x[c][r + 2]) : x[c][r + 2]);
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) s_lds[(2 * c + (r >> 2)) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))] = x[c][r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            cplx* reg = s_lds + (2 * c + p) * XR_SZ;
+            // ---- B' (inverse): b2, b3, b4
+#pragma unroll
+            for (int r = 0; r < 8; ++r) x[c][r] = reg[bBp + xq(idx_Bp(0, 0, r))];
+            const cplx* t2 = s_t + 5 * m2;
+            const cplx w2 = conj_(t2[0]);
+            dit_pairs<0>(x[c], [&](int) { return w2; });
+            const cplx w3 = t2[1];
+            dit_pairs<1>(x[c], [&](int r) { return conj_((r & 1) ? mul_i(w3) : w3); });
+            const cplx w4a = t2[2], w4b = t2[3];
+            dit_pairs<2>(x[c], [&](int r) {
+                const cplx base = (r & 1) ? w4b : w4a;
+                return conj_((r & 2) ? mul_i(base) : base);
+            });
+#pragma unroll
+            for (int r = 0; r < 8; ++r) reg[bBp + xq(idx_Bp(0, 0, r))] = x[c][r];
+        }
+        wave_sync();
+        cplx pst[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pst[r] = P[1024 + 128 * r];
+        const cplx w7 = conj_(bptr{w_rs, 64u * (uint32_t)u, 0u}[0]), w8 = bptr{w_rs, 32u * (uint32_t)u, 0u}[0];
+        const cplx w9a = bptr{w_rs, 16u * (uint32_t)u, 0u}[0], w9b = bptr{w_rs, 16u * (uint32_t)u, 0u}[128];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            cplx* reg = s_lds + (2 * c + p) * XR_SZ;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) x[c][r] = reg[bB + xq(idx_B(0, 0, r))];
+            const cplx w5 = s_t[20 + 17 * h + kB], w6 = s_t[54 + 17 * h + kB];
+            dit_pairs<1>(x[c], [&](int) { return conj_(w5); });
+            dit_pairs<2>(x[c], [&](int r) { return conj_((r & 2) ? mul_i(w6) : w6); });
+            // ---- B -> A
+#pragma unroll
+            for (int r = 0; r < 4; ++r) qx_permlane<5>(x[c][r], x[c][r + 4]);
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) qx_permlane<4>(x[c][r], x[c][r + 2]);
+            // ---- A (inverse): b7, b8, b9
+            dit_pairs<0>(x[c], [&](int) { return w7; });
+            dit_pairs<1>(x[c], [&](int r) { return conj_((r & 1) ? mul_i(w8) : w8); });
+            dit_pairs<2>(x[c], [&](int r) {
+                const cplx base = (r & 1) ? w9b : w9a;
+                return conj_((r & 2) ? mul_i(base) : base);
+            });
+            // ---- untwist, accumulate
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const cplx y = cmul_acc(make_double2(acc[c][r], acc[c][r + 8]), x[c][r], pst[r]);
+                acc[c][r] = y.x;
+                acc[c][r + 8] = y.y;
+            }
+        }
+        red_in = reduce;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (c == 1 && !has1) break;
+        if (red_in) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[c][r] = tor_red_s(acc[c][r]);
+        }
+        uint64_t* o = desc ? desc[cts[c]].dst : out + (size_t)cts[c] * 2049;
+        if (p == 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int j = 128 * r + u;
+                const uint64_t v = f64_to_torus(acc[c][r] * 0x1p41);
+                if (j == 0) o[0] = v;
+                else o[2048 - j] = 0ull - v;
+            }
+        } else if (u == 0) {
+            o[2048] = f64_to_torus(acc[c][0] * 0x1p41);
+        }
+    }
+    if (clk) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            atomicAdd(&clk[0], t1 - clk_t0);
+            atomicAdd(&clk[1], r1 - clk_r0);
+            atomicAdd(&clk[2], has1 ? 2ull : 1ull);
+        }
+    }
+}
+
 // Fourier BSK: blind-rotate layout (R = 4v + q, lane L' <-> idx = 4 (L' + 64 v) + q) -> E layout
 // [poly][wave e][point k][lane], one workgroup per polynomial.
 __global__ __launch_bounds__(256) void k_bsk_to_e(const cplx* __restrict__ src, cplx* __restrict__ dst) {
@@ -524,8 +850,13 @@ hipError_t launch_bsk_to_e(const cplx* bsk, int npoly, cplx* out, hipStream_t s)
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                   const uint64_t* luts, const cplx* bsk_e, const cplx* tw, const cplx* ps,
                                   const cplx* zfull, const cplx* mono, int grouping, uint64_t* out, int count, int n,
-                                  unsigned long long* clk, hipStream_t s) {
+                                  unsigned long long* clk, bool two_per_wg, hipStream_t s) {
     if (count <= 0) return hipSuccess;
+    if (grouping == 1 && two_per_wg) {
+        hipLaunchKernelGGL(k_blind_rotate_qy2, dim3((count + 1) / 2), dim3(256), 0, s, ms, ms_stride, desc, lut_idx,
+                           luts, bsk_e, tw, ps, zfull, mono, out, n, count, clk);
+        return hipGetLastError();
+    }
     if (grouping == 2)
         hipLaunchKernelGGL(k_blind_rotate_qy<2>, dim3(count), dim3(256), 0, s, ms, ms_stride, desc, lut_idx, luts,
                            bsk_e, tw, ps, zfull, mono, out, n, clk);

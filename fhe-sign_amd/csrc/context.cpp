@@ -282,7 +282,7 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
                                         d_zeta_wide, d_mono, (int)p.grouping, out, (int)count, (int)p.n, stream);
     return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_e, d_tw_quad, d_psi_quad, d_zeta_full,
                                   d_mono, (int)p.grouping, out, (int)count, (int)p.n,
-                                  clock_probe ? d_clock : nullptr, stream);
+                                  clock_probe ? d_clock : nullptr, br_kernel == FHE_BR_QY2, stream);
 }
 
 // =========================================================================== C ABI (core)
@@ -745,7 +745,10 @@ int fhe_ctx_set_ks_kernel(fhe_ctx* c, int kind) {
 
 int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
     if (!c) return FHE_ERR_INVALID;
-    if (kind == FHE_BR_QY) return FHE_OK;  // the one throughput kernel (classic and multi-bit)
+    if (kind == FHE_BR_QY || kind == FHE_BR_QY2) {  // QY2: classic levels two ciphertexts per workgroup
+        c->br_kernel = kind;
+        return FHE_OK;
+    }
     if (kind == FHE_BR_NARROW || kind == FHE_BR_PAIR || kind == FHE_BR_QUAD || kind == FHE_BR_QX) {
         set_error("retired blind-rotate kernel (NARROW r1, PAIR r2, QUAD r3, QX r4; sources in tools/retired/); "
                   "FHE_BR_QY (br_qy.hip) is the throughput kernel");
