@@ -513,7 +513,8 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
 // twiddles W[4u], W[2u], W[u], W[u + 128] are read from global memory (loop-invariant per lane), so two
 // workgroups fit a CU (2 waves per SIMD).  Same f64 operation sequence per ciphertext as qy: identical
 // bits.  An odd count runs its last ciphertext twice and stores it once.
-__global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __restrict__ ms, int ms_stride,
+template <int H>
+__global__ __launch_bounds__(256 * H, H == 1 ? 2 : 1) void k_blind_rotate_qy2(const uint64_t* __restrict__ ms, int ms_stride,
                                                           const PbsDesc* __restrict__ desc,
                                                           const uint32_t* __restrict__ lut_idx,
                                                           const uint64_t* __restrict__ luts,
@@ -527,7 +528,7 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
         clk_t0 = __builtin_amdgcn_s_memtime();
         clk_r0 = __builtin_amdgcn_s_memrealtime();
     }
-    constexpr int XL_Z = NC * 2 * XR_SZ, XL_T = XL_Z + XZ_SZ;
+    constexpr int XL_Z = H * NC * 2 * XR_SZ, XL_T = XL_Z + XZ_SZ;
     __shared__ __attribute__((aligned(16))) cplx s_lds[XL_T + XT_SZ];
     cplx* s_z = s_lds + XL_Z;
     cplx* s_t = s_lds + XL_T;
@@ -548,13 +549,17 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
         else zi = 128 + 4 * ((k - 76) & 31) + 2 * ((k - 76) >> 5);
         s_z[k] = Z[zi];
     }
-    const int ct0 = blockIdx.x * NC;
-    const bool has1 = ct0 + 1 < count;  // wave-uniform
-    const int cts[NC] = {ct0, has1 ? ct0 + 1 : ct0};
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;
+    // H = 2: two independent halves of 4 waves (ciphertext pairs) in one 8-wave workgroup; the two waves a
+    // SIMD holds read the same key slices (same quarter of the points), the second mostly from L1
+    const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+    const int ct0 = (blockIdx.x * H + half) * NC;
+    const bool has0 = ct0 < count, has1 = ct0 + 1 < count;  // wave-uniform; a half with no ciphertext
+    const int cts[NC] = {has0 ? ct0 : count - 1, has1 ? ct0 + 1 : (has0 ? ct0 : count - 1)};  // still syncs
+    const int rb = half * NC * 2;  // this half's first region
+    const int w = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3), L = threadIdx.x & 63;
     const int p = w >> 1, h = w & 1;
     const int u = 2 * L + h;
-    const uint64_t* a_ct[NC] = {ms + (size_t)ct0 * ms_stride, ms + (size_t)(has1 ? ct0 + 1 : ct0) * ms_stride};
+    const uint64_t* a_ct[NC] = {ms + (size_t)cts[0] * ms_stride, ms + (size_t)cts[1] * ms_stride};
     const int bB = xq(idx_B(h, L, 0));
     const int bBp = xq(idx_Bp(h, L, 0));
     const int bE = xq(idx_E(w, L, 0));
@@ -668,7 +673,7 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
                     dit_bfly(x[c][r], x[c][r + 2], (r >> 2) ? mul_i(base) : base);
                 }
             }
-            cplx* reg = s_lds + (2 * c + p) * XR_SZ;
+            cplx* reg = s_lds + (rb + 2 * c + p) * XR_SZ;
 #pragma unroll
             for (int r = 0; r < 8; ++r) reg[bB + xq(idx_B(0, 0, r))] = x[c][r];
         }
@@ -676,7 +681,7 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
         wave_sync();
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            cplx* reg = s_lds + (2 * c + p) * XR_SZ;
+            cplx* reg = s_lds + (rb + 2 * c + p) * XR_SZ;
 #pragma unroll
             for (int r = 0; r < 8; ++r) x[c][r] = reg[bBp + xq(idx_Bp(0, 0, r))];
             // ---- phase B': stages 5, 6, 7
@@ -711,7 +716,7 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
         for (int c = 0; c < NC; ++c) {
             if (c) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) x[c][r] = s_lds[(2 * c + (r >> 2)) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
+            for (int r = 0; r < 8; ++r) x[c][r] = s_lds[(rb + 2 * c + (r >> 2)) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))];
 #pragma unroll
             for (int r = 0; r < 8; ++r)
                 if (!(r & 2)) dit_bfly(x[c][r], x[c][r + 2], z8);
@@ -740,12 +745,12 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
                 dit_bfly_unit(x[c][r], x[c][r + 2], (r & 1) ? mul_negi(x[c][r + 2]) : x[c][r + 2]);
             }
 #pragma unroll
-            for (int r = 0; r < 8; ++r) s_lds[(2 * c + (r >> 2)) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))] = x[c][r];
+            for (int r = 0; r < 8; ++r) s_lds[(rb + 2 * c + (r >> 2)) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))] = x[c][r];
         }
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            cplx* reg = s_lds + (2 * c + p) * XR_SZ;
+            cplx* reg = s_lds + (rb + 2 * c + p) * XR_SZ;
             // ---- B' (inverse): b2, b3, b4
 #pragma unroll
             for (int r = 0; r < 8; ++r) x[c][r] = reg[bBp + xq(idx_Bp(0, 0, r))];
@@ -770,7 +775,7 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
         const cplx w9a = bptr{w_rs, 16u * (uint32_t)u, 0u}[0], w9b = bptr{w_rs, 16u * (uint32_t)u, 0u}[128];
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            cplx* reg = s_lds + (2 * c + p) * XR_SZ;
+            cplx* reg = s_lds + (rb + 2 * c + p) * XR_SZ;
 #pragma unroll
             for (int r = 0; r < 8; ++r) x[c][r] = reg[bB + xq(idx_B(0, 0, r))];
             const cplx w5 = s_t[20 + 17 * h + kB], w6 = s_t[54 + 17 * h + kB];
@@ -801,7 +806,7 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        if (c == 1 && !has1) break;
+        if ((c == 0 && !has0) || (c == 1 && !has1)) break;
         if (red_in) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[c][r] = tor_red_s(acc[c][r]);
@@ -824,7 +829,7 @@ __global__ __launch_bounds__(256, 2) void k_blind_rotate_qy2(const uint64_t* __r
         if (threadIdx.x == 0) {
             atomicAdd(&clk[0], t1 - clk_t0);
             atomicAdd(&clk[1], r1 - clk_r0);
-            atomicAdd(&clk[2], has1 ? 2ull : 1ull);
+            atomicAdd(&clk[2], (unsigned long long)(min(count, (int)(blockIdx.x + 1) * H * NC) - (int)blockIdx.x * H * NC));
         }
     }
 }
@@ -850,11 +855,15 @@ hipError_t launch_bsk_to_e(const cplx* bsk, int npoly, cplx* out, hipStream_t s)
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                   const uint64_t* luts, const cplx* bsk_e, const cplx* tw, const cplx* ps,
                                   const cplx* zfull, const cplx* mono, int grouping, uint64_t* out, int count, int n,
-                                  unsigned long long* clk, bool two_per_wg, hipStream_t s) {
+                                  unsigned long long* clk, int two_per_wg, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    if (grouping == 1 && two_per_wg) {
-        hipLaunchKernelGGL(k_blind_rotate_qy2, dim3((count + 1) / 2), dim3(256), 0, s, ms, ms_stride, desc, lut_idx,
-                           luts, bsk_e, tw, ps, zfull, mono, out, n, count, clk);
+    if (grouping == 1 && two_per_wg > 0) {
+        if (two_per_wg == 2)
+            hipLaunchKernelGGL(k_blind_rotate_qy2<2>, dim3((count + 3) / 4), dim3(512), 0, s, ms, ms_stride, desc,
+                               lut_idx, luts, bsk_e, tw, ps, zfull, mono, out, n, count, clk);
+        else
+            hipLaunchKernelGGL(k_blind_rotate_qy2<1>, dim3((count + 1) / 2), dim3(256), 0, s, ms, ms_stride, desc,
+                               lut_idx, luts, bsk_e, tw, ps, zfull, mono, out, n, count, clk);
         return hipGetLastError();
     }
     if (grouping == 2)

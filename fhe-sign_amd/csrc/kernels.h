@@ -68,12 +68,13 @@ hipError_t launch_lincomb(const PbsDesc* desc, int count, hipStream_t s);
 // the Fourier BSK in the E layout (launch_bsk_to_e), zfull = the zeta table zeta(s, b) at [2^s + b]
 // (context.cpp zeta_table); grouping 2 = the multi-bit blind rotation on the multi-bit key; clk: null,
 // or the clock probe's accumulators {shader cycles, 100 MHz ticks, workgroups} (fhe_ctx_enable_clock);
-// two_per_wg (classic only): k_blind_rotate_qy2, two ciphertexts per workgroup sharing the key stream
+// two_per_wg (classic only): k_blind_rotate_qy2 -- 1: two ciphertexts per 4-wave workgroup sharing the key
+// stream, 2: two such halves per 8-wave workgroup
 hipError_t launch_bsk_to_e(const double2* bsk, int npoly, double2* out, hipStream_t s);
 hipError_t launch_blind_rotate_qy(const uint64_t* ms, int ms_stride, const PbsDesc* desc, const uint32_t* lut_idx,
                                   const uint64_t* luts, const double2* bsk_e, const double2* tw, const double2* ps,
                                   const double2* zfull, const double2* mono, int grouping, uint64_t* out, int count,
-                                  int n, unsigned long long* clk, bool two_per_wg, hipStream_t s);
+                                  int n, unsigned long long* clk, int two_per_wg, hipStream_t s);
 
 // dst[i][0..2049) = src[i * 2049 ..] for i < count (all-gathered level outputs -> block slots)
 hipError_t launch_scatter_blocks(const uint64_t* src, uint64_t* const* dst, int count, hipStream_t s);

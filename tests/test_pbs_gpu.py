@@ -189,7 +189,7 @@ def test_throughput_kernel_ragged_batches(env):
         assert not bad, f"batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(thr[37][:6], ref)
-    for bad_kind in (6, -1):
+    for bad_kind in (7, -1):
         with pytest.raises(Exception):
             ctx.set_br_kernel(bad_kind)
 
@@ -361,9 +361,9 @@ def test_multibit_qy_kernel_bit_identical():
 
 
 def test_two_ciphertext_kernel_bit_identical():
-    """k_blind_rotate_qy2 (FHE_BR_QY2: two ciphertexts per workgroup sharing each key slice) gives qy's
-    and the oracle's words at odd and even batches (the odd count's last workgroup runs one ciphertext
-    twice and stores it once)."""
+    """k_blind_rotate_qy2 (FHE_BR_QY2: two ciphertexts per workgroup sharing each key slice; FHE_BR_QY4: two
+    such pairs per 8-wave workgroup) gives qy's and the oracle's words at every batch residue (a pair
+    with one ciphertext runs it twice and stores it once; a half with none still joins the barriers)."""
     ck, sk = generate_keys(seed=SEED)
     ok = oracle.OracleKeys(SEED)
     tables = _luts()
@@ -377,14 +377,16 @@ def test_two_ciphertext_kernel_bit_identical():
         ids = np.array([ctx.lut(t) for t in tables], np.uint32)
         ctx.set_wide_threshold(0)
         got = {}
-        for kind in (4, 5):
+        for kind in (4, 5, 6):
             ctx.set_br_kernel(kind)
-            got[kind] = {c: ctx.pbs(cts[:c], ids[lut_of[:c]]) for c in (1, 2, 3, 258, B)}
+            got[kind] = {c: ctx.pbs(cts[:c], ids[lut_of[:c]]) for c in (1, 2, 3, 5, 6, 258, B)}
+        ctx.set_br_kernel(4)
     finally:
         ctx.close()
-    for c in got[4]:
-        bad = np.flatnonzero((got[4][c] != got[5][c]).any(axis=1))
-        assert bad.size == 0, f"batch {c}: ciphertexts {bad[:5]} differ between qy2 and qy"
+    for kind in (5, 6):
+        for c in got[4]:
+            bad = np.flatnonzero((got[4][c] != got[kind][c]).any(axis=1))
+            assert bad.size == 0, f"kind {kind}, batch {c}: ciphertexts {bad[:5]} differ from qy"
     pick = np.array([0, 1, 2, 515, 1030])
     ref = ok.pbs_batch(np.ascontiguousarray(cts[pick]), np.stack([ok.make_lut(t) for t in tables]),
                        lut_of[pick].astype(np.uint32))

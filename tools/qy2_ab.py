@@ -14,7 +14,9 @@ from fhe_sign import Context, generate_keys  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-QY, QY2 = 4, 5
+QY, QY2, QY4 = 4, 5, 6
+KINDS = (QY, QY2, QY4)
+NAME = {QY: "qy", QY2: "qy2", QY4: "qy4"}
 ck, sk = generate_keys(seed=1)
 ctx = Context(0)
 ctx.set_server_key(sk)
@@ -23,13 +25,13 @@ cts = ck.encrypt_blocks(np.arange(B) % 16)
 d_in, d_out, d_lut = ctx.alloc(cts.nbytes), ctx.alloc(cts.nbytes), ctx.alloc(B * 4)
 ctx.h2d(d_in, cts)
 ctx.h2d(d_lut, np.full(B, lid, np.uint32))
-for kind in (QY, QY2):  # warm-up
+for kind in KINDS:  # warm-up
     ctx.set_br_kernel(kind)
     ctx.pbs_device(d_in, B, d_lut, d_out)
 ctx.enable_timing(True)
-outs, times, cyc = {}, {QY: [], QY2: []}, {QY: [], QY2: []}
+outs, times, cyc = {}, {k: [] for k in KINDS}, {k: [] for k in KINDS}
 for rnd in range(rounds):
-    for kind in (QY, QY2) if rnd % 2 == 0 else (QY2, QY):
+    for kind in KINDS if rnd % 2 == 0 else KINDS[::-1]:
         ctx.set_br_kernel(kind)
         ctx.enable_clock(True)
         ctx.pbs_device(d_in, B, d_lut, d_out)
@@ -43,10 +45,10 @@ for rnd in range(rounds):
             o = np.zeros_like(cts)
             ctx.d2h(o, d_out)
             outs[kind] = o
-same = np.array_equal(outs[QY], outs[QY2])
-ok = all(ck.decrypt_block(outs[QY2][i]) == (i % 16 + 1) % 16 for i in range(0, B, 97))
-a, b = min(times[QY]), min(times[QY2])
-print(f"B={B}: qy {a:.2f} ms (runs {' '.join(f'{t:.1f}' for t in times[QY])}; {min(cyc[QY]) / 1e6:.4f} M CU-cycles/PBS), "
-      f"qy2 {b:.2f} ms (runs {' '.join(f'{t:.1f}' for t in times[QY2])}; {min(cyc[QY2]) / 1e6:.4f} M CU-cycles/PBS) "
-      f"-> qy2/qy {b / a:.3f}; identical={same} decrypt_ok={ok}", flush=True)
+same = all(np.array_equal(outs[QY], outs[k]) for k in KINDS)
+ok = all(ck.decrypt_block(outs[QY4][i]) == (i % 16 + 1) % 16 for i in range(0, B, 97))
+base = min(times[QY])
+print(f"B={B}: " + "; ".join(f"{NAME[k]} {min(times[k]):.2f} ms (runs {' '.join(f'{t:.1f}' for t in times[k])}; "
+                             f"{min(cyc[k]) / 1e6:.4f} M CU-cycles/PBS; x{min(times[k]) / base:.3f})" for k in KINDS)
+      + f"; identical={same} decrypt_ok={ok}", flush=True)
 sys.exit(0 if same and ok else 1)
