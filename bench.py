@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 METRIC = "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds @1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6        # MI355X dense FP64 peak (matrix = vector on gfx950), spec
 FP64_PEAK_MEASURED_TFLOPS = 65.0  # dependent-free v_fma_f64 stream on the GPU box (tools/fp64_peak.hip)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r5", "r5q_pmc_summary.json")  # tools/profile_round.sh
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r6", "r6_pmc_summary.json")  # tools/profile_round.sh
 FANOUT_MIN = 257  # levels with at least this many bootstraps are split over the GPUs (fan-out legs)
 OPS_REPS = 3  # timed runs per ops leg (median reported)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -271,7 +271,7 @@ def cpu_baseline(seed, target_s, op_levels=None):
     return res
 
 
-def pmc_traffic(batch, kernels=("k_blind_rotate_qy<1>", "k_blind_rotate_qy grid")):
+def pmc_traffic(batch, kernels=("k_blind_rotate_qy2<1>",)):
     """HBM-side bytes per launch of the blind-rotate kernel at this batch, from the committed PMC
     summary of the same kernel (tools/profile_round.sh; FETCH_SIZE x2 + WRITE_SIZE, gfx950
     correction of MI355X_MICROARCH.md 'HBM'; Infinity-Cache hits included).  `kernels`: name
@@ -598,9 +598,10 @@ def pbs_leg(a, kind, dist, rank, world, device):
     # algorithmic HBM bytes of one blind-rotate launch: the Fourier BSK once, per PBS the keyswitched
     # LWE u64[n + 1] in, the big LWE u64[2049] out and its u32 LUT index
     hbm_bytes = bsk_bytes + B * ((n + 1) * 8 + 2049 * 8 + 4)
-    # every workgroup streams the whole Fourier BSK from L2 (one ciphertext per workgroup): the bytes
-    # the blind rotate moves L2 -> CU per launch, and their rate against the L2 peak
-    l2_bytes = B * bsk_bytes
+    # every workgroup streams the whole Fourier BSK from L2 (classic: k_blind_rotate_qy2, two ciphertexts
+    # per workgroup sharing it; multi-bit: one per workgroup): the bytes the blind rotate moves L2 -> CU
+    # per launch, and their rate against the L2 peak
+    l2_bytes = ((B + 1) // 2 if kind == "classic" else B) * bsk_bytes
     res = {
         "value": world * B * a.steps / dt,
         "ms_per_step": dt / a.steps * 1e3,
@@ -608,7 +609,7 @@ def pbs_leg(a, kind, dist, rank, world, device):
         "roofline": {
             "bound": "fp64_valu",
             "compute_pipe": "fp64 VALU (FFT butterflies; no dense contraction on the path)",
-            "kernel": "k_blind_rotate_qy<1>" if kind == "classic" else "k_blind_rotate_qy<2>",
+            "kernel": "k_blind_rotate_qy2<1>" if kind == "classic" else "k_blind_rotate_qy<2>",
             "achieved": achieved,
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
@@ -676,7 +677,7 @@ def compose_line(a, world, cl, ops, mb, fan, cpu):
     arrays, the reference-equivalent op/s, the README comparison, the multi-bit op legs and the CPU
     per-op replay."""
     B = a.batch
-    traffic, traffic_src = pmc_traffic(B)
+    traffic, traffic_src = pmc_traffic(B, (cl["roofline"]["kernel"],))
     r = cl["roofline"]
     roof = {k: r[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "peak_measured", "frac_measured",
                               "flops_per_pbs", "kernel_ms", "keyswitch_ms")}

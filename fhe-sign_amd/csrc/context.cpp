@@ -283,7 +283,10 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_e, d_tw_quad, d_psi_quad, d_zeta_full,
                                   d_mono, (int)p.grouping, out, (int)count, (int)p.n,
                                   clock_probe ? d_clock : nullptr,
-                                  br_kernel == FHE_BR_QY2 ? 1 : br_kernel == FHE_BR_QY4 ? 2 : 0, stream);
+                                  br_kernel == FHE_BR_QY2 || (br_kernel == FHE_BR_AUTO && (int)count >= kQy2Min) ? 1
+                                  : br_kernel == FHE_BR_QY4                                                 ? 2
+                                                                                                            : 0,
+                                  stream);
 }
 
 // =========================================================================== C ABI (core)
@@ -746,7 +749,7 @@ int fhe_ctx_set_ks_kernel(fhe_ctx* c, int kind) {
 
 int fhe_ctx_set_br_kernel(fhe_ctx* c, int kind) {
     if (!c) return FHE_ERR_INVALID;
-    if (kind == FHE_BR_QY || kind == FHE_BR_QY2 || kind == FHE_BR_QY4) {  // QY2 / QY4: qy2<1> / qy2<2> (classic)
+    if (kind == FHE_BR_QY || kind == FHE_BR_QY2 || kind == FHE_BR_QY4 || kind == FHE_BR_AUTO) {
         c->br_kernel = kind;
         return FHE_OK;
     }

@@ -59,7 +59,11 @@ struct fhe_ctx {
     double2* d_mono = nullptr;      // monomial table E[4096] of the multi-bit blind rotation (mono_table)
     int8_t* d_ksk_planes = nullptr; // KSK as balanced signed-byte planes (ks_mfma.hip)
     int ks_kernel = FHE_KS_MFMA;
-    int br_kernel = FHE_BR_QY;  // classic throughput kernel: FHE_BR_QY or FHE_BR_QY2 (fhe_ctx_set_br_kernel)
+    // classic throughput kernel (fhe_ctx_set_br_kernel): FHE_BR_AUTO = qy2 (two ciphertexts per workgroup)
+    // for levels of >= kQy2Min bootstraps, qy below (qy2 fills half the workgroups: slower from 257 to ~2k,
+    // profiles/r6/qy2_sizes_r6l.txt); FHE_BR_QY / _QY2 / _QY4 force one kernel
+    int br_kernel = FHE_BR_AUTO;
+    static constexpr int kQy2Min = 3072;
     int8_t* d_ks_digits = nullptr;  // keyswitch digits workspace
     uint64_t* d_ks_body = nullptr;
     size_t ks_cap = 0;              // ciphertexts

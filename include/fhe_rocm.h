@@ -169,6 +169,7 @@ int fhe_ctx_set_wide_threshold(fhe_ctx* ctx, int threshold);
 #define FHE_BR_QY 4
 #define FHE_BR_QY2 5 /* br_qy.hip k_blind_rotate_qy2<1>: classic, two ciphertexts per workgroup sharing key slices */
 #define FHE_BR_QY4 6 /* k_blind_rotate_qy2<2>: two such pairs per 8-wave workgroup (the pairs' key reads meet in L1) */
+#define FHE_BR_AUTO 7 /* default: qy2<1> for classic levels of >= 3072 bootstraps, qy below and for multi-bit */
 int fhe_ctx_set_br_kernel(fhe_ctx* ctx, int kind);
 
 /* Keyswitch: int8 matrix-core contraction against the KSK's byte planes (FHE_KS_MFMA, default) or

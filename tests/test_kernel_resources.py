@@ -35,7 +35,8 @@ def descriptors(src, tmp_path, flags=()):
     ("br_wide.hip", (), "k_blind_rotate_wideILi2", 1, 256, 0),  # the same, multi-bit
     ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qyILi1", 3, 168, 0),  # classic: 3 four-wave workgroups per CU, 3 waves/SIMD
     ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qyILi2", 2, 256, 0),  # multi-bit: 2 per CU, 2 waves/SIMD
-    ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qy2", 2, 256, 0),  # classic, two ciphertexts per workgroup: 2 per CU
+    ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qy2ILi1", 2, 256, 0),  # classic, two ciphertexts per workgroup: 2 per CU
+    ("br_qy.hip", ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"), "k_blind_rotate_qy2ILi2", 1, 256, 0),  # 8-wave variant: 1 per CU
     ("ks_mfma.hip", (), "k_ks_mfmaILi2", 3, 168, 0),  # keyswitch, latency levels: 3 workgroups per CU
     ("ks_mfma.hip", (), "k_ks_mfmaILi4", 2, 512, 0),  # keyswitch, large batches: one wave per SIMD, no spill
 ])

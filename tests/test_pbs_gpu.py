@@ -184,12 +184,13 @@ def test_throughput_kernel_ragged_batches(env):
         thr = {c: ctx.pbs(cts[:c], lut_ids[:c]) for c in (1, 2, 3, 37, 259)}
     finally:
         ctx.set_wide_threshold(256)
+        ctx.set_br_kernel(7)
     for c, out in thr.items():
         bad = [i for i in range(c) if not np.array_equal(out[i], wide[i])]
         assert not bad, f"batch {c}: ciphertexts {bad[:5]} differ from the latency kernel"
     ref = ok.pbs_batch(cts[:6], np.stack([ok.make_lut(t) for t in tables]), np.arange(6, dtype=np.uint32) % len(tables))
     assert np.array_equal(thr[37][:6], ref)
-    for bad_kind in (7, -1):
+    for bad_kind in (8, -1):
         with pytest.raises(Exception):
             ctx.set_br_kernel(bad_kind)
 
@@ -380,7 +381,7 @@ def test_two_ciphertext_kernel_bit_identical():
         for kind in (4, 5, 6):
             ctx.set_br_kernel(kind)
             got[kind] = {c: ctx.pbs(cts[:c], ids[lut_of[:c]]) for c in (1, 2, 3, 5, 6, 258, B)}
-        ctx.set_br_kernel(4)
+        ctx.set_br_kernel(7)
     finally:
         ctx.close()
     for kind in (5, 6):
