@@ -636,7 +636,7 @@ def pbs_leg(a, kind, dist, rank, world, device):
             # step (KS + BR + SE) and of the blind rotate alone (HIP-event kernel time)
             "cu_cycles_per_pbs": res["ms_per_step"] * 1e-3 * ghz * 1e9 * CUS / B,
             "br_cu_cycles_per_pbs": br_ms * 1e-3 * ghz * 1e9 * CUS / B,
-            "wg_cycles": cycles / wgs,  # one workgroup's (= one ciphertext's) lifetime, shader cycles
+            "wg_cycles": cycles / wgs,  # one workgroup's lifetime (classic: two ciphertexts), shader cycles
             "workgroups": wgs,
             "source": "s_memtime / s_memrealtime of every blind-rotate workgroup over the timed steps",
         }

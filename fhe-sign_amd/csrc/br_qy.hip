@@ -829,7 +829,7 @@ __global__ __launch_bounds__(256 * H, H == 1 ? 2 : 1) void k_blind_rotate_qy2(co
         if (threadIdx.x == 0) {
             atomicAdd(&clk[0], t1 - clk_t0);
             atomicAdd(&clk[1], r1 - clk_r0);
-            atomicAdd(&clk[2], (unsigned long long)(min(count, (int)(blockIdx.x + 1) * H * NC) - (int)blockIdx.x * H * NC));
+            atomicAdd(&clk[2], 1ull);  // workgroups (each lives one pair's / H pairs' whole blind rotation)
         }
     }
 }
