@@ -1,11 +1,11 @@
 """One rank of the world-2 fan-out test on ONE GPU (tests/test_fanout_gpu.py::test_world2_fanout_gloo_
 transport; not collected by pytest).  Both ranks share device 0 and exchange through the test transport
 (tests/gloo_transport.py) -- the production split with real rank slices:
-  * rank 1 has no server key: it receives rank 0's over fhe_ctx_broadcast_server_key (the receive side:
+  * ranks >= 1 have no server key: they receive rank 0's over fhe_ctx_broadcast_server_key (the receive side:
     fresh buffers, ksk_to_planes, bsk_to_e on a non-root rank);
-  * the operands exist on rank 0 only and reach rank 1 through fhe_ctx_broadcast_biguint;
+  * the operands exist on rank 0 only and reach the others through fhe_ctx_broadcast_biguint;
   * every level of >= 257 bootstraps is split, each rank bootstrapping only its own slice, outputs
-    all-gathered; dead nodes agreed by the min all-reduce while rank 1 holds a handle rank 0 dropped;
+    all-gathered; dead nodes agreed by the min all-reduce while ranks >= 1 hold a handle rank 0 dropped;
   * compat / fast 256-bit mul and sign_fhe_with_k0 (BIP-340 vectors 0 and 1, fused and call-site forms).
 Rank 0 then detaches and recomputes the compat product alone: the serialized ciphertext words of the
 split run (both ranks) must equal the unsplit run's.  Prints one JSON line per rank."""
@@ -41,10 +41,10 @@ def main():
     set_server_key(ctx)
     ck.seed_encryption(0x5EED, 100)
     A, B = (BigUintFHE.broadcast(BigUintFHE.new(v, ck) if rank == 0 else None, 0, ctx) for v in (a, b))
-    # a node only rank 1 keeps alive: rank 0 drops its handle before the next flush, so the dead-node
+    # a node only ranks >= 1 keep alive: rank 0 drops its handle before the next flush, so the dead-node
     # agreement (min over the ranks) must keep it on both
     extra = A.add(B, FAST)
-    if rank == 0:
+    if rank == 0:  # only the other ranks keep it
         del extra
     _, _, lv0 = ctx.fanout_info()
     P = A.mul(B, COMPAT)
@@ -52,7 +52,7 @@ def main():
     _, _, lv1 = ctx.fanout_info()
     out["compat_split_levels"] = lv1 - lv0
     out["compat_sha"] = hashlib.sha256(P.serialize()).hexdigest()
-    if rank == 1:
+    if rank >= 1:
         out["extra_ok"] = extra.to_biguint(ck) == a + b  # graph empty: a local read
     out["fast_ok"] = A.mul(B, FAST).to_biguint(ck) == a * b
     s = Schnorr()
