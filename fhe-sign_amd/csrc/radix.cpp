@@ -248,6 +248,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
             engine_check(it.half_table.size() == mc, "raw LUT table size");
             int64_t cst2 = 2 * (int64_t)it.cst + it.half_cst;  // half steps
             uint32_t noise = 0;
+            int64_t lo2 = 0, hi2 = 0;  // worst-case interval of the live terms (half steps, from degrees)
             for (const Term& t : it.terms) {
                 if (t.coef == 0) continue;
                 if (t.b.trivial())
@@ -255,9 +256,16 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
                 else {
                     live[i].push_back(t);
                     noise += (uint32_t)(t.coef * t.coef) * t.b.noise;
+                    const int64_t bl = t.b.half_neg ? -1 : 0, bh = 2 * (int64_t)t.b.degree - (t.b.half_neg ? 1 : 0);
+                    lo2 += t.coef > 0 ? t.coef * bl : t.coef * bh;
+                    hi2 += t.coef > 0 ? t.coef * bh : t.coef * bl;
                 }
             }
             engine_check(noise <= kMaxNoise, "raw PBS input noise above the budget");
+            // the caller guarantees the actual input lies in [-16, 16) (kSim checks every sampled one); the
+            // degrees alone must keep it inside one period of the negacyclic domain, [-32, 32) units (the
+            // widest raw item of the test suite reaches [-22.5, 21.5)), or a misuse could alias unseen
+            engine_check(cst2 + lo2 >= -64 && cst2 + hi2 < 64, "raw PBS item: input interval beyond one negacyclic period");
             if (live[i].empty()) {  // a known input: evaluate on the host
                 engine_check(cst2 % 2 == 0 && cst2 >= -32 && cst2 < 32, "raw PBS item: known input off the grid");
                 const int64_t v = cst2 / 2;

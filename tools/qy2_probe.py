@@ -1,6 +1,7 @@
 """One process's timing of the classic throughput kernel of a library build (product or a
 tools/build_variant.sh variant): HIP-event ms and clock-probe CU-cycles per PBS over `reps` launches
 at B distinct encryptions.  usage: python3 tools/qy2_probe.py PKG_DIR KIND(4 qy, 5 qy2) [B] [reps]"""
+import hashlib
 import os
 import sys
 
@@ -41,4 +42,5 @@ o = np.zeros_like(cts)
 ctx.d2h(o, d_out)
 ok = all(ck.decrypt_block(o[i]) == (i % 16 + 1) % 16 for i in range(0, B, 97))
 print(f"{os.path.basename(os.path.dirname(pkg)) or pkg} kind={kind} B={B}: {min(ms):.2f} ms (runs {' '.join(f'{x:.1f}' for x in ms)}), "
-      f"{min(cyc) / 1e6:.4f} M CU-cycles/PBS, {max(ghz_l):.3f} GHz, decrypt_ok={ok}", flush=True)
+      f"{min(cyc) / 1e6:.4f} M CU-cycles/PBS, {max(ghz_l):.3f} GHz, decrypt_ok={ok}, "
+      f"out_sha={hashlib.sha256(o.tobytes()).hexdigest()[:16]}", flush=True)
