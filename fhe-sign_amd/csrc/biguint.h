@@ -3,6 +3,10 @@
 #pragma once
 #include "radix.h"
 
+struct fhe_ctx;
+struct fhe_client_key;
+struct fhe_biguint;
+
 namespace fhe {
 
 constexpr uint32_t kLimbBlocks = 16;  // FheUint32 = 16 radix blocks
@@ -38,5 +42,9 @@ BigUint compat_chain_mul(Engine& e, const BigUint& a, const BigUint& b);
 // the chain's g = 15 - [K mod 2^32 >= 2^32 - 16] * (K mod 16) of each prefix column set (16 columns:
 // column 0 one block, columns 1..15 two blocks, each <= 3), K = sum_m (sum of column m) 4^m
 Blocks compat_chain_g(Engine& e, const std::vector<const std::vector<Blocks>*>& prefixes);
+// fhe_biguint_encrypt of several operands as one batch (capi_radix.cpp): outs[i] as if encrypted one
+// after the other
+int biguint_encrypt_batch(fhe_ctx* c, fhe_client_key* ck, const std::vector<const std::vector<uint32_t>*>& limbs,
+                          fhe_biguint** outs);
 
 }  // namespace fhe

@@ -142,6 +142,42 @@ static void column_value(const std::vector<Blocks>& cols, uint32_t nblocks, V&& 
     }
 }
 
+namespace fhe {
+// several BigUintFHE encryptions as one batch -- one pass of encrypt_big_many (its host threads over the
+// whole batch) and one upload: ciphertexts and encryption-stream state identical to encrypting the
+// operands one after the other (the signer's e_fhe and k_fhe)
+int biguint_encrypt_batch(fhe_ctx* c, fhe_client_key* ck, const std::vector<const std::vector<uint32_t>*>& limbs,
+                          fhe_biguint** outs) {
+    int rc = need_engine(c);
+    if (rc) return rc;
+    if (!ck || !outs) return FHE_ERR_INVALID;
+    return guarded([&] {
+        size_t total = 0;
+        for (auto* l : limbs) total += l->size();
+        std::vector<uint64_t> ct(total * kLimbBlocks * kBigCt), pts(total * kLimbBlocks);
+        size_t q = 0;
+        for (auto* l : limbs)
+            for (uint32_t x : *l)
+                for (uint32_t k = 0; k < kLimbBlocks; ++k) pts[q++] = (uint64_t)((x >> (2 * k)) & 3u) * ck->params.delta();
+        encrypt_big_many(ck, pts.data(), pts.size(), ct.data());
+        Blocks all = c->engine->upload_many(ct.data(), total * kLimbBlocks, 3);
+        std::vector<std::unique_ptr<fhe_biguint>> made;
+        size_t at = 0;
+        for (auto* l : limbs) {
+            auto b = std::make_unique<fhe_biguint>();
+            for (size_t i = 0; i < l->size(); ++i, at += kLimbBlocks) {
+                Radix r;
+                r.blocks.assign(all.begin() + at, all.begin() + at + kLimbBlocks);
+                b->v.digits.push_back(std::move(r));
+            }
+            made.push_back(std::move(b));
+        }
+        for (size_t i = 0; i < made.size(); ++i) outs[i] = made[i].release();
+        return FHE_OK;
+    });
+}
+}  // namespace fhe
+
 extern "C" {
 
 int fhe_radix_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint64_t* words, uint32_t bits, fhe_radix** out) {
@@ -499,25 +535,9 @@ int fhe_ctx_broadcast_biguint(fhe_ctx* c, fhe_biguint** x, int root) {
 
 // --------------------------------------------------------------------------- BigUintFHE
 int fhe_biguint_encrypt(fhe_ctx* c, fhe_client_key* ck, const uint32_t* limbs, size_t n, fhe_biguint** out) {
-    int rc = need_engine(c);
-    if (rc) return rc;
-    if (!ck || !out || (n && !limbs)) return FHE_ERR_INVALID;
-    return guarded([&] {
-        auto b = std::make_unique<fhe_biguint>();
-        std::vector<uint64_t> ct(n * kLimbBlocks * kBigCt), pts(n * kLimbBlocks);
-        for (size_t i = 0; i < n; ++i)
-            for (uint32_t k = 0; k < kLimbBlocks; ++k)
-                pts[i * kLimbBlocks + k] = (uint64_t)((limbs[i] >> (2 * k)) & 3u) * ck->params.delta();
-        encrypt_big_many(ck, pts.data(), pts.size(), ct.data());
-        Blocks all = c->engine->upload_many(ct.data(), n * kLimbBlocks, 3);
-        for (size_t i = 0; i < n; ++i) {
-            Radix r;
-            r.blocks.assign(all.begin() + i * kLimbBlocks, all.begin() + (i + 1) * kLimbBlocks);
-            b->v.digits.push_back(std::move(r));
-        }
-        *out = b.release();
-        return FHE_OK;
-    });
+    if (n && !limbs) return FHE_ERR_INVALID;
+    const std::vector<uint32_t> l(limbs, limbs + n);
+    return fhe::biguint_encrypt_batch(c, ck, {&l}, out);
 }
 
 int fhe_biguint_from_digits(const fhe_radix* const* digits, size_t n, fhe_biguint** out) {

@@ -271,7 +271,7 @@ void encrypt_big_many(fhe_client_key* ck, const uint64_t* pts, size_t n, uint64_
     constexpr uint64_t kWords = 2 * (uint64_t)kBigCt;  // 32-bit stream words one encryption consumes
     const uint64_t w0 = ck->enc_rng.word_pos();
     const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t T = std::min<size_t>(std::min<size_t>(hw, 16), n / 32);
+    const size_t T = std::min<size_t>(std::min<size_t>(hw, 16), n / 8);  // >= 8 blocks (16 KB of stream each) per thread
     ChaChaStream probe = ck->enc_rng;
     if (T <= 1 || !probe.seek(w0 + kWords * n)) {
         for (size_t i = 0; i < n; ++i) encrypt_with(ck->enc_rng, ck, pts[i], cts + i * kBigCt);

@@ -7,6 +7,7 @@
 // itself.  The plaintext EC/hash work is milliseconds on the host; the FHE block
 // (BigUintFHE::new, *, +, to_biguint) runs through the GPU radix engine.
 #include <array>
+#include <chrono>
 #include <cstring>
 #include <string>
 
@@ -477,8 +478,10 @@ int sign_prepare(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t le
     j->c = core(msg, len, U256::from_be(k0), U256::from_be(privkey));
     if (mode == FHE_SIGN_PUBLIC_OPERANDS) return FHE_OK;
     std::vector<uint32_t> el = u32_digits(j->c.e), kl = u32_digits(j->c.k);
-    int rc = fhe_biguint_encrypt(ctx, ck, el.data(), el.size(), &j->e_fhe);
-    if (!rc) rc = fhe_biguint_encrypt(ctx, ck, kl.data(), kl.size(), &j->k_fhe);
+    fhe_biguint* ek[2] = {nullptr, nullptr};
+    const int rc = biguint_encrypt_batch(ctx, ck, {&el, &kl}, ek);  // e_fhe = new(e), then k_fhe = new(k)
+    j->e_fhe = ek[0];
+    j->k_fhe = ek[1];
     return rc;
 }
 
@@ -550,10 +553,20 @@ extern "C" {
 int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t len, const uint8_t k0[32],
                                  const uint8_t privkey[32], const fhe_biguint* privkey_fhe, int mode, uint8_t sig[64]) {
     if (!sig) return FHE_ERR_INVALID;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     SignJob j;
     int rc = sign_prepare(ctx, ck, msg, len, k0, privkey, privkey_fhe, mode, &j);
+    const auto t1 = clk::now();
     if (!rc) rc = sign_begin(ctx, privkey_fhe, mode, &j);
-    return rc ? rc : sign_end(ctx, ck, &j, sig);
+    const auto t2 = clk::now();
+    if (!rc) rc = sign_end(ctx, ck, &j, sig);
+    if (fhe::debug().levels) {  // FHE_DEBUG=levels: host phases of the call
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "[sign] prologue + encryptions %.3f ms, FHE block recorded %.3f ms, flush + decrypt %.3f ms\n",
+                ms(t0, t1), ms(t1, t2), ms(t2, clk::now()));
+    }
+    return rc;
 }
 
 // A batch of independent sign_fhe_with_k0 calls run as one engine schedule (their bootstraps share
