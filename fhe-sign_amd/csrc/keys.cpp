@@ -128,6 +128,69 @@ void ChaChaStream::refill() {
     pos_ = 0;
 }
 
+// Eight consecutive ChaCha20 blocks at once, lane w = block counter + w (no counter wrap inside): the
+// rounds of refill() on 8-lane vectors (AVX2 where the host has it, two SSE halves otherwise).  Bulk
+// mask generation for encryption (fill_u64).
+namespace {
+constexpr int kLanes = 8;
+typedef uint32_t v8 __attribute__((ext_vector_type(8)));
+using Lanes = uint32_t[16][kLanes];
+__attribute__((always_inline)) inline v8 rotl8(v8 v, int c) { return (v << c) | (v >> (32 - c)); }
+#define QR8(a, b, c, d)                      \
+    a += b; d ^= a; d = rotl8(d, 16);        \
+    c += d; b ^= c; b = rotl8(b, 12);        \
+    a += b; d ^= a; d = rotl8(d, 8);         \
+    c += d; b ^= c; b = rotl8(b, 7);
+__attribute__((always_inline)) inline void chacha8_body(const uint32_t* key, const uint32_t* nonce, uint32_t ctr,
+                                                        Lanes& out) {
+    const v8 ctrs = (v8)(ctr) + (v8){0, 1, 2, 3, 4, 5, 6, 7};
+    v8 x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+    v8 x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3], x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
+    v8 x12 = ctrs, x13 = nonce[0], x14 = nonce[1], x15 = nonce[2];
+    for (int r = 0; r < 10; ++r) {
+        QR8(x0, x4, x8, x12) QR8(x1, x5, x9, x13) QR8(x2, x6, x10, x14) QR8(x3, x7, x11, x15)
+        QR8(x0, x5, x10, x15) QR8(x1, x6, x11, x12) QR8(x2, x7, x8, x13) QR8(x3, x4, x9, x14)
+    }
+    const v8 o[16] = {x0 + 0x61707865u, x1 + 0x3320646eu, x2 + 0x79622d32u, x3 + 0x6b206574u,
+                      x4 + key[0], x5 + key[1], x6 + key[2], x7 + key[3], x8 + key[4], x9 + key[5], x10 + key[6], x11 + key[7],
+                      x12 + ctrs, x13 + nonce[0], x14 + nonce[1], x15 + nonce[2]};
+    for (int i = 0; i < 16; ++i)
+        for (int w = 0; w < kLanes; ++w) out[i][w] = o[i][w];
+}
+#undef QR8
+__attribute__((target("avx2"))) void chacha8_avx2(const uint32_t* key, const uint32_t* nonce, uint32_t ctr, Lanes& out) {
+    chacha8_body(key, nonce, ctr, out);
+}
+void chacha8_base(const uint32_t* key, const uint32_t* nonce, uint32_t ctr, Lanes& out) {
+    chacha8_body(key, nonce, ctr, out);
+}
+bool has_avx2() {  // host code (this file is compiled as HIP: the device pass has no cpu builtins)
+#if defined(__HIP_DEVICE_COMPILE__)
+    return false;
+#else
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx2");
+#endif
+}
+const bool kHasAvx2 = has_avx2();
+}  // namespace
+
+void ChaChaStream::fill_u64(uint64_t* out, size_t n) {
+    size_t i = 0;
+    while (i < n && pos_ != 16) out[i++] = next_u64();  // drain the buffered block (pairs of words)
+    // whole blocks 8 at a time while more than 8 blocks remain, so the last block always comes from
+    // refill() and the buffered state equals the word-by-word path's
+    while (n - i > 8 * (size_t)kLanes && counter_ <= 0xFFFFFFFFu - kLanes) {
+        Lanes b;
+        (kHasAvx2 ? chacha8_avx2 : chacha8_base)(key_.data(), nonce_.data(), counter_, b);
+        for (int w = 0; w < kLanes; ++w)
+            for (int k = 0; k < 8; ++k) out[i + 8 * w + k] = (uint64_t)b[2 * k][w] | (uint64_t)b[2 * k + 1][w] << 32;
+        counter_ += kLanes;
+        i += 8 * kLanes;
+    }
+    while (i < n) out[i++] = next_u64();
+}
+
 void ChaChaStream::save(uint32_t* out) const {
     size_t k = 0;
     for (uint32_t v : key_) out[k++] = v;
@@ -168,12 +231,13 @@ uint64_t ChaChaStream::next_u64() {
     return lo | (hi << 32);
 }
 
-int64_t ChaChaStream::tuniform(uint32_t b) {
-    const uint64_t x = next_u64();
+int64_t tuniform_of(uint64_t x, uint32_t b) {
     const uint64_t u = x & ((1ull << (b + 1)) - 1);
     const uint64_t c = (x >> (b + 1)) & 1ull;
     return (int64_t)(u + c) - (int64_t)(1ull << b);
 }
+
+int64_t ChaChaStream::tuniform(uint32_t b) { return tuniform_of(next_u64(), b); }
 
 // ------------------------------------------------------------------------------ keygen
 // r += S * a mod (X^N + 1), S binary, exact in Z/2^64
@@ -211,11 +275,9 @@ void generate_keys(const Params& p, const KeyWords& seed, fhe_client_key* ck, fh
         for (uint32_t j = 0; j < N; ++j)
             for (uint32_t l = 0; l < L; ++l) {
                 uint64_t* row = sk->ksk.data() + ((size_t)j * L + l) * (n + 1);
+                r.fill_u64(row, n);
                 uint64_t dot = 0;
-                for (uint32_t t = 0; t < n; ++t) {
-                    row[t] = r.next_u64();
-                    dot += row[t] * ck->lwe_sk[t];
-                }
+                for (uint32_t t = 0; t < n; ++t) dot += row[t] * ck->lwe_sk[t];
                 const int64_t e = r.tuniform(p.lwe_noise_log2);
                 row[n] = dot + (ck->glwe_sk[j] << (64 - p.ks_base_log * (l + 1))) + (uint64_t)e;
             }
@@ -232,8 +294,9 @@ void generate_keys(const Params& p, const KeyWords& seed, fhe_client_key* ck, fh
             for (int row = 0; row < 2; ++row) {
                 uint64_t* A = sk->bsk.data() + (((size_t)i * 2 + row) * 2 + 0) * N;
                 uint64_t* B = sk->bsk.data() + (((size_t)i * 2 + row) * 2 + 1) * N;
-                for (uint32_t j = 0; j < N; ++j) A[j] = r.next_u64();
-                for (uint32_t j = 0; j < N; ++j) B[j] = (uint64_t)r.tuniform(p.glwe_noise_log2);
+                r.fill_u64(A, N);
+                r.fill_u64(B, N);  // tuniform of each word, in place
+                for (uint32_t j = 0; j < N; ++j) B[j] = (uint64_t)tuniform_of(B[j], p.glwe_noise_log2);
             }
     }
     const uint32_t rows = ngg * 2;
@@ -256,11 +319,9 @@ void generate_keys(const Params& p, const KeyWords& seed, fhe_client_key* ck, fh
 }
 
 static void encrypt_with(ChaChaStream& rng, const fhe_client_key* ck, uint64_t pt, uint64_t* ct) {
+    rng.fill_u64(ct, kBigDim);
     uint64_t dot = 0;
-    for (uint32_t j = 0; j < kBigDim; ++j) {
-        ct[j] = rng.next_u64();
-        dot += ct[j] * ck->glwe_sk[j];
-    }
+    for (uint32_t j = 0; j < kBigDim; ++j) dot += ct[j] * ck->glwe_sk[j];
     const int64_t e = rng.tuniform(ck->params.glwe_noise_log2);
     ct[kBigDim] = dot + pt + (uint64_t)e;
 }

@@ -63,6 +63,7 @@ public:
     void reset(uint64_t seed, uint32_t stream) { reset(seed_key(seed), stream); }
     void reset(const KeyWords& key, uint32_t stream);
     uint64_t next_u64();
+    void fill_u64(uint64_t* out, size_t n);  // n next_u64() values (bulk: 8 blocks per step)
     int64_t tuniform(uint32_t log2_bound);
     // absolute position (32-bit words) of the next output within the current nonce epoch, and a
     // jump to such a position (false if it leaves the epoch): lets independent encryptions of a
@@ -82,6 +83,9 @@ private:
     std::array<uint32_t, 16> buf_{};
     uint32_t pos_ = 16;
 };
+
+// the TUniform(b) sample ChaChaStream::tuniform draws from one 64-bit stream word x
+int64_t tuniform_of(uint64_t x, uint32_t log2_bound);
 
 // Stream ids (shared convention with the oracle so key bytes can be compared).
 enum : uint32_t { kStreamSecret = 1, kStreamKsk = 2, kStreamBsk = 3, kStreamEncrypt = 100 };
