@@ -34,7 +34,25 @@ BigUint biguint_add(Engine& e, const BigUint& A, const BigUint& B, int mode) {
     for (auto& d : B.digits) pb.push_back(&d);
     Radix wa = concat(pa), wb = concat(pb);
     const uint32_t nb = (uint32_t)(max_len + 1) * kLimbBlocks;
-    Radix s = radix_sum(e, {&wa, &wb}, nb);
+    Radix s;
+    if (A.product_cols || B.product_cols) {
+        // an exact product operand: its block-product columns + the other operand, one propagation (the
+        // limbs are the same integer: the add is exact, the product's columns sum to the product)
+        std::vector<Blocks> cols(nb);
+        for (const BigUint* x : {&A, &B}) {
+            if (x->product_cols) {
+                engine_check(x->product_cols->size() <= nb, "product columns beyond the sum");
+                for (size_t k = 0; k < x->product_cols->size(); ++k)
+                    cols[k].insert(cols[k].end(), (*x->product_cols)[k].begin(), (*x->product_cols)[k].end());
+            } else {
+                const Radix& w = x == &A ? wa : wb;
+                for (uint32_t k = 0; k < nb && k < w.nblocks(); ++k) cols[k].push_back(w.blocks[k]);
+            }
+        }
+        s = radix_propagate_columns(e, std::move(cols), nb);
+    } else {
+        s = radix_sum(e, {&wa, &wb}, nb);
+    }
     for (size_t i = 0; i <= max_len; ++i) out.digits.push_back(slice(s, (uint32_t)i * kLimbBlocks, kLimbBlocks));
     return out;
 }
@@ -125,8 +143,10 @@ static BigUint mul_impl(Engine& e, const BigUint& A, const BigUint& B, int mode,
         for (auto& d : A.digits) pa.push_back(&d);
         for (auto& d : B.digits) pb.push_back(&d);
         Radix wa = concat(pa), wb = concat(pb);
-        Radix p = radix_mul(e, wa, wb, (uint32_t)len * kLimbBlocks);
+        auto cols = std::make_shared<std::vector<Blocks>>();
+        Radix p = radix_mul_keep_columns(e, wa, wb, (uint32_t)len * kLimbBlocks, cols.get());
         for (size_t i = 0; i < len; ++i) out.digits.push_back(slice(p, (uint32_t)i * kLimbBlocks, kLimbBlocks));
+        if (!cols->empty()) out.product_cols = std::move(cols);
         return out;
     }
     // result = vec![Enc(0); la + lb]: trivial zeros (decrypt identically to src/biguint.rs:207)

@@ -1,6 +1,8 @@
 // biguint.h -- BigUintFHE: encrypted unsigned big integer as LSB-first FheUint32 limbs
 // (reference: src/biguint.rs:8-13).  add/mul follow src/biguint.rs:120-265.
 #pragma once
+#include <memory>
+
 #include "radix.h"
 
 struct fhe_ctx;
@@ -13,6 +15,11 @@ constexpr uint32_t kLimbBlocks = 16;  // FheUint32 = 16 radix blocks
 
 struct BigUint {
     std::vector<Radix> digits;  // each kLimbBlocks blocks
+    // an exact product's block-product columns (radix_mul_keep_columns), value = the digits' value:
+    // biguint_add propagates the other operand + these columns directly, so when the product itself is
+    // released unread (the reference's `k_fhe + (e_fhe * privkey_fhe)`), its normalization is dead
+    // work the engine drops at the flush.  Null for every other value.
+    std::shared_ptr<const std::vector<Blocks>> product_cols;
 };
 
 enum BigUintMode : int {

@@ -711,7 +711,8 @@ int fhe_host_set_tuning(int key, int64_t value, int64_t* previous) {
 int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64_t* pbs, uint64_t* levels,
                                uint32_t* level_sizes, size_t cap) {
     const bool columns = (mode & FHE_HOST_STATS_COLUMNS) != 0;  // the signer's column form instead
-    mode &= ~FHE_HOST_STATS_COLUMNS;
+    const bool callsite = (mode & FHE_HOST_CALL_SITE) != 0;    // mul, then add (the product released)
+    mode &= ~(FHE_HOST_STATS_COLUMNS | FHE_HOST_CALL_SITE);
     if (!pbs || !levels || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
     return guarded([&] {
         fhe_ctx c;
@@ -731,6 +732,8 @@ int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64
         uint32_t nb = 0;
         if (columns)
             cols = biguint_mul_add_columns(e, A, B, make(lk), mode, &nb);
+        else if (callsite && lk)
+            R = biguint_add(e, make(lk), biguint_mul(e, A, B, mode), mode);
         else
             R = lk ? biguint_mul_add(e, A, B, make(lk), mode) : biguint_mul(e, A, B, mode);
         e.flush();
@@ -858,6 +861,8 @@ void fhe_columns_destroy(fhe_columns* x) { delete x; }
 // radix algorithms on the CPU.  *pbs / *levels (optional): the op's schedule, as fhe_host_*_stats.
 int fhe_host_sim_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k, size_t lk,
                              int mode, uint32_t* out, size_t cap, size_t* n, uint64_t* pbs, uint64_t* levels) {
+    const bool callsite = (mode & FHE_HOST_CALL_SITE) != 0;
+    mode &= ~FHE_HOST_CALL_SITE;
     if ((la && !a) || (lb && !b) || (lk && !k) || !n || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
     return guarded([&] {
         fhe_ctx c;
@@ -872,7 +877,9 @@ int fhe_host_sim_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, si
             return r;
         };
         const BigUint A = make(a, la), B = make(b, lb);
-        const BigUint R = k ? biguint_mul_add(e, A, B, make(k, lk), mode) : biguint_mul(e, A, B, mode);
+        const BigUint R = k ? (callsite ? biguint_add(e, make(k, lk), biguint_mul(e, A, B, mode), mode)
+                                        : biguint_mul_add(e, A, B, make(k, lk), mode))
+                            : biguint_mul(e, A, B, mode);
         e.flush();
         *n = R.digits.size();
         engine_check(R.digits.size() <= cap || !out, "output buffer too small");

@@ -2049,6 +2049,14 @@ Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {
     return radix_mul_many(e, {{&a, &b}}, nblocks)[0];
 }
 
+Radix radix_mul_keep_columns(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks, std::vector<Blocks>* cols) {
+    std::vector<ColProblem> probs = mul_problems(e, {{&a, &b}}, nblocks, {}, true);
+    cols->clear();
+    // exact columns only: no Karatsuba split (whose top-level columns may hold value + q 4^N)
+    if (std::min(live_len(a), live_len(b)) < kara_min()) *cols = probs[0].cols;
+    return propagate_many(e, probs)[0];
+}
+
 std::vector<Blocks> radix_mul_add_columns(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks) {
     std::vector<ColProblem> probs = mul_problems(e, {{&a, &b}}, nblocks, {&c}, true);
     // compressed until each column fits one block (value <= 15): the columns are then the blocks of a

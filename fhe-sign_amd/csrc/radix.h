@@ -284,6 +284,11 @@ Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblo
 Blocks radix_carry_outs(Engine& e, const std::vector<std::vector<Blocks>>& problems);
 // Wrapping product.
 Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks);
+// radix_mul that also hands back the product's block-product columns (before any compression) when
+// they sum to the product exactly (no Karatsuba split), else leaves *cols empty: a later add can
+// propagate its operand + these columns in one pass (biguint_add), the product's own normalization
+// then being dead if nothing else reads it
+Radix radix_mul_keep_columns(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks, std::vector<Blocks>* cols);
 // Batched independent products (one level schedule for all); addends[i], if given, is summed into
 // product i's columns before its carry propagation (a multiply-add costs no extra level).
 std::vector<Radix> radix_mul_many(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& ops,

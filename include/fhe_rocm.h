@@ -350,6 +350,10 @@ int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t
  * mode | FHE_HOST_STATS_COLUMNS: k + a * b in the signer's column form (fhe_biguint_mul_add_columns).
  * level_sizes (optional, up to cap entries): bootstraps per launched level. */
 #define FHE_HOST_STATS_COLUMNS 0x100
+/* mode | FHE_HOST_CALL_SITE (with lk > 0; fhe_host_biguint_mul_stats and fhe_host_sim_biguint_mul): the
+ * reference's call site k + (a * b) as two ops -- fhe_biguint_mul, then fhe_biguint_add with the product
+ * released before the flush -- instead of the one-call mul-add. */
+#define FHE_HOST_CALL_SITE 0x200
 /* The same dry run's recording-order fingerprint: a hash of every scheduled level's nodes in order (LUT,
  * coefficients, constants, producers by recording index; no addresses).  The multi-GPU fan-out needs it
  * equal on every rank: ranks scatter the all-gathered slices by their own node order. */

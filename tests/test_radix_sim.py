@@ -146,6 +146,37 @@ def _biguint_mul_cases(rng):
     assert R.from_limbs(sim_mul(a, b, FAST, k)) == R.from_limbs(a) * R.from_limbs(b) + R.from_limbs(k)
 
 
+CALL_SITE = 0x200  # FHE_HOST_CALL_SITE
+
+
+@pytest.mark.parametrize("mode", [COMPAT, FAST])
+def test_call_site_mul_then_add_simulated(mode):
+    """The reference's call site k_fhe + (e_fhe * privkey_fhe) as two ops (fhe_biguint_mul, then
+    fhe_biguint_add with the product released unread): the add takes an exact product's block-product
+    columns (BigUint::product_cols), the product's own normalization is dead and dropped -- same limbs
+    as the reference's add of its mul, and the one-call mul-add's schedule (vector 0's 8 x 1 + 8 shape),
+    not a second propagation.  Shapes without exact columns (compat 2..8 limbs: the chain) keep both ops."""
+    rng = random.Random(11 + mode)
+    for la, lb, lk in [(8, 1, 8), (1, 8, 8), (3, 1, 5), (1, 1, 1), (1, 1, 3), (8, 8, 8), (2, 3, 1)]:
+        for _ in range(3):
+            a, b, k = _limbs(rng, la), _limbs(rng, lb), _limbs(rng, lk)
+            got = sim_mul(a, b, mode | CALL_SITE, k)
+            if mode == COMPAT:
+                assert got == R.biguint_add(k, R.biguint_mul(a, b)), (la, lb, lk)
+            else:
+                assert R.from_limbs(got) == R.from_limbs(a) * R.from_limbs(b) + R.from_limbs(k), (la, lb, lk)
+    full = [M32 - 1] * 8
+    assert sim_mul(full, [M32 - 1], mode | CALL_SITE, full) == R.biguint_add(full, R.biguint_mul(full, [M32 - 1]))
+    lib = _lib.load()
+
+    def stats(m):
+        p, lev = C.c_uint64(), C.c_uint64()
+        assert lib.fhe_host_biguint_mul_stats(8, 1, 8, m, C.byref(p), C.byref(lev), None, 0) == 0, lib.fhe_last_error()
+        return p.value, lev.value
+
+    assert stats(mode | CALL_SITE) == stats(mode)
+
+
 def sim_mul_add_columns(a, b, k, mode):
     A = (C.c_uint32 * max(1, len(a)))(*a)
     B = (C.c_uint32 * max(1, len(b)))(*b)
