@@ -51,6 +51,8 @@ BigUint compat_chain_mul(Engine& e, const BigUint& a, const BigUint& b);
 Blocks compat_chain_g(Engine& e, const std::vector<const std::vector<Blocks>*>& prefixes);
 // fhe_biguint_encrypt of several operands as one batch (capi_radix.cpp): outs[i] as if encrypted one
 // after the other
+// Engine::eager_next_batch on the context's engine (capi_radix.cpp)
+void engine_eager_next_batch(fhe_ctx* c, bool on);
 int biguint_encrypt_batch(fhe_ctx* c, fhe_client_key* ck, const std::vector<const std::vector<uint32_t>*>& limbs,
                           fhe_biguint** outs);
 

@@ -143,6 +143,10 @@ static void column_value(const std::vector<Blocks>& cols, uint32_t nblocks, V&& 
 }
 
 namespace fhe {
+void engine_eager_next_batch(fhe_ctx* c, bool on) {
+    if (c && c->engine) c->engine->eager_next_batch(on);
+}
+
 // several BigUintFHE encryptions as one batch -- one pass of encrypt_big_many (its host threads over the
 // whole batch) and one upload: ciphertexts and encryption-stream state identical to encrypting the
 // operands one after the other (the signer's e_fhe and k_fhe)
@@ -696,6 +700,7 @@ int fhe_host_set_tuning(int key, int64_t value, int64_t* previous) {
     case FHE_TUNE_KARA_COMPAT_MIN: old = t.kara_compat_min; t.kara_compat_min = (uint32_t)std::max<int64_t>(0, value); break;
     case FHE_TUNE_KARA_FORCE: old = t.kara_force; t.kara_force = value != 0; break;
     case FHE_TUNE_DIV_R16_LEAD: old = t.div_r16_lead; t.div_r16_lead = (uint32_t)std::max<int64_t>(0, value); break;
+    case FHE_TUNE_FLUSH_DEPTH: old = t.flush_depth; t.flush_depth = (uint32_t)std::max<int64_t>(0, value); break;
     case FHE_TUNE_SCALAR_DIV_RESIDUE:
         old = t.scalar_div_residue;
         t.scalar_div_residue = value < 0 ? -1 : value != 0;

@@ -327,6 +327,8 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     // register LUTs, allocate destinations, record pending nodes
     const uint64_t delta = p.delta();
     std::vector<TermExt> terms;
+    const size_t n_before = pending_.size();
+    bool all_independent = true;  // no new node reads a pending one
     for (size_t i : gpu) {
         uint32_t lut = 0;
         const bool raw = items[i].raw;
@@ -403,10 +405,19 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
         d.dst = out[i].slot->p;
         for (int32_t dep : n.deps) n.depth = std::max(n.depth, pending_[dep].depth + 1);
         out[i].slot->node = (int64_t)pending_.size();
-        if (!n.deps.empty()) ++pending_dependent_;
+        if (!n.deps.empty()) {
+            ++pending_dependent_;
+            all_independent = false;
+        }
+        pending_depth_ = std::max(pending_depth_, n.depth);
         pending_.push_back(std::move(n));
     }
     if (pending_.size() >= (size_t)1 << 20) flush();  // bound the deferred graph (host memory)
+    // a deep graph (a long dependent chain: the encrypted division's 660 levels) is launched in slices
+    // of flush_depth levels, so the GPU runs one slice while the host records the next instead of
+    // waiting for the whole graph (the 256-bit division's ~150 ms of host recording); the slice's
+    // levels are scheduled on their own (a boundary can cost a fill opportunity, not a level)
+    if (tuning().flush_depth && pending_depth_ >= (int32_t)tuning().flush_depth) flush();
     // the first large batch with nothing pending before it (e.g. a wide multiplication's block
     // products) is one throughput level under any schedule: launch it now, so the GPU works while
     // the host builds the rest of the graph (once per explicit flush: later independent batches,
@@ -414,8 +425,39 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     if (eager_ok_ && pending_.size() >= kEagerBatch && pending_dependent_ == 0) {
         flush();
         eager_ok_ = false;
+        eager_batch_next_ = false;
+    } else if (eager_batch_next_ && n_before > 0 && all_independent && pending_.size() - n_before >= kEagerBatch &&
+               !gstats_) {
+        // (a batch of independent programs, eager_next_batch) the program's first large batch that reads
+        // nothing pending, recorded behind the earlier programs' pending work -- the next signature's
+        // block products -- is launched now on its own, so the GPU runs it while the host records the
+        // rest; everything else stays deferred and is scheduled together (the programs share their
+        // latency levels)
+        eager_batch_next_ = false;
+        flush_tail(n_before);
     }
     return out;
+}
+
+// flush() of the nodes recorded from index k0 on (none of which reads an earlier pending node); the
+// nodes before k0 stay pending, with their indices
+void Engine::flush_tail(size_t k0) {
+    std::vector<Pending> keep(std::make_move_iterator(pending_.begin()), std::make_move_iterator(pending_.begin() + k0));
+    pending_.erase(pending_.begin(), pending_.begin() + k0);
+    for (size_t i = 0; i < pending_.size(); ++i) {
+        engine_check(pending_[i].deps.empty(), "tail flush of a node with pending producers");
+        pending_[i].hold[0]->node = (int64_t)i;
+    }
+    const size_t dependent = pending_dependent_;
+    const int32_t depth = pending_depth_;
+    const bool eager = eager_ok_;
+    pending_dependent_ = 0;
+    pending_depth_ = 1;
+    flush();
+    pending_ = std::move(keep);
+    pending_dependent_ = dependent;
+    pending_depth_ = depth;
+    eager_ok_ = eager;
 }
 
 // Level schedule of a dependency graph (deps[i]: earlier nodes node i reads).  Returns the nodes of
@@ -577,6 +619,7 @@ void Engine::flush() {
         }
         if (pending_.empty()) {
             pending_dependent_ = 0;
+        pending_depth_ = 0;
             eager_ok_ = true;
             return;
         }
@@ -614,6 +657,7 @@ void Engine::flush() {
         for (auto& n : pending_) n.hold[0]->node = -1;
         pending_.clear();
         pending_dependent_ = 0;
+        pending_depth_ = 0;
         eager_ok_ = true;
         return;
     }
@@ -724,6 +768,7 @@ void Engine::flush() {
     for (auto& n : pending_) n.hold[0]->node = -1;
     pending_.clear();  // the stream orders any later reuse of the held slots behind these launches
     pending_dependent_ = 0;
+        pending_depth_ = 0;
     eager_ok_ = true;
 }
 

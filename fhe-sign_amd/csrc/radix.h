@@ -39,6 +39,7 @@ struct Tuning {
     bool kara_force = false;        // split publicly known operands too (the host-folding algebra checks)
     uint32_t div_r16_lead = 32;     // encrypted division: leading dividend blocks taken in radix-16 steps
     int scalar_div_residue = -1;    // public divisors: -1 size rule (dividends >= 64 blocks), 0 never, 1 where valid
+    uint32_t flush_depth = 64;      // flush the deferred graph once it is this many levels deep (0: only on demand)
 };
 Tuning& tuning();
 // Engine diagnostics on stderr, read once per process from FHE_DEBUG (comma-separated): levels (sync and
@@ -182,6 +183,10 @@ public:
     static constexpr size_t kEagerHead = 3072;  // 4 rounds of the throughput kernel (3 x 256 CUs)
     // nothing pending and no eager batch since the last flush (radix_mul_many's early head launch)
     bool eager_head_ok() const { return eager_ok_ && pending_.empty(); }
+    // one-shot, before each program of a batch of independent programs recorded back to back
+    // (fhe_schnorr_sign_fhe_with_k0_batch): the program's first large batch of bootstraps that reads
+    // nothing pending (its block products) is launched as soon as it is recorded
+    void eager_next_batch(bool on) { eager_batch_next_ = on; }
     // statistics
     uint64_t pbs_count = 0, levels = 0, fanout_levels = 0;
     uint64_t dead_nodes = 0;  // recorded bootstraps dropped at flush: nothing could read their outputs
@@ -215,6 +220,7 @@ private:
     size_t run_calls_ = 0;
     static constexpr size_t kEagerBatch = 4096;
     bool eager_ok_ = true;
+    bool eager_batch_next_ = false;
     struct Pending {
         PbsDesc d;
         std::vector<std::shared_ptr<Slot>> hold;  // [0] output, then inputs: alive until launched
@@ -224,6 +230,7 @@ private:
     };
     std::vector<Pending> pending_;
     size_t pending_dependent_ = 0;  // pending nodes with at least one pending producer
+    int32_t pending_depth_ = 0;     // the deepest pending node (levels of the graph recorded so far)
     PbsDesc* h_desc_[2] = {nullptr, nullptr};  // pinned, double-buffered
     hipEvent_t desc_ev_[2] = {nullptr, nullptr};
     size_t desc_cap_ = 0;
@@ -232,6 +239,7 @@ private:
     size_t d_desc_cap_ = 0;
     void ensure_desc(size_t n);
     void graph_stats(const std::vector<std::vector<int32_t>>& deps);
+    void flush_tail(size_t k0);
     PbsDesc* stage_desc(size_t n, PbsDesc** dev);
 };
 

@@ -581,7 +581,9 @@ int fhe_schnorr_sign_fhe_with_k0_batch(fhe_ctx* ctx, fhe_client_key* ck, size_t 
         if (rc) return rc;
     }
     for (size_t i = 0; i < count; ++i) {
+        engine_eager_next_batch(ctx, true);  // this signature's block products launch as they are recorded
         int rc = sign_begin(ctx, privkeys_fhe[i], mode, &jobs[i]);
+        engine_eager_next_batch(ctx, false);
         if (rc) return rc;
     }
     for (size_t i = 0; i < count; ++i) {

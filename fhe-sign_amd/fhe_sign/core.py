@@ -276,7 +276,8 @@ class Context:
         return int(cy.value), int(tk.value), int(wg.value)
 
 
-TUNE_KEYS = {"kara_min": 1, "kara_compat_min": 2, "kara_force": 3, "div_r16_lead": 4, "scalar_div_residue": 5}
+TUNE_KEYS = {"kara_min": 1, "kara_compat_min": 2, "kara_force": 3, "div_r16_lead": 4, "scalar_div_residue": 5,
+             "flush_depth": 6}
 
 
 @contextlib.contextmanager

@@ -366,6 +366,7 @@ int fhe_host_biguint_mul_fingerprint(size_t la, size_t lb, size_t lk, int mode, 
 #define FHE_TUNE_KARA_FORCE 3          /* 1: split publicly known operands too (host-fold checks) */
 #define FHE_TUNE_DIV_R16_LEAD 4        /* encrypted division: leading radix-16 dividend blocks (default 32) */
 #define FHE_TUNE_SCALAR_DIV_RESIDUE 5  /* public divisors: -1 size rule (default), 0 never, 1 where valid */
+#define FHE_TUNE_FLUSH_DEPTH 6         /* launch the deferred graph in slices of this many levels (default 64; 0: on demand) */
 int fhe_host_set_tuning(int key, int64_t value, int64_t* previous);
 int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64_t* pbs, uint64_t* levels,
                                uint32_t* level_sizes, size_t cap);

@@ -116,6 +116,27 @@ def test_encrypted_divrem_256_simulated():
         assert sim_radix(DIVREM, 256, a, b) == expect(DIVREM, 256, a, b)
 
 
+@pytest.mark.parametrize("depth", [0, 7, 64])
+def test_sliced_flushes_keep_results(depth):
+    """The deferred graph launched in slices of `depth` levels (tuning flush_depth; default 64, 0 = only
+    on demand): every slice is scheduled on its own, results unchanged -- the 256-bit division (660
+    levels) and the compat 8 x 8 mul under small slices, and their schedules at the default depth within
+    a fraction of a percent of the unsliced one."""
+    rng = random.Random(64 + depth)
+    with tuning(flush_depth=depth):
+        a, b = rng.getrandbits(256), rng.getrandbits(130) | 1
+        assert sim_radix(DIVREM, 256, a, b) == expect(DIVREM, 256, a, b)
+        x, y = _limbs(rng, 8), _limbs(rng, 8)
+        assert sim_mul(x, y, COMPAT) == R.biguint_mul(x, y)
+    lib = _lib.load()
+    p, lev = C.c_uint64(), C.c_uint64()
+    with tuning(flush_depth=0):
+        assert lib.fhe_host_radix_stats(DIVREM, 256, C.byref(p), C.byref(lev), None, 0) == 0
+        p0, lev0 = p.value, lev.value
+    assert lib.fhe_host_radix_stats(DIVREM, 256, C.byref(p), C.byref(lev), None, 0) == 0
+    assert lev.value == lev0 and p.value <= p0 * 1.005, (p.value, lev.value, p0, lev0)
+
+
 def _limbs(rng, n):
     special = [0, 1, M32 - 1, M32 - 2, M32 // 2, 0xFFFF0000, M32 - 16, 15, 16]
     return [rng.choice(special) if rng.random() < 0.4 else rng.getrandbits(32) for _ in range(n)]
