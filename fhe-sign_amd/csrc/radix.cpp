@@ -453,11 +453,19 @@ void Engine::flush_tail(size_t k0) {
     const bool eager = eager_ok_;
     pending_dependent_ = 0;
     pending_depth_ = 1;
-    flush();
-    pending_ = std::move(keep);
-    pending_dependent_ = dependent;
-    pending_depth_ = depth;
-    eager_ok_ = eager;
+    auto restore = [&] {
+        pending_ = std::move(keep);
+        pending_dependent_ = dependent;
+        pending_depth_ = depth;
+        eager_ok_ = eager;
+    };
+    try {
+        flush();
+    } catch (...) {
+        restore();  // the earlier graph stays consistent for the caller's error path
+        throw;
+    }
+    restore();
 }
 
 // Level schedule of a dependency graph (deps[i]: earlier nodes node i reads).  Returns the nodes of
