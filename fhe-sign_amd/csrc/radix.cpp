@@ -462,6 +462,7 @@ void Engine::flush_tail(size_t k0) {
     try {
         flush();
     } catch (...) {
+        for (auto& n : pending_) n.hold[0]->node = -1;  // the tail is abandoned with the error
         restore();  // the earlier graph stays consistent for the caller's error path
         throw;
     }
