@@ -707,6 +707,11 @@ __global__ __launch_bounds__(256 * H, H == 1 ? 2 : 1) void k_blind_rotate_qy2(co
             Ebn[c] = lane_factor(a_next[c]);
         }
         __syncthreads();
+        // phase E at issue priority 1, back to 0 at the second barrier: the other workgroup's waves on the
+        // SIMD (inverse / forward transforms, no barrier due) yield to the MAC section every wave of this
+        // workgroup must finish before barrier 2 (same box: -0.6 to -1.0 % per 32768, -1.7 % cycles;
+        // profiles/r6/qy2_prio_ab_r6x.txt; the window over the transforms instead: +5.5 %)
+        __builtin_amdgcn_s_setprio(1);
         // ---- phase E: both polynomials of each ciphertext at this wave's points, one ciphertext after the
         // other (only one ciphertext's E registers live at a time: the MAC is the register peak)
 #pragma unroll
@@ -747,6 +752,7 @@ __global__ __launch_bounds__(256 * H, H == 1 ? 2 : 1) void k_blind_rotate_qy2(co
 #pragma unroll
             for (int r = 0; r < 8; ++r) s_lds[(rb + 2 * c + (r >> 2)) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))] = x[c][r];
         }
+        __builtin_amdgcn_s_setprio(0);
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
