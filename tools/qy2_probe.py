@@ -1,6 +1,6 @@
 """One process's timing of the classic throughput kernel of a library build (product or a
 tools/build_variant.sh variant): HIP-event ms and clock-probe CU-cycles per PBS over `reps` launches
-at B distinct encryptions.  usage: python3 tools/qy2_probe.py PKG_DIR KIND(4 qy, 5 qy2) [B] [reps]"""
+at B distinct encryptions.  usage: python3 tools/qy2_probe.py PKG_DIR KIND(4 qy, 5 qy2) [B] [reps] [mb: multi-bit keys]"""
 import hashlib
 import os
 import sys
@@ -10,13 +10,13 @@ sys.path.insert(0, pkg)
 import numpy as np  # noqa: E402
 
 import fhe_sign  # noqa: E402
-from fhe_sign import Context, generate_keys  # noqa: E402
+from fhe_sign import Context, generate_keys, multi_bit_params  # noqa: E402
 
 assert os.path.dirname(fhe_sign.__file__).startswith(pkg), fhe_sign.__file__
 kind = int(sys.argv[2])
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 32768
 reps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
-ck, sk = generate_keys(seed=1)
+ck, sk = generate_keys(multi_bit_params() if sys.argv[5:6] == ["mb"] else None, seed=1)
 ctx = Context(0)
 ctx.set_server_key(sk)
 ctx.set_br_kernel(kind)
