@@ -362,6 +362,10 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
             Ebn = lane_factor(a_next);
         }
         __syncthreads();
+        // multi-bit (two workgroups per CU): phase E at issue priority 1 until the second barrier, as in
+        // k_blind_rotate_qy2 (same box: -1.4 to -4 % at 512 / 1536 / 32768, -6 % cycles, same words;
+        // profiles/r6/qy2_prio_ab_r6x.txt); the classic instance (three per CU) was 1-3 % slower with it
+        if constexpr (G == 2) __builtin_amdgcn_s_setprio(1);
         if constexpr (G == 2) {
             issue(5, Gb);
             fold(4, Ga);
@@ -420,6 +424,7 @@ __global__ __launch_bounds__(256, G == 1 ? 3 : 2) void k_blind_rotate_qy(const u
         // (no barrier before these stores: E reads and writes only this wave's own points)
 #pragma unroll
         for (int r = 0; r < 8; ++r) s_lds[(r >> 2) * XR_SZ + bE + xq(idx_E(0, 0, r & 3))] = x[r];
+        if constexpr (G == 2) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         // ---- B' (inverse): b2 (register bit 0), b3 (bit 1), b4 (bit 2)
 #pragma unroll
