@@ -283,7 +283,7 @@ hipError_t fhe_ctx::blind_rotate(const fhe::PbsDesc* desc, const uint32_t* lut_i
     return launch_blind_rotate_qy(d_ms, ms_stride, desc, lut_idx, d_luts, d_bsk_e, d_tw_quad, d_psi_quad, d_zeta_full,
                                   d_mono, (int)p.grouping, out, (int)count, (int)p.n,
                                   clock_probe ? d_clock : nullptr,
-                                  br_kernel == FHE_BR_QY2 || (br_kernel == FHE_BR_AUTO && (int)count >= kQy2Min) ? 1
+                                  br_kernel == FHE_BR_QY2 || (br_kernel == FHE_BR_AUTO && qy2_fills(count)) ? 1
                                   : br_kernel == FHE_BR_QY4                                                 ? 2
                                                                                                             : 0,
                                   stream);

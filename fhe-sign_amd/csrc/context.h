@@ -60,10 +60,15 @@ struct fhe_ctx {
     int8_t* d_ksk_planes = nullptr; // KSK as balanced signed-byte planes (ks_mfma.hip)
     int ks_kernel = FHE_KS_MFMA;
     // classic throughput kernel (fhe_ctx_set_br_kernel): FHE_BR_AUTO = qy2 (two ciphertexts per workgroup)
-    // for levels of >= kQy2Min bootstraps, qy below (qy2 fills half the workgroups: slower from 257 to ~2k,
-    // profiles/r6/qy2_sizes_r6l.txt); FHE_BR_QY / _QY2 / _QY4 force one kernel
+    // where its rounds of 1024 (256 CUs x 2 workgroups x 2) fill well -- from kQy2Min bootstraps on, and
+    // from 1024 on when the last round is at least three quarters full -- qy below and between (qy2
+    // quantises worse: profiles/r6/qy2_sizes_r6l.txt, qy_qy2_thresh_r6z.txt: 1024 -5 %, 2048 -2 %, 2560
+    // even, 1280 / 1536 +19 / +2 %); FHE_BR_QY / _QY2 / _QY4 force one kernel
     int br_kernel = FHE_BR_AUTO;
     static constexpr int kQy2Min = 3072;
+    static bool qy2_fills(size_t count) {
+        return count >= (size_t)kQy2Min || (count >= 1024 && (count % 1024 == 0 || count % 1024 > 768));
+    }
     int8_t* d_ks_digits = nullptr;  // keyswitch digits workspace
     uint64_t* d_ks_body = nullptr;
     size_t ks_cap = 0;              // ciphertexts
