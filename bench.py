@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 METRIC = "PBS/s + 256-bit FHE mul wall-clock; sign_fhe_with_k0 seconds @1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6        # MI355X dense FP64 peak (matrix = vector on gfx950), spec
 FP64_PEAK_MEASURED_TFLOPS = 65.0  # dependent-free v_fma_f64 stream on the GPU box (tools/fp64_peak.hip)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r6", "r6_pmc_summary.json")  # tools/profile_round.sh
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r6", "r6f_pmc_summary.json")  # tools/profile_round.sh (final r6 tree)
 FANOUT_MIN = 257  # levels with at least this many bootstraps are split over the GPUs (fan-out legs)
 OPS_REPS = 3  # timed runs per ops leg (median reported)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
