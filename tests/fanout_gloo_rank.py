@@ -6,7 +6,8 @@ transport; not collected by pytest).  Both ranks share device 0 and exchange thr
   * the operands exist on rank 0 only and reach the others through fhe_ctx_broadcast_biguint;
   * every level of >= 257 bootstraps is split, each rank bootstrapping only its own slice, outputs
     all-gathered; dead nodes agreed by the min all-reduce while ranks >= 1 hold a handle rank 0 dropped;
-  * compat / fast 256-bit mul and sign_fhe_with_k0 (BIP-340 vectors 0 and 1, fused and call-site forms).
+  * compat / fast 256-bit mul and sign_fhe_with_k0 (BIP-340 vectors 0 and 1, fused and call-site forms),
+    the batch signer and a 128-bit encrypted division (launched in slices).
 Rank 0 then detaches and recomputes the compat product alone: the serialized ciphertext words of the
 split run (both ranks) must equal the unsplit run's.  Prints one JSON line per rank."""
 import csv
@@ -24,8 +25,8 @@ def main():
     import torch.distributed as dist
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    from fhe_sign import (COMPAT, FAST, BigUintFHE, Context, Schnorr, compute_nonce, generate_keys, rank_pbs,
-                          set_server_key, stats)
+    from fhe_sign import (COMPAT, FAST, BigUintFHE, Context, FheUint128, Schnorr, compute_nonce, generate_keys,
+                          rank_pbs, set_server_key, stats)
     import gloo_transport
     out = {"rank": rank}
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "biguint_vectors.json")))["mul"][0]
@@ -65,6 +66,19 @@ def main():
         sigs[idx] = [s.sign_fhe_with_k0(msg, k0, d, dF, ck, COMPAT).hex().upper(),
                      s.sign_fhe_with_k0_callsite(msg, k0, d, dF, ck, COMPAT).hex().upper()]
         out[f"sig{idx}_ok"] = sigs[idx] == [rows[idx]["signature"].upper()] * 2
+    # the batch signer (each signature's products launched as recorded: Engine::flush_tail) and a
+    # 128-bit encrypted division deep enough to launch in slices (flush_depth), both split over the ranks
+    jobs, want = [], []
+    for idx in ("0", "1"):
+        d = int(rows[idx]["secret key"], 16)
+        msg, aux = bytes.fromhex(rows[idx]["message"]), bytes.fromhex(rows[idx]["aux_rand"])
+        jobs.append((msg, compute_nonce(d, msg, aux), d, BigUintFHE.broadcast(BigUintFHE.new(d, ck) if rank == 0 else None, 0, ctx)))
+        want.append(bytes.fromhex(rows[idx]["signature"]))
+    out["batch_ok"] = s.sign_fhe_with_k0_batch(jobs, ck, COMPAT) == want
+    x, y = (a >> 128) | 1, (b & ((1 << 64) - 1)) | (1 << 63)
+    X, Y = (FheUint128.broadcast(FheUint128.try_encrypt(v, ck) if rank == 0 else None, 0, ctx) for v in (x, y))
+    qo, ro = X.div_rem(Y)
+    out["div_ok"] = (qo.decrypt(ck), ro.decrypt(ck)) == (x // y, x % y)
     _, _, lv2 = ctx.fanout_info()
     out["split_levels"] = lv2
     out["rank_pbs"], out["pbs"] = rank_pbs(ctx), stats(ctx)[0]

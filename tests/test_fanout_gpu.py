@@ -343,8 +343,9 @@ def test_world2_fanout_gloo_transport(world):
     ranks per device): rank 1 receives the server key (broadcast_server_key's receive side) and the
     operands (broadcast_biguint); each rank bootstraps only its own slice of every split level; the
     dead-node all-reduce runs while rank 1 holds a handle rank 0 dropped.  The compat 256-bit product's
-    ciphertext bytes are equal on both ranks and equal to the unsplit run's; fast mul, the extra node
-    and both signers on BIP-340 vectors 0 and 1 are exact on both ranks."""
+    ciphertext bytes are equal on both ranks and equal to the unsplit run's; fast mul, the extra node,
+    both signers on BIP-340 vectors 0 and 1, the batch signer (tail flushes) and a 128-bit encrypted
+    division (launch slices) are exact on both ranks."""
     import socket
     import subprocess
     import sys
@@ -372,6 +373,7 @@ def test_world2_fanout_gloo_transport(world):
     print(*(json.dumps(r) for r in res), sep="\n")
     for r in res:
         assert r["compat_ok"] and r["fast_ok"] and r["sig0_ok"] and r["sig1_ok"], res
+        assert r["batch_ok"] and r["div_ok"], r
         assert r["compat_split_levels"] > 0 and r["split_levels"] > r["compat_split_levels"], r
         assert r["rank_pbs"] < r["pbs"], r  # each rank bootstrapped only its slices of the split levels
         assert r["compat_sha"] == res[0]["unsplit_sha"], r
