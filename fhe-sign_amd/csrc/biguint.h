@@ -49,11 +49,12 @@ BigUint compat_chain_mul(Engine& e, const BigUint& a, const BigUint& b);
 // the chain's g = 15 - [K mod 2^32 >= 2^32 - 16] * (K mod 16) of each prefix column set (16 columns:
 // column 0 one block, columns 1..15 two blocks, each <= 3), K = sum_m (sum of column m) 4^m
 Blocks compat_chain_g(Engine& e, const std::vector<const std::vector<Blocks>*>& prefixes);
-// fhe_biguint_encrypt of several operands as one batch (capi_radix.cpp): outs[i] as if encrypted one
-// after the other
 // Engine::eager_next_batch on the context's engine (capi_radix.cpp)
 void engine_eager_next_batch(fhe_ctx* c, bool on);
+// fhe_biguint_encrypt of several operands as one batch (capi_radix.cpp): outs[i] as if encrypted one
+// after the other.  deferred: the encryption runs on a helper thread and the blocks are uploaded right
+// before the engine's next launch (Engine::upload_deferred); the client key must not be used meanwhile.
 int biguint_encrypt_batch(fhe_ctx* c, fhe_client_key* ck, const std::vector<const std::vector<uint32_t>*>& limbs,
-                          fhe_biguint** outs);
+                          fhe_biguint** outs, bool deferred = false);
 
 }  // namespace fhe

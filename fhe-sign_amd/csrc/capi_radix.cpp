@@ -7,6 +7,8 @@
 #include <string>
 #include <stdexcept>
 
+#include <future>
+
 #include "biguint.h"
 #include "fhe_rocm.h"
 #include "serial.h"
@@ -151,20 +153,33 @@ void engine_eager_next_batch(fhe_ctx* c, bool on) {
 // whole batch) and one upload: ciphertexts and encryption-stream state identical to encrypting the
 // operands one after the other (the signer's e_fhe and k_fhe)
 int biguint_encrypt_batch(fhe_ctx* c, fhe_client_key* ck, const std::vector<const std::vector<uint32_t>*>& limbs,
-                          fhe_biguint** outs) {
+                          fhe_biguint** outs, bool deferred) {
     int rc = need_engine(c);
     if (rc) return rc;
     if (!ck || !outs) return FHE_ERR_INVALID;
     return guarded([&] {
         size_t total = 0;
         for (auto* l : limbs) total += l->size();
-        std::vector<uint64_t> ct(total * kLimbBlocks * kBigCt), pts(total * kLimbBlocks);
+        std::vector<uint64_t> pts(total * kLimbBlocks);
         size_t q = 0;
         for (auto* l : limbs)
             for (uint32_t x : *l)
                 for (uint32_t k = 0; k < kLimbBlocks; ++k) pts[q++] = (uint64_t)((x >> (2 * k)) & 3u) * ck->params.delta();
-        encrypt_big_many(ck, pts.data(), pts.size(), ct.data());
-        Blocks all = c->engine->upload_many(ct.data(), total * kLimbBlocks, 3);
+        Blocks all;
+        if (deferred) {
+            // the encryption runs on a helper thread while the caller records the graph that reads the
+            // blocks; the engine uploads them right before its next launch (Engine::upload_deferred)
+            auto job = std::make_shared<std::future<std::vector<uint64_t>>>(std::async(std::launch::async, [ck, pts] {
+                std::vector<uint64_t> ct(pts.size() * kBigCt);
+                encrypt_big_many(ck, pts.data(), pts.size(), ct.data());
+                return ct;
+            }));
+            all = c->engine->upload_deferred(pts.size(), 3, [job] { return job->get(); });
+        } else {
+            std::vector<uint64_t> ct(total * kLimbBlocks * kBigCt);
+            encrypt_big_many(ck, pts.data(), pts.size(), ct.data());
+            all = c->engine->upload_many(ct.data(), total * kLimbBlocks, 3);
+        }
         std::vector<std::unique_ptr<fhe_biguint>> made;
         size_t at = 0;
         for (auto* l : limbs) {

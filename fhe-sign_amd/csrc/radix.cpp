@@ -551,7 +551,15 @@ std::vector<std::vector<int32_t>> schedule_levels(const std::vector<std::vector<
     return lv;
 }
 
+void Engine::run_before_launch() {
+    if (!before_launch_) return;
+    auto f = std::move(before_launch_);
+    before_launch_ = nullptr;
+    f();
+}
+
 void Engine::flush() {
+    run_before_launch();  // a deferred upload lands before anything that could read it is launched
     if (pending_.empty()) return;
     const auto f0 = std::chrono::steady_clock::now();
     if (trace_) {
@@ -904,6 +912,39 @@ Blocks Engine::upload_many(const uint64_t* cts, size_t n, uint32_t degree) {
     hip_check(hipMemcpyAsync(d_dst, dst.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice, ctx_->stream), "upload");
     hip_check(launch_scatter_blocks(d_up_, d_dst, (int)n, ctx_->stream), "upload scatter");
     hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");  // host buffers may go
+    return out;
+}
+
+Blocks Engine::upload_deferred(size_t n, uint32_t degree, std::function<std::vector<uint64_t>()> fill) {
+    run_before_launch();  // an earlier deferred upload first (one at a time)
+    Blocks out(n);
+    for (size_t i = 0; i < n; ++i) {
+        out[i].slot = pool_->alloc();
+        out[i].degree = degree;
+        out[i].noise = 1;
+    }
+    if (n == 0 || host_mode_ != kDevice) return out;
+    std::vector<std::shared_ptr<Slot>> held(n);  // alive until the upload, whatever the caller drops
+    for (size_t i = 0; i < n; ++i) held[i] = out[i].slot;
+    before_launch_ = [this, n, held = std::move(held), fill = std::move(fill)]() {
+        std::vector<uint64_t*> dst(n);
+        for (size_t i = 0; i < n; ++i) dst[i] = held[i]->p;
+        const std::vector<uint64_t> cts = fill();
+        engine_check(cts.size() == n * kBigCt, "deferred upload: ciphertext count");
+        const size_t words = n * kBigCt + n;
+        if (words > up_cap_) {
+            hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");
+            if (d_up_) hip_check(hipFree(d_up_), "hipFree");
+            hip_check(hipMalloc(&d_up_, words * 8), "hipMalloc upload");
+            up_cap_ = words;
+        }
+        uint64_t** d_dst = reinterpret_cast<uint64_t**>(d_up_ + n * kBigCt);
+        hip_check(hipMemcpyAsync(d_up_, cts.data(), n * kBigCt * 8, hipMemcpyHostToDevice, ctx_->stream), "upload");
+        hip_check(hipMemcpyAsync(d_dst, dst.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice, ctx_->stream),
+                  "upload");
+        hip_check(launch_scatter_blocks(d_up_, d_dst, (int)n, ctx_->stream), "upload scatter");
+        hip_check(hipStreamSynchronize(ctx_->stream), "upload sync");  // cts and dst go out of scope
+    };
     return out;
 }
 

@@ -171,6 +171,12 @@ public:
     Block upload(const uint64_t* ct, uint32_t degree);
     // n client-encrypted blocks (contiguous big LWEs): one copy + one scatter into their slots
     Blocks upload_many(const uint64_t* cts, size_t n, uint32_t degree);
+    // Deferred upload: n fresh slots now (degree, noise 1), their ciphertexts later.  `fill` produces the
+    // n contiguous big LWEs (e.g. a host encryption still running on another thread); it is called, and
+    // its result uploaded into the slots, right before the next flush launches anything -- so the graph
+    // that reads the slots is recorded while the ciphertexts are being made, and the upload still
+    // precedes every launch on the stream.  One pending deferred upload at a time.
+    Blocks upload_deferred(size_t n, uint32_t degree, std::function<std::vector<uint64_t>()> fill);
     void download(const Block& b, uint64_t* ct);
     // the slot blocks' ciphertexts -> host, contiguous (one gather + one copy + one wait instead of a
     // round trip per block: the decryption of a 256-bit result is 128-144 blocks)
@@ -221,6 +227,8 @@ private:
     static constexpr size_t kEagerBatch = 4096;
     bool eager_ok_ = true;
     bool eager_batch_next_ = false;
+    std::function<void()> before_launch_;  // upload_deferred's pending upload (run at the next flush)
+    void run_before_launch();
     struct Pending {
         PbsDesc d;
         std::vector<std::shared_ptr<Slot>> hold;  // [0] output, then inputs: alive until launched

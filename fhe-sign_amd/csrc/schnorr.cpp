@@ -473,13 +473,14 @@ struct SignJob {
 
 // plaintext prologue and the client-side encryptions (uploads) of e and k
 int sign_prepare(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t* msg, size_t len, const uint8_t k0[32],
-                 const uint8_t privkey[32], const fhe_biguint* privkey_fhe, int mode, SignJob* j) {
+                 const uint8_t privkey[32], const fhe_biguint* privkey_fhe, int mode, SignJob* j,
+                 bool deferred = false) {
     if (!ctx || !ck || (len && !msg) || !k0 || !privkey || !privkey_fhe) return FHE_ERR_INVALID;
     j->c = core(msg, len, U256::from_be(k0), U256::from_be(privkey));
     if (mode == FHE_SIGN_PUBLIC_OPERANDS) return FHE_OK;
     std::vector<uint32_t> el = u32_digits(j->c.e), kl = u32_digits(j->c.k);
     fhe_biguint* ek[2] = {nullptr, nullptr};
-    const int rc = biguint_encrypt_batch(ctx, ck, {&el, &kl}, ek);  // e_fhe = new(e), then k_fhe = new(k)
+    const int rc = biguint_encrypt_batch(ctx, ck, {&el, &kl}, ek, deferred);  // e_fhe = new(e), then k_fhe = new(k)
     j->e_fhe = ek[0];
     j->k_fhe = ek[1];
     return rc;
@@ -556,7 +557,9 @@ int fhe_schnorr_sign_fhe_with_k0(fhe_ctx* ctx, fhe_client_key* ck, const uint8_t
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     SignJob j;
-    int rc = sign_prepare(ctx, ck, msg, len, k0, privkey, privkey_fhe, mode, &j);
+    // e and k are encrypted on a helper thread while sign_begin records the FHE block; their upload
+    // lands right before the block's first launch
+    int rc = sign_prepare(ctx, ck, msg, len, k0, privkey, privkey_fhe, mode, &j, true);
     const auto t1 = clk::now();
     if (!rc) rc = sign_begin(ctx, privkey_fhe, mode, &j);
     const auto t2 = clk::now();

@@ -1,6 +1,6 @@
 """One op (compat / fast 256-bit mul, the 256-bit / encrypted division, or the 8-signature batch), run twice, the second time
 timed; under rocprofv3 --kernel-trace its kernel timeline shows where the GPU waits for the host.
-usage: rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 tools/op_gaps.py compat|fast|div|divu32|batch8
+usage: rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 tools/op_gaps.py compat|fast|div|divu32|batch8|sign
 then:  python3 tools/op_gaps.py --analyze DIR/run_kernel_trace.csv"""
 import os
 import sys
@@ -53,6 +53,12 @@ elif op == "batch8":  # bench.py's config-5b batch: BIP-340 vectors 0, 1, 2, 15,
         mm, aux = bytes.fromhex(rows[idx]["message"]), bytes.fromhex(rows[idx]["aux_rand"])
         jobs.append((mm, compute_nonce(dd, mm, aux), dd, BigUintFHE.new(dd, ck)))
     fn = lambda: Schnorr().sign_fhe_with_k0_batch(jobs, ck, COMPAT)  # noqa: E731
+elif op == "sign":  # sign_fhe_with_k0, BIP-340 vector 0 (fused column form)
+    from fhe_sign import Schnorr, compute_nonce
+    d0, msg0 = 3, bytes(32)
+    k00 = compute_nonce(d0, msg0, bytes(32))
+    dF0 = BigUintFHE.new(d0, ck)
+    fn = lambda: Schnorr().sign_fhe_with_k0(msg0, k00, d0, dF0, ck, COMPAT)  # noqa: E731
 elif op == "divu32":  # 256-bit / public u32 (the residue split)
     A = FheUint256.try_encrypt(a, ck)
     fn = lambda: (A // 0xC0FFEE01).decrypt(ck)  # noqa: E731
