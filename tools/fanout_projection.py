@@ -8,7 +8,8 @@ the level's whole gather buffer on this GPU (the bytes every rank writes into it
 scatter's read included as a second copy), allgather_link_s = the (W - 1) / W of it each rank receives
 at XGMI_GBS (one 153 GB/s xGMI link: the conservative ring bound) plus COLL_LAT_S per collective.
 projected_rank_s = rank_replay_s + allgather_copy_s + allgather_link_s + host_call_s (the host graph
-build runs on every rank).  emulated_wall_s is NOT a projection: one GPU computing every rank's slice
+build runs on every rank; for the signer, which decrypts inside the call, host_call_s is its wall time
+minus its levels replayed at one rank).  emulated_wall_s is NOT a projection: one GPU computing every rank's slice
 (it grows with the rank count).
 usage: python3 tools/fanout_projection.py [ranks...]   (default 1 2 4 8)"""
 import json
@@ -88,6 +89,7 @@ ops = {
 ref = {"biguint256_mul_compat": [int(x) for x in g["out"]], "biguint256_mul_fast": a * b,
        "sign_fhe_with_k0_v0_compat": s.sign_with_k0(msg, k0, d)}
 rows = []
+host_only = {}
 for W in ranks_list:
     ctx.set_fanout(min_level=257, emulate_ranks=W if W > 1 else 0)
     for name, fn in ops.items():
@@ -113,6 +115,13 @@ for W in ranks_list:
             G, split = e & ~LEVEL_SPLIT, bool(e & LEVEL_SPLIT)
             share.append((G + W - 1) // W if split else G)
         t_rank = replay(share)
+        if name.startswith("sign"):
+            # the signer reads its result on the host (decryption), so t_call holds the GPU levels too:
+            # its host-only part is the call's wall time minus its levels replayed, taken at one rank
+            # (the host work does not depend on the rank count; emulated ranks would inflate it)
+            if W == 1 or name not in host_only:
+                host_only[name] = max(0.0, t_op - t_rank) if W == 1 else t_call
+            t_call = host_only[name]
         split_pbs = sum(e & ~LEVEL_SPLIT for e in log if e & LEVEL_SPLIT)
         nsplit = sum(1 for e in log if e & LEVEL_SPLIT)
         level_bytes = [(e & ~LEVEL_SPLIT) * 2049 * 8 for e in log if e & LEVEL_SPLIT]
