@@ -61,13 +61,14 @@ struct fhe_ctx {
     int ks_kernel = FHE_KS_MFMA;
     // classic throughput kernel (fhe_ctx_set_br_kernel): FHE_BR_AUTO = qy2 (two ciphertexts per workgroup)
     // where its rounds of 1024 (256 CUs x 2 workgroups x 2) fill well -- from kQy2Min bootstraps on, and
-    // from 1024 on when the last round is at least three quarters full -- qy below and between (qy2
+    // above 960 when the last round is more than three quarters full (1012: 7.45 vs 7.9 ms) -- qy below
+    // and between (qy2
     // quantises worse: profiles/r6/qy2_sizes_r6l.txt, qy_qy2_thresh_r6z.txt: 1024 -5 %, 2048 -2 %, 2560
     // even, 1280 / 1536 +19 / +2 %); FHE_BR_QY / _QY2 / _QY4 force one kernel
     int br_kernel = FHE_BR_AUTO;
     static constexpr int kQy2Min = 3072;
     static bool qy2_fills(size_t count) {
-        return count >= (size_t)kQy2Min || (count >= 1024 && (count % 1024 == 0 || count % 1024 > 768));
+        return count >= (size_t)kQy2Min || (count > 960 && (count % 1024 == 0 || count % 1024 > 768));
     }
     int8_t* d_ks_digits = nullptr;  // keyswitch digits workspace
     uint64_t* d_ks_body = nullptr;

@@ -1137,6 +1137,9 @@ struct ColProblem {
     // columns >= hi_from: their own target (a consumer that reads them through a wider input, e.g. the
     // compat chain's prefix sums: radix_mul_many_columns lim_hi)
     uint32_t hi_from = ~0u, lim_hi = 6, max_cnt_hi = 3;
+    // first compression round: at most this many groups per column (0: no cap); the rest of the column
+    // passes to the next round -- shapes the first level to whole rounds of the throughput kernel
+    uint32_t cap0 = 0;
 };
 
 static uint32_t col_degree(const Blocks& c) {
@@ -1161,7 +1164,7 @@ static bool col_live(const Blocks& c) {
 // satisfy that bound -- so a column that is fine on its own but gains a carry part is split in the
 // same round (lo <= 3 + incoming hi <= 3), instead of rippling one column per round afterwards.
 static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
-    for (;;) {
+    for (int round = 0;; ++round) {
         std::vector<PbsItem> items;
         struct Dest {
             size_t pi;
@@ -1198,6 +1201,10 @@ static void compress_columns(Engine& e, std::vector<ColProblem*>& probs) {
                 size_t s = 0, end = c.size();  // unassigned: c[s, end)
                 size_t made = 0;               // groups bootstrapped in this column this round
                 while (s < end) {
+                    if (round == 0 && P.cap0 && made >= P.cap0) {  // capped: the rest waits a round
+                        for (size_t q = s; q < end; ++q) next[pi][k].push_back(c[q]);
+                        break;
+                    }
                     std::vector<Term> g;
                     uint32_t deg = 0, noi = 0;
                     while (s < end && g.size() < (size_t)kMaxTerms) {
@@ -2159,6 +2166,13 @@ std::vector<Blocks> radix_mul_add_columns(Engine& e, const Radix& a, const Radix
     constexpr uint32_t lim = 15;
     probs[0].lim0 = probs[0].lim = lim;
     probs[0].max_cnt = 6;
+    // a product with a narrow factor (<= 16 blocks: columns of <= 16 pairs, mass <= 83) takes at most
+    // four groups per column in its first round: the signer's 128 x 16 block product then compresses
+    // in 1012 / 768 / 256 bootstraps -- one throughput round each -- instead of 1490 / 512 / 256, and 222
+    // fewer in all (sign 48.4 -> 47.1 ms same box, profiles/r6/sign_cap_ab_r6ae.txt)
+    const bool enc_a = !std::all_of(a.blocks.begin(), a.blocks.end(), [](const Block& x) { return x.trivial(); });
+    const bool enc_b = !std::all_of(b.blocks.begin(), b.blocks.end(), [](const Block& x) { return x.trivial(); });
+    if (enc_a && enc_b && std::min(live_len(a), live_len(b)) <= 16u) probs[0].cap0 = 4;
     std::vector<ColProblem*> ptrs{&probs[0]};
     compress_columns(e, ptrs);
     return std::move(probs[0].cols);

@@ -62,6 +62,6 @@ def test_signer_column_form_schedule_budget():
     signer uses (FHE_HOST_STATS_COLUMNS: biguint_mul_add_columns) against the normalized mul-add of the
     reference's call site."""
     pbs, levels = mul_stats(8, 1, 8, COMPAT | STATS_COLUMNS)
-    assert levels <= 4 and pbs <= 6_500, (pbs, levels)
+    assert levels <= 4 and pbs <= 6_200, (pbs, levels)  # r6: 6,132 (first compression round capped)
     pbs_n, levels_n = mul_stats(8, 1, 8, COMPAT)
     assert levels_n > levels and pbs_n > pbs
