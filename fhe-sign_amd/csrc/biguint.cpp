@@ -49,7 +49,8 @@ BigUint biguint_add(Engine& e, const BigUint& A, const BigUint& B, int mode) {
                 for (uint32_t k = 0; k < nb && k < w.nblocks(); ++k) cols[k].push_back(w.blocks[k]);
             }
         }
-        s = radix_propagate_columns(e, std::move(cols), nb);
+        // the product's first-round cap, as radix_mul_add takes it (radix.cpp narrow_cap)
+        s = radix_propagate_columns(e, std::move(cols), nb, A.product_cols ? A.product_cap : B.product_cap);
     } else {
         s = radix_sum(e, {&wa, &wb}, nb);
     }
@@ -146,7 +147,10 @@ static BigUint mul_impl(Engine& e, const BigUint& A, const BigUint& B, int mode,
         auto cols = std::make_shared<std::vector<Blocks>>();
         Radix p = radix_mul_keep_columns(e, wa, wb, (uint32_t)len * kLimbBlocks, cols.get());
         for (size_t i = 0; i < len; ++i) out.digits.push_back(slice(p, (uint32_t)i * kLimbBlocks, kLimbBlocks));
-        if (!cols->empty()) out.product_cols = std::move(cols);
+        if (!cols->empty()) {
+            out.product_cols = std::move(cols);
+            out.product_cap = narrow_cap(wa, wb);
+        }
         return out;
     }
     // result = vec![Enc(0); la + lb]: trivial zeros (decrypt identically to src/biguint.rs:207)

@@ -20,6 +20,7 @@ struct BigUint {
     // released unread (the reference's `k_fhe + (e_fhe * privkey_fhe)`), its normalization is dead
     // work the engine drops at the flush.  Null for every other value.
     std::shared_ptr<const std::vector<Blocks>> product_cols;
+    uint32_t product_cap = 0;  // narrow_cap of the product's factors (the first compression round)
 };
 
 enum BigUintMode : int {

@@ -1706,10 +1706,11 @@ Blocks radix_carry_outs(Engine& e, const std::vector<std::vector<Blocks>>& probl
     return res;
 }
 
-Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks) {
+Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks, uint32_t cap0) {
     std::vector<ColProblem> probs(1);
     probs[0].cols = std::move(cols);
     probs[0].nblocks = nblocks;
+    probs[0].cap0 = cap0;
     return propagate_many(e, probs)[0];
 }
 
@@ -2147,12 +2148,28 @@ std::vector<std::vector<Blocks>> radix_mul_many_columns(Engine& e,
     return res;
 }
 
+// The first-round cap (ColProblem::cap0) for a product of two encrypted operands with a narrow factor
+// (<= 16 blocks: columns of <= 16 pairs): at most four groups per column in the first compression round,
+// the rest of a column waiting a round.  The signer's 128 x 16 block product then compresses in
+// 1012 / 768 / 256 bootstraps -- one throughput round each -- instead of 1490 / 512 / 256, 222 fewer in
+// all (sign 48.4 -> 47.1 ms same box, profiles/r6/sign_cap_ab_r6ae.txt); its normalized form 7381 ->
+// 7155 bootstraps at 12 levels.  Dry schedules of the other ops unchanged or smaller.
+uint32_t narrow_cap(const Radix& a, const Radix& b) {
+    auto enc = [](const Radix& r) {
+        return !std::all_of(r.blocks.begin(), r.blocks.end(), [](const Block& x) { return x.trivial(); });
+    };
+    return enc(a) && enc(b) && std::min(live_len(a), live_len(b)) <= 16u ? 4u : 0u;
+}
+
 Radix radix_mul(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks) {
-    return radix_mul_many(e, {{&a, &b}}, nblocks)[0];
+    std::vector<ColProblem> probs = mul_problems(e, {{&a, &b}}, nblocks, {}, true);
+    probs[0].cap0 = narrow_cap(a, b);
+    return propagate_many(e, probs)[0];
 }
 
 Radix radix_mul_keep_columns(Engine& e, const Radix& a, const Radix& b, uint32_t nblocks, std::vector<Blocks>* cols) {
     std::vector<ColProblem> probs = mul_problems(e, {{&a, &b}}, nblocks, {}, true);
+    probs[0].cap0 = narrow_cap(a, b);
     cols->clear();
     // exact columns only: no Karatsuba split (whose top-level columns may hold value + q 4^N)
     if (std::min(live_len(a), live_len(b)) < kara_min()) *cols = probs[0].cols;
@@ -2166,20 +2183,16 @@ std::vector<Blocks> radix_mul_add_columns(Engine& e, const Radix& a, const Radix
     constexpr uint32_t lim = 15;
     probs[0].lim0 = probs[0].lim = lim;
     probs[0].max_cnt = 6;
-    // a product with a narrow factor (<= 16 blocks: columns of <= 16 pairs, mass <= 83) takes at most
-    // four groups per column in its first round: the signer's 128 x 16 block product then compresses
-    // in 1012 / 768 / 256 bootstraps -- one throughput round each -- instead of 1490 / 512 / 256, and 222
-    // fewer in all (sign 48.4 -> 47.1 ms same box, profiles/r6/sign_cap_ab_r6ae.txt)
-    const bool enc_a = !std::all_of(a.blocks.begin(), a.blocks.end(), [](const Block& x) { return x.trivial(); });
-    const bool enc_b = !std::all_of(b.blocks.begin(), b.blocks.end(), [](const Block& x) { return x.trivial(); });
-    if (enc_a && enc_b && std::min(live_len(a), live_len(b)) <= 16u) probs[0].cap0 = 4;
+    probs[0].cap0 = narrow_cap(a, b);
     std::vector<ColProblem*> ptrs{&probs[0]};
     compress_columns(e, ptrs);
     return std::move(probs[0].cols);
 }
 
 Radix radix_mul_add(Engine& e, const Radix& a, const Radix& b, const Radix& c, uint32_t nblocks) {
-    return radix_mul_many(e, {{&a, &b}}, nblocks, {&c})[0];
+    std::vector<ColProblem> probs = mul_problems(e, {{&a, &b}}, nblocks, {&c}, true);
+    probs[0].cap0 = narrow_cap(a, b);
+    return propagate_many(e, probs)[0];
 }
 
 // ============================================================================ scalar ops

@@ -293,7 +293,10 @@ std::vector<Radix> radix_sum_many(Engine& e, const std::vector<std::vector<const
 std::vector<Radix> radix_sum_lazy(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& xs,
                                   std::vector<Radix*>& refresh);
 // Carry propagation of raw column blocks (each column may hold several blocks).
-Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks);
+Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks, uint32_t cap0 = 0);
+// first-round compression cap for the columns of a * b (4 when both are encrypted and one has <= 16
+// live blocks, else 0; radix.cpp)
+uint32_t narrow_cap(const Radix& a, const Radix& b);
 // The carry out of the top column of each problem (columns already bounded: each a sum <= 6, <= 7 at
 // position 0, of <= 3 blocks), and nothing below it: one state level + the carry-chain nodes that
 // carry depends on.  A clean bit per problem.
