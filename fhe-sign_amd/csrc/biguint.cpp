@@ -50,9 +50,15 @@ BigUint biguint_add(Engine& e, const BigUint& A, const BigUint& B, int mode) {
             }
         }
         // the product's first-round cap, as radix_mul_add takes it (radix.cpp narrow_cap)
-        s = radix_propagate_columns(e, std::move(cols), nb, A.product_cols ? A.product_cap : B.product_cap);
+        auto sc = std::make_shared<std::vector<Blocks>>();
+        s = radix_propagate_columns(e, std::move(cols), nb, A.product_cols ? A.product_cap : B.product_cap, sc.get());
+        out.sum_cols = std::move(sc);  // the compressed columns (before the propagation), as below
     } else {
         s = radix_sum(e, {&wa, &wb}, nb);
+        auto cols = std::make_shared<std::vector<Blocks>>(nb);
+        for (const Radix* w : {&wa, &wb})
+            for (uint32_t k = 0; k < nb && k < w->nblocks(); ++k) (*cols)[k].push_back(w->blocks[k]);
+        out.sum_cols = std::move(cols);
     }
     for (size_t i = 0; i <= max_len; ++i) out.digits.push_back(slice(s, (uint32_t)i * kLimbBlocks, kLimbBlocks));
     return out;

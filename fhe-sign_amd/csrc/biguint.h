@@ -21,6 +21,12 @@ struct BigUint {
     // work the engine drops at the flush.  Null for every other value.
     std::shared_ptr<const std::vector<Blocks>> product_cols;
     uint32_t product_cap = 0;  // narrow_cap of the product's factors (the first compression round)
+    // a sum's column form (biguint_add): cols[j] = both operands' blocks at position j, or, when the
+    // add took a product's columns, those columns compressed (each <= 7) -- value = the digits' value.  fhe_biguint_decrypt reads these and
+    // launches only what they depend on (Engine::flush_for): a sum decrypted and then released unread
+    // -- the reference's `(k_fhe + e_fhe * privkey_fhe).to_biguint(ck)` -- never runs its carry
+    // propagation, which the engine drops as dead before its next recording.  Null otherwise.
+    std::shared_ptr<const std::vector<Blocks>> sum_cols;
 };
 
 enum BigUintMode : int {

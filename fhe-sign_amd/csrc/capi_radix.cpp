@@ -225,6 +225,44 @@ int fhe_radix_trivial(fhe_ctx* c, const uint64_t* words, uint32_t bits, fhe_radi
     return FHE_OK;
 }
 
+// the blocks of a column form, for Engine::flush_for
+static std::vector<const Block*> col_blocks(const std::vector<Blocks>& cols) {
+    std::vector<const Block*> v;
+    for (const Blocks& col : cols)
+        for (const Block& b : col)
+            if (!b.trivial()) v.push_back(&b);
+    return v;
+}
+
+// the value of a column form (sum_j sum cols[j] 4^j mod 4^nblocks): every slot block (lazy entries:
+// their terms) in one download, decrypted on the host.  only_needed: launch just the pending bootstraps
+// the blocks depend on (Engine::flush_for)
+static void decrypt_columns(fhe_ctx* c, const fhe_client_key* ck, const std::vector<Blocks>& cols, uint32_t nblocks,
+                            uint64_t* words, size_t nwords, bool only_needed) {
+    std::vector<const Block*> enc;
+    std::vector<const uint64_t*> keys;
+    std::unordered_set<const uint64_t*> seen;
+    auto want = [&](const Block& b) {
+        if (!seen.insert(b.ptr()).second) return;
+        keys.push_back(b.ptr());
+        enc.push_back(&b);
+    };
+    for (const Blocks& col : cols)
+        for (const Block& b : col) {
+            if (b.trivial()) continue;
+            if (b.lazy())
+                for (const Term& t : *b.lin) want(t.b);
+            else
+                want(b);
+        }
+    std::vector<uint64_t> cts(enc.size() * kBigCt);
+    c->engine->download_many(enc, cts.data(), only_needed);
+    std::unordered_map<const uint64_t*, int64_t> vals;
+    for (size_t i = 0; i < enc.size(); ++i)
+        vals[keys[i]] = (int64_t)decode_block(ck->params, decrypt_phase_big(ck, cts.data() + i * kBigCt));
+    column_value(cols, nblocks, [&](const Block& b) { return vals.at(b.ptr()); }, words, nwords);
+}
+
 // the decoded values of a radix's blocks (carry bits included): trivial blocks as they are, the
 // others downloaded together and decrypted on the host
 static std::vector<uint32_t> decrypt_blocks(fhe_ctx* c, const fhe_client_key* ck, const Radix& r) {
@@ -538,7 +576,10 @@ int fhe_ctx_broadcast_biguint(fhe_ctx* c, fhe_biguint** x, int root) {
     const bool sends = c && (!c->attached() || c->rank == root);
     if (!c || !x || (sends && !*x)) return FHE_ERR_INVALID;
     std::vector<Radix> g;
-    if (sends) g = (*x)->v.digits;
+    if (sends) {
+        g = (*x)->v.digits;
+        (*x)->v.sum_cols.reset();  // the receivers get digits only: every rank decrypts the same way
+    }
     const int rc = bcast_radix_groups(c, root, &g);
     if (rc || (c->attached() && c->rank == root)) return rc;
     for (const Radix& d : g)
@@ -585,6 +626,13 @@ int fhe_biguint_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_biguint*
         return FHE_ERR_INVALID;
     }
     return guarded([&] {
+        if (x->v.sum_cols) {  // a sum: its column form (the digits' carry propagation may stay pending)
+            const uint32_t nb = (uint32_t)*n * kLimbBlocks;
+            std::vector<uint64_t> w((2 * (size_t)nb + 63) / 64);
+            decrypt_columns(c, ck, *x->v.sum_cols, nb, w.data(), w.size(), true);
+            for (size_t i = 0; i < *n; ++i) limbs[i] = (uint32_t)(w[i / 2] >> (32 * (i % 2)));
+            return FHE_OK;
+        }
         // every limb's blocks in one download: limb = sum v_k 4^k mod 2^32
         Radix all;
         for (size_t i = 0; i < *n; ++i) all.blocks.insert(all.blocks.end(), x->v.digits[i].blocks.begin(), x->v.digits[i].blocks.end());
@@ -732,7 +780,8 @@ int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64
                                uint32_t* level_sizes, size_t cap) {
     const bool columns = (mode & FHE_HOST_STATS_COLUMNS) != 0;  // the signer's column form instead
     const bool callsite = (mode & FHE_HOST_CALL_SITE) != 0;    // mul, then add (the product released)
-    mode &= ~(FHE_HOST_STATS_COLUMNS | FHE_HOST_CALL_SITE);
+    const bool dec = (mode & FHE_HOST_DECRYPT_SUM) != 0;       // ... and the sum's decryption launched
+    mode &= ~(FHE_HOST_STATS_COLUMNS | FHE_HOST_CALL_SITE | FHE_HOST_DECRYPT_SUM);
     if (!pbs || !levels || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
     return guarded([&] {
         fhe_ctx c;
@@ -756,7 +805,10 @@ int fhe_host_biguint_mul_stats(size_t la, size_t lb, size_t lk, int mode, uint64
             R = biguint_add(e, make(lk), biguint_mul(e, A, B, mode), mode);
         else
             R = lk ? biguint_mul_add(e, A, B, make(lk), mode) : biguint_mul(e, A, B, mode);
-        e.flush();
+        if (dec && R.sum_cols)
+            e.flush_for(col_blocks(*R.sum_cols));
+        else
+            e.flush();
         *pbs = e.pbs_count;
         *levels = e.levels;
         for (size_t i = 0; level_sizes && i < e.level_log.size() && i < cap; ++i) level_sizes[i] = e.level_log[i];
@@ -846,29 +898,7 @@ int fhe_columns_decrypt(fhe_ctx* c, const fhe_client_key* ck, const fhe_columns*
         return FHE_ERR_INVALID;
     }
     return guarded([&] {
-        // every slot block (lazy entries: their terms) in one download
-        std::vector<const Block*> enc;
-        std::vector<const uint64_t*> keys;
-        std::unordered_set<const uint64_t*> seen;
-        auto want = [&](const Block& b) {
-            if (!seen.insert(b.ptr()).second) return;
-            keys.push_back(b.ptr());
-            enc.push_back(&b);
-        };
-        for (const Blocks& col : x->cols)
-            for (const Block& b : col) {
-                if (b.trivial()) continue;
-                if (b.lazy())
-                    for (const Term& t : *b.lin) want(t.b);
-                else
-                    want(b);
-            }
-        std::vector<uint64_t> cts(enc.size() * kBigCt);
-        c->engine->download_many(enc, cts.data());
-        std::unordered_map<const uint64_t*, int64_t> vals;
-        for (size_t i = 0; i < enc.size(); ++i)
-            vals[keys[i]] = (int64_t)decode_block(ck->params, decrypt_phase_big(ck, cts.data() + i * kBigCt));
-        column_value(x->cols, x->nblocks, [&](const Block& b) { return vals.at(b.ptr()); }, words, nwords);
+        decrypt_columns(c, ck, x->cols, x->nblocks, words, nwords, false);
         return FHE_OK;
     });
 }
@@ -882,7 +912,8 @@ void fhe_columns_destroy(fhe_columns* x) { delete x; }
 int fhe_host_sim_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t lb, const uint32_t* k, size_t lk,
                              int mode, uint32_t* out, size_t cap, size_t* n, uint64_t* pbs, uint64_t* levels) {
     const bool callsite = (mode & FHE_HOST_CALL_SITE) != 0;
-    mode &= ~FHE_HOST_CALL_SITE;
+    const bool dec = (mode & FHE_HOST_DECRYPT_SUM) != 0;
+    mode &= ~(FHE_HOST_CALL_SITE | FHE_HOST_DECRYPT_SUM);
     if ((la && !a) || (lb && !b) || (lk && !k) || !n || (mode != kCompat && mode != kFast)) return FHE_ERR_INVALID;
     return guarded([&] {
         fhe_ctx c;
@@ -900,7 +931,22 @@ int fhe_host_sim_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, si
         const BigUint R = k ? (callsite ? biguint_add(e, make(k, lk), biguint_mul(e, A, B, mode), mode)
                                         : biguint_mul_add(e, A, B, make(k, lk), mode))
                             : biguint_mul(e, A, B, mode);
-        e.flush();
+        if (dec && R.sum_cols) {
+            // what fhe_biguint_decrypt launches for a sum: its columns' closure; their value (the
+            // columns' plaintext shadows) must be the digits' (whose carry propagation stays pending)
+            e.flush_for(col_blocks(*R.sum_cols));
+            const uint32_t nb = (uint32_t)R.digits.size() * kLimbBlocks;
+            std::vector<uint64_t> w((2 * (size_t)nb + 63) / 64), d(w.size(), 0);
+            column_value(*R.sum_cols, nb, [&](const Block& b) { return e.sim_half2(b) / 2; }, w.data(), w.size());
+            for (size_t i = 0; i < R.digits.size(); ++i)
+                for (uint32_t q = 0; q < kLimbBlocks; ++q) {
+                    const uint32_t bit = (uint32_t)(i * 32 + 2 * q);
+                    d[bit / 64] |= (uint64_t)(e.sim_half2(R.digits[i].blocks[q]) / 2) << (bit % 64);
+                }
+            engine_check(w == d, "sim: the sum's column form and its digits differ");
+        } else {
+            e.flush();
+        }
         *n = R.digits.size();
         engine_check(R.digits.size() <= cap || !out, "output buffer too small");
         for (size_t i = 0; out && i < R.digits.size(); ++i) {

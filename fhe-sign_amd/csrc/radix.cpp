@@ -324,6 +324,7 @@ Blocks Engine::run(std::vector<PbsItem>& items) {
     if (gpu.empty()) return out;
     engine_check(host_mode_ != kHostFold, "host-only engine: an item needs a bootstrap (encrypted input)");
 
+    settle();  // nodes a partial flush left behind that were released since (flush_for)
     // register LUTs, allocate destinations, record pending nodes
     const uint64_t delta = p.delta();
     std::vector<TermExt> terms;
@@ -469,6 +470,76 @@ void Engine::flush_tail(size_t k0) {
     restore();
 }
 
+// flush() of the pending nodes `blocks` depend on (their ancestor closure); the others stay pending,
+// their reads of launched nodes resolved.  Dead nodes are swept first (over the whole graph: a value
+// released since the last flush); a closure that is the whole graph is a plain flush.
+void Engine::flush_for(const std::vector<const Block*>& blocks) {
+    if (pending_.empty() || gstats_) return flush();
+    sweep_dead();
+    const size_t N = pending_.size();
+    std::vector<uint8_t> need(N, 0);
+    std::vector<int32_t> stack;
+    auto mark = [&](const Block& b) {
+        if (b.slot && b.slot->node >= 0 && (size_t)b.slot->node < N && !need[b.slot->node]) {
+            need[b.slot->node] = 1;
+            stack.push_back((int32_t)b.slot->node);
+        }
+    };
+    for (const Block* b : blocks) {
+        if (b->lazy())
+            for (const Term& t : *b->lin) mark(t.b);
+        else
+            mark(*b);
+    }
+    size_t n_need = stack.size();
+    while (!stack.empty()) {
+        const int32_t k = stack.back();
+        stack.pop_back();
+        for (int32_t d : pending_[k].deps)
+            if (!need[d]) {
+                need[d] = 1;
+                ++n_need;
+                stack.push_back(d);
+            }
+    }
+    if (n_need == N) return flush();
+    if (n_need == 0) return run_before_launch();
+    // split in recording order; the closure reads nothing outside itself
+    std::vector<int32_t> idx(N);
+    std::vector<Pending> sub, keep;
+    sub.reserve(n_need);
+    keep.reserve(N - n_need);
+    int32_t ns = 0, nk = 0;
+    for (size_t k = 0; k < N; ++k) idx[k] = need[k] ? ns++ : nk++;
+    for (size_t k = 0; k < N; ++k) {
+        Pending& n = pending_[k];
+        std::vector<int32_t> deps;
+        for (int32_t d : n.deps) {
+            if (need[k]) {
+                engine_check(need[d], "closure reads a node outside it");
+                deps.push_back(idx[d]);
+            } else if (!need[d]) {
+                deps.push_back(idx[d]);  // a launched producer's output is ready: no dependency
+            }
+        }
+        n.deps = std::move(deps);
+        n.hold[0]->node = idx[k];
+        (need[k] ? sub : keep).push_back(std::move(n));
+    }
+    pending_ = std::move(sub);
+    const bool eager = eager_ok_;
+    try {
+        flush();
+    } catch (...) {
+        for (auto& n : keep) n.hold[0]->node = -1;  // abandoned with the error (they read the closure)
+        throw;
+    }
+    pending_ = std::move(keep);
+    eager_ok_ = eager;
+    sweep_next_ = true;
+    recount();
+}
+
 // Level schedule of a dependency graph (deps[i]: earlier nodes node i reads).  Returns the nodes of
 // each launch level, in order; the level count is the critical path.  mode 0: backward list
 // scheduling (default), 1: forward deadline-driven; levels are filled to multiples of `round`
@@ -558,6 +629,84 @@ void Engine::run_before_launch() {
     f();
 }
 
+void Engine::recount() {
+    pending_dependent_ = 0;
+    pending_depth_ = 0;
+    for (Pending& n : pending_) {
+        n.depth = 1;
+        for (int32_t d : n.deps) n.depth = std::max(n.depth, pending_[d].depth + 1);
+        if (!n.deps.empty()) ++pending_dependent_;
+        pending_depth_ = std::max(pending_depth_, n.depth);
+    }
+}
+
+void Engine::sweep_dead() {
+    // Dead nodes: an output slot referenced by nothing but its own node (no later node reads it, no
+    // block of the program holds it -- e.g. a carry-chain state whose every consumer folded to a
+    // constant on the host) can never be read, so the node is dropped; newest first, so dropping a
+    // node releases its inputs and can make their producers dead in turn.
+    // The output counts come from host reference counts, i.e. from how long the caller keeps its
+    // handles: under a real communicator the ranks could disagree (one rank still holding an
+    // intermediate), and every rank must schedule the same levels (the split, the chunk and the
+    // all-gather size all follow from them).  So the ranks agree first: a node is dropped only if it
+    // is dead on EVERY rank (one byte-wise min all-reduce).  The result is closed under the cascade --
+    // a node kept on some rank keeps its producers' outputs referenced on that rank.
+    const size_t N0 = pending_.size();
+    std::vector<int32_t> remap(N0, -1);
+    std::vector<uint8_t> dead(N0, 0);
+    {
+        // count the references without releasing any: refs[k] = holders of node k's output slot
+        std::vector<long> refs(N0);
+        for (size_t k = 0; k < N0; ++k) refs[k] = pending_[k].hold[0].use_count();
+        for (size_t k = N0; k-- > 0;) {
+            if (refs[k] != 1) continue;
+            dead[k] = 1;
+            for (size_t h = 1; h < pending_[k].hold.size(); ++h) {
+                const int64_t prod = pending_[k].hold[h]->node;
+                if (prod >= 0) --refs[prod];
+            }
+        }
+    }
+    // Only a real multi-rank communicator needs the agreement (the collective is rank-uniform: every
+    // rank takes this branch or none does); at world size 1 it would only drain the stream.
+    if (ctx_->attached() && ctx_->nranks > 1) {
+        const int rc = ctx_->allreduce_min_u8(dead.data(), N0);
+        if (rc != FHE_OK) throw EngineError(rc, std::string("dead-node agreement: ") + last_error());
+    }
+    for (size_t k = N0; k-- > 0;)
+        if (dead[k]) pending_[k].hold.clear();
+    size_t live = 0;
+    for (size_t k = 0; k < N0; ++k)
+        if (!dead[k]) remap[k] = (int32_t)live++;
+    if (live < N0) {
+        dead_nodes += N0 - live;
+        std::vector<Pending> kept;
+        kept.reserve(live);
+        if (gstats_ && in_key_.size() == N0) {
+            size_t o = 0;
+            for (size_t k = 0; k < N0; ++k)
+                if (!dead[k]) {
+                    in_key_[o] = std::move(in_key_[k]);
+                    in_deg_[o++] = in_deg_[k];
+                }
+            in_key_.resize(o);
+            in_deg_.resize(o);
+        }
+        for (size_t k = 0; k < N0; ++k) {
+            if (dead[k]) continue;
+            Pending& n = pending_[k];
+            for (int32_t& d : n.deps) {
+                engine_check(remap[d] >= 0, "live node reads a dropped node");
+                d = remap[d];
+            }
+            n.hold[0]->node = remap[k];
+            kept.push_back(std::move(n));
+        }
+        pending_.swap(kept);
+    }
+    recount();  // the survivors' counters (their producers may have been launched by flush_for)
+}
+
 void Engine::flush() {
     run_before_launch();  // a deferred upload lands before anything that could read it is launched
     if (pending_.empty()) return;
@@ -570,76 +719,13 @@ void Engine::flush() {
         g_pool_grows = 0;
         g_pool_grow_ns = 0.0;
     }
-    // Dead nodes: an output slot referenced by nothing but its own node (no later node reads it, no
-    // block of the program holds it -- e.g. a carry-chain state whose every consumer folded to a
-    // constant on the host) can never be read, so the node is dropped; newest first, so dropping a
-    // node releases its inputs and can make their producers dead in turn.
-    // The output counts come from host reference counts, i.e. from how long the caller keeps its
-    // handles: under a real communicator the ranks could disagree (one rank still holding an
-    // intermediate), and every rank must schedule the same levels (the split, the chunk and the
-    // all-gather size all follow from them).  So the ranks agree first: a node is dropped only if it
-    // is dead on EVERY rank (one byte-wise min all-reduce).  The result is closed under the cascade --
-    // a node kept on some rank keeps its producers' outputs referenced on that rank.
-    {
-        const size_t N0 = pending_.size();
-        std::vector<int32_t> remap(N0, -1);
-        std::vector<uint8_t> dead(N0, 0);
-        {
-            // count the references without releasing any: refs[k] = holders of node k's output slot
-            std::vector<long> refs(N0);
-            for (size_t k = 0; k < N0; ++k) refs[k] = pending_[k].hold[0].use_count();
-            for (size_t k = N0; k-- > 0;) {
-                if (refs[k] != 1) continue;
-                dead[k] = 1;
-                for (size_t h = 1; h < pending_[k].hold.size(); ++h) {
-                    const int64_t prod = pending_[k].hold[h]->node;
-                    if (prod >= 0) --refs[prod];
-                }
-            }
-        }
-        // Only a real multi-rank communicator needs the agreement (the collective is rank-uniform: every
-        // rank takes this branch or none does); at world size 1 it would only drain the stream.
-        if (ctx_->attached() && ctx_->nranks > 1) {
-            const int rc = ctx_->allreduce_min_u8(dead.data(), N0);
-            if (rc != FHE_OK) throw EngineError(rc, std::string("dead-node agreement: ") + last_error());
-        }
-        for (size_t k = N0; k-- > 0;)
-            if (dead[k]) pending_[k].hold.clear();
-        size_t live = 0;
-        for (size_t k = 0; k < N0; ++k)
-            if (!dead[k]) remap[k] = (int32_t)live++;
-        if (live < N0) {
-            dead_nodes += N0 - live;
-            std::vector<Pending> kept;
-            kept.reserve(live);
-            if (gstats_ && in_key_.size() == N0) {
-                size_t o = 0;
-                for (size_t k = 0; k < N0; ++k)
-                    if (!dead[k]) {
-                        in_key_[o] = std::move(in_key_[k]);
-                        in_deg_[o++] = in_deg_[k];
-                    }
-                in_key_.resize(o);
-                in_deg_.resize(o);
-            }
-            for (size_t k = 0; k < N0; ++k) {
-                if (dead[k]) continue;
-                Pending& n = pending_[k];
-                for (int32_t& d : n.deps) {
-                    engine_check(remap[d] >= 0, "live node reads a dropped node");
-                    d = remap[d];
-                }
-                n.hold[0]->node = remap[k];
-                kept.push_back(std::move(n));
-            }
-            pending_.swap(kept);
-        }
-        if (pending_.empty()) {
-            pending_dependent_ = 0;
+    sweep_next_ = false;
+    sweep_dead();
+    if (pending_.empty()) {
+        pending_dependent_ = 0;
         pending_depth_ = 0;
-            eager_ok_ = true;
-            return;
-        }
+        eager_ok_ = true;
+        return;
     }
     const size_t N = pending_.size();
     std::vector<std::vector<int32_t>> deps(N);
@@ -785,7 +871,7 @@ void Engine::flush() {
     for (auto& n : pending_) n.hold[0]->node = -1;
     pending_.clear();  // the stream orders any later reuse of the held slots behind these launches
     pending_dependent_ = 0;
-        pending_depth_ = 0;
+    pending_depth_ = 0;
     eager_ok_ = true;
 }
 
@@ -955,11 +1041,15 @@ void Engine::download(const Block& b, uint64_t* ct) {
     wait_check(ctx_, "download");
 }
 
-void Engine::download_many(const std::vector<const Block*>& blocks, uint64_t* cts) {
+void Engine::download_many(const std::vector<const Block*>& blocks, uint64_t* cts, bool only_needed) {
     const size_t n = blocks.size();
     if (n == 0) return;
-    if (n == 1) return download(*blocks[0], cts);
-    flush();
+    if (only_needed)
+        flush_for(blocks);
+    else if (n == 1)
+        return download(*blocks[0], cts);
+    else
+        flush();
     const size_t words = n * kBigCt + n;  // gathered ciphertexts, then the slot pointers
     if (words > up_cap_) {
         hip_check(hipStreamSynchronize(ctx_->stream), "download sync");
@@ -1706,12 +1796,15 @@ Blocks radix_carry_outs(Engine& e, const std::vector<std::vector<Blocks>>& probl
     return res;
 }
 
-Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks, uint32_t cap0) {
+Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks, uint32_t cap0,
+                              std::vector<Blocks>* compressed) {
     std::vector<ColProblem> probs(1);
     probs[0].cols = std::move(cols);
     probs[0].nblocks = nblocks;
     probs[0].cap0 = cap0;
-    return propagate_many(e, probs)[0];
+    Radix r = propagate_many(e, probs)[0];
+    if (compressed) *compressed = std::move(probs[0].cols);  // compress_columns left them in place
+    return r;
 }
 
 std::vector<Radix> radix_sum_many(Engine& e, const std::vector<std::vector<const Radix*>>& xs,

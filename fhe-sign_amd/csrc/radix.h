@@ -165,6 +165,11 @@ public:
     Blocks run(std::vector<PbsItem>& items);
     // Schedules and launches every pending bootstrap (asynchronously on the context's stream).
     void flush();
+    // Schedules and launches only the pending bootstraps the given blocks (lazy ones: their terms)
+    // depend on; the rest stay pending with their dependencies on the launched ones resolved (a
+    // decryption that reads a value's column form leaves the value's normalization pending -- dead,
+    // and dropped before the next recording, once the caller releases the value).
+    void flush_for(const std::vector<const Block*>& blocks);
     // Linear combination without bootstrap (caller guarantees degree/noise stay legal).
     Block lincomb(const std::vector<Term>& terms, uint32_t cst);
     // Upload client-encrypted blocks.
@@ -180,7 +185,8 @@ public:
     void download(const Block& b, uint64_t* ct);
     // the slot blocks' ciphertexts -> host, contiguous (one gather + one copy + one wait instead of a
     // round trip per block: the decryption of a 256-bit result is 128-144 blocks)
-    void download_many(const std::vector<const Block*>& blocks, uint64_t* cts);
+    // (only_needed: flush_for(blocks) instead of flush())
+    void download_many(const std::vector<const Block*>& blocks, uint64_t* cts, bool only_needed = false);
     // n big LWEs contiguous in device memory -> fresh slots (one scatter); degree/noise set by the caller
     Blocks adopt_device(const uint64_t* d_cts, size_t n);
     // the slot blocks' ciphertexts -> contiguous device buffer (one gather; flushes first)
@@ -188,7 +194,10 @@ public:
     void sync();
     static constexpr size_t kEagerHead = 3072;  // 4 rounds of the throughput kernel (3 x 256 CUs)
     // nothing pending and no eager batch since the last flush (radix_mul_many's early head launch)
-    bool eager_head_ok() const { return eager_ok_ && pending_.empty(); }
+    bool eager_head_ok() {
+        settle();
+        return eager_ok_ && pending_.empty();
+    }
     // one-shot, before each program of a batch of independent programs recorded back to back
     // (fhe_schnorr_sign_fhe_with_k0_batch): the program's first large batch of bootstraps that reads
     // nothing pending (its block products) is launched as soon as it is recorded
@@ -248,6 +257,16 @@ private:
     void ensure_desc(size_t n);
     void graph_stats(const std::vector<std::vector<int32_t>>& deps);
     void flush_tail(size_t k0);
+    // drop the dead pending nodes (flush's first step; ranks agree by an all-reduce)
+    void sweep_dead();
+    void recount();  // pending_dependent_ / pending_depth_ / depths from pending_'s deps
+    bool sweep_next_ = false;  // flush_for left nodes pending: sweep them before the next recording
+    void settle() {
+        if (sweep_next_) {
+            sweep_next_ = false;
+            sweep_dead();
+        }
+    }
     PbsDesc* stage_desc(size_t n, PbsDesc** dev);
 };
 
@@ -293,7 +312,10 @@ std::vector<Radix> radix_sum_many(Engine& e, const std::vector<std::vector<const
 std::vector<Radix> radix_sum_lazy(Engine& e, const std::vector<std::pair<const Radix*, const Radix*>>& xs,
                                   std::vector<Radix*>& refresh);
 // Carry propagation of raw column blocks (each column may hold several blocks).
-Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks, uint32_t cap0 = 0);
+// (compressed: if set, the columns after compression, before the carry propagation -- same value mod
+// 4^nblocks, each column <= 7)
+Radix radix_propagate_columns(Engine& e, std::vector<Blocks> cols, uint32_t nblocks, uint32_t cap0 = 0,
+                              std::vector<Blocks>* compressed = nullptr);
 // first-round compression cap for the columns of a * b (4 when both are encrypted and one has <= 16
 // live blocks, else 0; radix.cpp)
 uint32_t narrow_cap(const Radix& a, const Radix& b);

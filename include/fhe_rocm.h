@@ -354,6 +354,10 @@ int fhe_host_biguint_mul(const uint32_t* a, size_t la, const uint32_t* b, size_t
  * reference's call site k + (a * b) as two ops -- fhe_biguint_mul, then fhe_biguint_add with the product
  * released before the flush -- instead of the one-call mul-add. */
 #define FHE_HOST_CALL_SITE 0x200
+/* mode | FHE_HOST_CALL_SITE | FHE_HOST_DECRYPT_SUM: the call site followed by fhe_biguint_decrypt of the
+ * sum, which reads the sum's column form and launches only what that depends on -- the statistics stop
+ * there (the sum's own carry propagation stays pending; the sim checks the columns' value = the digits'). */
+#define FHE_HOST_DECRYPT_SUM 0x400
 /* The same dry run's recording-order fingerprint: a hash of every scheduled level's nodes in order (LUT,
  * coefficients, constants, producers by recording index; no addresses).  The multi-GPU fan-out needs it
  * equal on every rank: ranks scatter the all-gathered slices by their own node order. */

@@ -192,6 +192,40 @@ def test_sign_fhe_with_k0_vector0_limb_flow(keys):
     assert s.to_biguint(ck) % R.N == int(v["s"], 16)
 
 
+def test_sum_decrypted_from_its_columns(keys):
+    """fhe_biguint_decrypt of a sum reads the sum's column form and launches only what that depends on
+    (Engine::flush_for): the sum's own carry propagation stays pending -- run when the sum is used again
+    (its digits, a further add), dropped as dead before the next recording once the sum is released."""
+    ck, ctx = keys
+    v = json.load(open(os.path.join(G, "sign_vectors.json")))["vectors"][0]
+    e, d, k = _big(ck, v["e"]), _big(ck, v["d"]), _big(ck, v["k"])
+    s = k + e * d  # exact 8 x 1 product: the add takes its columns (compressed ones decrypted)
+    assert s.decrypt_limbs(ck) == v["sum"]
+    assert s.to_biguint(ck) % R.N == int(v["s"], 16)
+    t = s + k  # the pending propagation of s feeds a further add
+    assert t.decrypt_limbs(ck) == R.biguint_add(v["sum"], v["k"])
+    assert [x.decrypt(ck) for x in s.digits] == v["sum"]  # the digits themselves (a full flush)
+    rng = random.Random(0x5C01)
+    al, bl = R.to_u32_digits(rng.getrandbits(256)), R.to_u32_digits(rng.getrandbits(224))
+    a, b = _big(ck, al), _big(ck, bl)
+    p0, _ = stats(ctx)
+    assert (a + b).decrypt_limbs(ck) == R.biguint_add(al, bl)
+    assert stats(ctx)[0] == p0  # the operands' own blocks: nothing launched
+    # released after the decryption: its propagation never runs -- the next op launches its own
+    # bootstraps only (as many as the same op on a clean engine)
+    counts = []
+    for _ in range(2):
+        x = a + b
+        assert x.decrypt_limbs(ck) == R.biguint_add(al, bl)
+        del x
+        p1, _ = stats(ctx)
+        assert (a * d).decrypt_limbs(ck) == R.biguint_mul(al, v["d"])
+        counts.append(stats(ctx)[0] - p1)
+    p2, _ = stats(ctx)
+    assert (a * d).decrypt_limbs(ck) == R.biguint_mul(al, v["d"])
+    assert counts == [stats(ctx)[0] - p2] * 2
+
+
 def test_biguint_mul_add_equals_mul_then_add(keys):
     """fhe_biguint_mul_add (the signer's FHE block k + e*d' in one schedule) gives the limbs of
     add(k, mul(a, b)) of src/biguint.rs in both modes: exact 8x1 (k enters the product columns), the

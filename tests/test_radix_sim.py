@@ -198,6 +198,43 @@ def test_call_site_mul_then_add_simulated(mode):
     assert stats(mode | CALL_SITE) == stats(mode)
 
 
+DECRYPT_SUM = 0x400  # FHE_HOST_DECRYPT_SUM
+
+
+@pytest.mark.parametrize("mode", [COMPAT, FAST])
+def test_call_site_decrypt_reads_the_sums_columns(mode):
+    """fhe_biguint_decrypt of a sum (the call site's `(k_fhe + e_fhe * privkey_fhe).to_biguint`) reads the
+    sum's column form (BigUint::sum_cols) and launches only what that depends on (Engine::flush_for): the
+    sim checks the columns' value against the digits' at that point, and the schedule is the product's
+    alone -- the add's carry propagation stays pending (dead once the sum is released).  An add that
+    took an exact product's columns (vector 0's 8 x 1 + 8) decrypts those columns compressed: the
+    one-call column form's schedule (FHE_HOST_STATS_COLUMNS) plus at most one compression level."""
+    rng = random.Random(23 + mode)
+    for la, lb, lk in [(8, 8, 8), (8, 1, 8), (1, 8, 8), (2, 3, 1), (3, 1, 5), (1, 1, 3)]:
+        a, b, k = _limbs(rng, la), _limbs(rng, lb), _limbs(rng, lk)
+        got = sim_mul(a, b, mode | CALL_SITE | DECRYPT_SUM, k)
+        assert R.from_limbs(got) == R.from_limbs(k) + R.from_limbs(sim_mul(a, b, mode)), (la, lb, lk)
+    full = [M32 - 1] * 8
+    for b in ([M32 - 1], full):
+        got = sim_mul(full, b, mode | CALL_SITE | DECRYPT_SUM, full)
+        assert R.from_limbs(got) == R.from_limbs(full) + R.from_limbs(sim_mul(full, b, mode))
+    lib = _lib.load()
+
+    def stats(la, lb, lk, m):
+        p, lev = C.c_uint64(), C.c_uint64()
+        assert lib.fhe_host_biguint_mul_stats(la, lb, lk, m, C.byref(p), C.byref(lev), None, 0) == 0, lib.fhe_last_error()
+        return p.value, lev.value
+
+    if mode == COMPAT:  # the chain's limbs: no product columns, the add is a plain sum
+        lazy, full = stats(8, 8, 8, mode | CALL_SITE | DECRYPT_SUM), stats(8, 8, 8, mode | CALL_SITE)
+        assert lazy == stats(8, 8, 0, mode)
+        assert lazy[1] < full[1] and lazy[0] < full[0]
+    lazy, full = stats(8, 1, 8, mode | CALL_SITE | DECRYPT_SUM), stats(8, 1, 8, mode | CALL_SITE)
+    fused = stats(8, 1, 8, mode | 0x100)  # FHE_HOST_STATS_COLUMNS
+    assert lazy[1] < full[1] and lazy[0] < full[0]
+    assert lazy[1] <= fused[1] + 1 and lazy[0] <= fused[0] * 1.06
+
+
 def sim_mul_add_columns(a, b, k, mode):
     A = (C.c_uint32 * max(1, len(a)))(*a)
     B = (C.c_uint32 * max(1, len(b)))(*b)
