@@ -472,9 +472,13 @@ void Engine::flush_tail(size_t k0) {
 
 // flush() of the pending nodes `blocks` depend on (their ancestor closure); the others stay pending,
 // their reads of launched nodes resolved.  Dead nodes are swept first (over the whole graph: a value
-// released since the last flush); a closure that is the whole graph is a plain flush.
+// released since the last flush); a closure that is the whole graph is a plain flush.  One rank only:
+// under a communicator (or emulated ranks) it is a plain flush -- what it leaves pending could only be
+// swept by a collective, and a rank-local read (a broadcast's root, one rank's decryption) that found
+// pending work would then run one collective on its own rank.
 void Engine::flush_for(const std::vector<const Block*>& blocks) {
-    if (pending_.empty() || gstats_) return flush();
+    if (pending_.empty() || gstats_ || ctx_->fanout_world() > 1 || (ctx_->attached() && ctx_->nranks > 1))
+        return flush();
     sweep_dead();
     const size_t N = pending_.size();
     std::vector<uint8_t> need(N, 0);
