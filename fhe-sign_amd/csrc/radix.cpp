@@ -531,15 +531,14 @@ void Engine::flush_for(const std::vector<const Block*>& blocks) {
         (need[k] ? sub : keep).push_back(std::move(n));
     }
     pending_ = std::move(sub);
-    const bool eager = eager_ok_;
     try {
-        flush();
+        flush();  // a host read, like a full flush: the next program's first large batch may launch
+                  // eagerly (eager_ok_), once whatever stays pending has been swept as dead
     } catch (...) {
         for (auto& n : keep) n.hold[0]->node = -1;  // abandoned with the error (they read the closure)
         throw;
     }
     pending_ = std::move(keep);
-    eager_ok_ = eager;
     sweep_next_ = true;
     recount();
 }
